@@ -1,0 +1,238 @@
+"""PerformantNet1 + Worker.fwd_bkwd + the server step, restated on torch-CPU -- TEST INFRASTRUCTURE.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module.
+
+  PerformantNet1Ref    models.py:11-25 (layer construction order => identical default init under
+                       torch.manual_seed) and models.py:27-47 (forward) with dropout masks injected
+                       from the build's Philox spec instead of torch's RNG
+  fwd_bkwd             agents.py:32-40 (forward, CrossEntropyLoss mean, backward accumulating into
+                       the shared .grad, returns the loss)
+  OracleSim            main.py:126-188: per-epoch worker loop (schedule from oracle.schedule),
+                       aggregation rule main.py:23-25 (oracle.cascade_mean == torch stack-mean),
+                       Central.update_model agents.py:9-21 (oracle.adam_step == torch Adam)
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import oracle as O
+
+PARAM_NAMES = [
+    "conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias", "conv3.weight", "conv3.bias",
+    "conv4.weight", "conv4.bias", "conv5.weight", "conv5.bias", "conv6.weight", "conv6.bias",
+    "linear1.weight", "linear1.bias", "linear2.weight", "linear2.bias", "linear3.weight",
+    "linear3.bias",
+]
+
+# NCHW shapes (per sample) at the five dropout sites, models.py:32,36,40,43,45
+DROPOUT_SHAPES = [(48, 18, 18), (96, 11, 11), (192, 7, 7), (512,), (256,)]
+
+
+class PerformantNet1Ref(nn.Module):
+    """Same parameter set and construction order as models.py:13-25."""
+
+    def __init__(self):
+        super().__init__()
+        self.conv1 = nn.Conv2d(3, 48, 3, padding=(2, 2))
+        self.conv2 = nn.Conv2d(48, 48, 3, padding=(2, 2))
+        self.conv3 = nn.Conv2d(48, 96, 3, padding=(2, 2))
+        self.conv4 = nn.Conv2d(96, 96, 3, padding=(2, 2))
+        self.conv5 = nn.Conv2d(96, 192, 3, padding=(2, 2))
+        self.conv6 = nn.Conv2d(192, 192, 3, padding=(2, 2))
+        self.linear1 = nn.Linear(9408, 512)
+        self.linear2 = nn.Linear(512, 256)
+        self.linear3 = nn.Linear(256, 10)
+
+
+def init_params(seed=0):
+    """torch default init of PerformantNet1 under torch.manual_seed(seed) -> flat fp32 numpy."""
+    torch.manual_seed(seed)
+    m = PerformantNet1Ref()
+    return torch.cat([p.detach().reshape(-1) for _, p in m.named_parameters()]).numpy().copy()
+
+
+def param_shapes():
+    m = PerformantNet1Ref()
+    return [(n, tuple(p.shape)) for n, p in m.named_parameters()]
+
+
+SHAPES = None
+
+
+def _shapes():
+    global SHAPES
+    if SHAPES is None:
+        SHAPES = param_shapes()
+    return SHAPES
+
+
+def split_flat(flat):
+    """flat numpy/torch vector -> list of per-tensor views (named_parameters order)."""
+    out, off = [], 0
+    for _, shp in _shapes():
+        n = int(np.prod(shp))
+        out.append(flat[off:off + n].reshape(shp))
+        off += n
+    return out
+
+
+def dropout_noise(seed, t, worker, nsamples, dtype=torch.float32):
+    """The five noise tensors (keep * fp32(1/(1-p))) for one worker-step, NCHW."""
+    res = []
+    for site, p, shp in zip(O.SITE_DROPOUT, O.DROPOUT_P, DROPOUT_SHAPES):
+        numel = nsamples * int(np.prod(shp))
+        keep = O.dropout_keep(seed, t, worker, site, p, numel)
+        noise = torch.from_numpy(keep).reshape((nsamples,) + shp).to(torch.float32).div_(1 - p)
+        res.append(noise.to(dtype))
+    return res
+
+
+def forward(params, x, noise):
+    """models.py:27-47 with dropout = x * noise (noise None -> eval mode / dropout off)."""
+    (w1, b1, w2, b2, w3, b3, w4, b4, w5, b5, w6, b6, l1w, l1b, l2w, l2b, l3w, l3b) = params
+    bs = x.shape[0]
+    d = (lambda h, i: h) if noise is None else (lambda h, i: h * noise[i])
+    h = F.relu(F.conv2d(x, w1, b1, padding=2))
+    h = F.relu(F.conv2d(h, w2, b2, padding=2))
+    h = d(F.max_pool2d(h, 2, 2), 0)
+    h = F.relu(F.conv2d(h, w3, b3, padding=2))
+    h = F.relu(F.conv2d(h, w4, b4, padding=2))
+    h = d(F.max_pool2d(h, 2, 2), 1)
+    h = F.relu(F.conv2d(h, w5, b5, padding=2))
+    h = F.relu(F.conv2d(h, w6, b6, padding=2))
+    h = d(F.max_pool2d(h, 2, 2), 2)
+    h = h.reshape(bs, -1)
+    h = d(F.relu(F.linear(h, l1w, l1b)), 3)
+    h = d(F.relu(F.linear(h, l2w, l2b)), 4)
+    return F.linear(h, l3w, l3b)
+
+
+def fwd_bkwd(params, x, y, noise):
+    """agents.py:32-40: loss = CE(mean) ; backward() accumulates into p.grad ; returns loss."""
+    pred = forward(params, x, noise)
+    loss = F.cross_entropy(pred, y)
+    loss.backward()
+    return loss.detach()
+
+
+class OracleSim:
+    """main.py:126-188 restated on CPU, reference (torch>=2 aliasing) or torch1 semantics."""
+
+    def __init__(self, n, delay=None, delays=None, throttle=False, seed=0, dtype=torch.float32,
+                 semantics="reference", dropout=True, pool=None, lr=1e-3, theta0=None,
+                 max_throttle=32):
+        self.n = n
+        self.delays = np.asarray(delays if delays is not None else O.reference_delays(n, delay),
+                                 np.int32)
+        self.throttle = bool(throttle)
+        self.seed = seed
+        self.dtype = dtype
+        self.semantics = semantics
+        self.dropout = dropout
+        self.lr = lr
+        self.max_throttle = max_throttle
+        imgs, labels = pool if pool is not None else O.make_pool(seed)
+        self.imgs, self.labels = imgs, labels
+        self.lists = O.class_lists(labels)
+        self.lut = O.normalize_lut()
+        theta0 = O_init(seed) if theta0 is None else theta0
+        self.theta = np.ascontiguousarray(theta0, np.float32).copy()
+        self.m = np.zeros_like(self.theta)
+        self.v = np.zeros_like(self.theta)
+        self.step_count = 0
+        self.rs = np.random.RandomState(seed)   # main.py:138 global numpy RNG stream
+        self.t = 0
+        self.ring = {}                           # epoch -> S (stale entries kept alive)
+        self.window = 0
+        self.gone = False
+        self.fifo = {i: [] for i in range(n) if self.delays[i] != 0}
+        self.trace = []
+
+    # ---- data (main.py:138-142) ----
+    def batch(self, t, i, k, dtype=None):
+        idx = O.batch_indices(self.seed, t, i, k, self.n, self.lists)
+        x = self.lut[self.imgs[idx]]                      # [128,3,32,32] fp32
+        y = self.labels[idx]
+        dt = dtype or self.dtype
+        return torch.from_numpy(x).to(dt), torch.from_numpy(y)
+
+    def grad_of(self, theta_np, items, dtype=None):
+        """Sum over `items` [(t, i, k)] of per-worker mean-CE gradients at theta (in order)."""
+        dt = dtype or self.dtype
+        params = [torch.tensor(a, dtype=dt, requires_grad=True)
+                  for a in split_flat(theta_np.astype(np.float64 if dt == torch.float64
+                                                      else np.float32))]
+        losses = []
+        for (t, i, k) in items:
+            x, y = self.batch(t, i, k, dt)
+            noise = dropout_noise(self.seed, t, i, x.shape[0], dt) if self.dropout else None
+            losses.append(float(fwd_bkwd(params, x, y, noise)))
+        g = torch.cat([p.grad.reshape(-1) for p in params]).numpy()
+        return g, losses
+
+    # ---- one epoch (main.py:126-188) ----
+    def epoch(self):
+        t, n = self.t, self.n
+        ks = self.rs.randint(0, n, size=n)
+        items, fast_losses_idx, appended = [], [], []
+        for i in range(n):
+            if self.delays[i] != 0:
+                self.gone = False
+                d = abs(int(self.delays[i]))
+                popped = None
+                if t == 0:
+                    items.append((t, i, int(ks[i])))
+                    self.fifo[i].append(t)
+                elif t % d == 0:
+                    items.append((t, i, int(ks[i])))
+                    self.fifo[i].append(t)
+                    popped = self.fifo[i].pop(0)
+                if popped is not None:
+                    appended.append(("stale", popped))
+                    self.gone = True
+            else:
+                if self.window <= 0:
+                    fast_losses_idx.append(len(items))
+                    items.append((t, i, int(ks[i])))
+                    appended.append(("fast", t))
+                    if self.throttle:
+                        self.window = 1
+                        if not self.gone:
+                            self.window = min(self.window * 2, self.max_throttle)
+            if self.window > 0:
+                self.window -= 1
+        if not appended:
+            raise IndexError("list index out of range")   # rule(): ups_list[0] (main.py:25)
+        S, losses = self.grad_of(self.theta, items)
+        S = S.astype(np.float32)
+        entries = []
+        for kind, src in appended:
+            if kind == "fast":
+                entries.append(S)
+            else:
+                entries.append(self.ring.pop(src) if self.semantics == "reference"
+                               else np.zeros_like(S))
+        if any(self.delays[i] != 0 and (t == 0 or t % abs(int(self.delays[i])) == 0)
+               for i in range(n)):
+            self.ring[t] = S
+        g = np.empty_like(S)
+        off = 0
+        for _, shp in _shapes():                          # rule() is per parameter tensor
+            nel = int(np.prod(shp))
+            g[off:off + nel] = O.cascade_mean([e[off:off + nel] for e in entries])
+            off += nel
+        self.step_count += 1
+        O.adam_step(self.theta, self.m, self.v, g, self.step_count, lr=self.lr)
+        mean_loss = float(np.mean(np.asarray([losses[j] for j in fast_losses_idx], np.float32)))\
+            if fast_losses_idx else float("nan")
+        self.trace.append(dict(t=t, items=items, appended=appended, loss=mean_loss))
+        self.t += 1
+        self.last_S, self.last_g = S, g
+        return mean_loss
+
+
+def O_init(seed):
+    return init_params(seed)

@@ -1,0 +1,162 @@
+"""The oracle (CPU restatement) against golden vectors produced by the reference itself.
+
+tests/golden/make_golden.py ran the reference's own main.py loop / rule() / Central.update_model /
+Worker.fwd_bkwd in the build container; these tests pin oracle/ to those outputs.
+"""
+import hashlib
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from oracle import model_ref as MR
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).digest()
+
+
+def _schedule_keys(g):
+    return sorted({re.match(r"(n\d+_d\d+_thr\d_e\d+)_", k).group(1) for k in g.files})
+
+
+def _parse(key):
+    n, d, thr, ep = re.match(r"n(\d+)_d(\d+)_thr(\d)_e(\d+)", key).groups()
+    return int(n), int(d), int(thr), int(ep)
+
+
+def test_schedule_bit_exact(golden):
+    g = golden.schedule
+    keys = _schedule_keys(g)
+    assert len(keys) == 40
+    for key in keys:
+        n, d, thr, ep = _parse(key)
+        s = O.schedule(n, O.reference_delays(n, d), thr, ep)
+        assert s.rc == 0
+        assert np.array_equal(np.packbits(s.computes, axis=1), g[key + "_computes"]), key
+        assert np.array_equal(s.c_t, g[key + "_c_t"]), key
+        stale = s.stale_src[:, n - 1]
+        assert np.array_equal(stale, g[key + "_stale"]), key
+        assert np.array_equal(s.s_t, (g[key + "_stale"] >= 0).astype(np.int32)), key
+        fw, fg = g[key + "_final"]
+        assert s.window_end[-1] == fw and s.gone_end[-1] == fg, key
+
+
+def test_worker_k_sequence(golden):
+    g = golden.schedule
+    for key in _schedule_keys(g):
+        n, _, _, ep = _parse(key)
+        ks = O.worker_k_sequence(0, n, ep)
+        assert np.array_equal(ks[:3], g[key + "_k_head"]), key
+        assert _sha(ks.astype(np.int64)) == g[key + "_k_sha"].tobytes(), key
+
+
+def test_cascade_mean_bit_exact(golden):
+    g = golden.cascade
+    n = 0
+    for key in g.files:
+        kind, k, P = key.split("_")
+        k, P = int(k[1:]), int(P[1:])
+        rs = np.random.RandomState(1000 * k + P)
+        S = rs.standard_normal(P).astype(np.float32)
+        st = rs.standard_normal(P).astype(np.float32)
+        if kind == "rep":
+            out = O.cascade_mean([S] * (k - 1) + [st])
+        else:
+            ent = rs.standard_normal((k, P)).astype(np.float32)
+            out = O.cascade_mean(list(ent))
+        assert np.array_equal(out.view(np.uint32), g[key].view(np.uint32)), key
+        n += 1
+    assert n >= 90
+
+
+def test_adam_teacher_forced(golden):
+    """m, v bit-exact; p within 1 ulp of the update on <0.5% of elements (torch CPU sqrt is
+    MKL-VML, not correctly rounded; the oracle's sqrt is, like the GPU kernel's)."""
+    g = golden.adam
+    for j in range(3):
+        p = g[f"p0_{j}"].copy()
+        m = np.zeros_like(p)
+        v = np.zeros_like(p)
+        for step in range(1, 11):
+            if step > 1:
+                p = g[f"p{step - 1}_{j}"].copy()
+                m = g[f"m{step - 1}_{j}"].copy()
+                v = g[f"v{step - 1}_{j}"].copy()
+            p0 = p.copy()
+            O.adam_step(p, m, v, g[f"g{step}_{j}"].copy(), step)
+            assert np.array_equal(m.view(np.uint32), g[f"m{step}_{j}"].view(np.uint32))
+            assert np.array_equal(v.view(np.uint32), g[f"v{step}_{j}"].view(np.uint32))
+            ref = g[f"p{step}_{j}"]
+            diff = p != ref
+            assert diff.mean() <= 0.005
+            upd = np.abs(ref.astype(np.float64) - p0)
+            assert np.all(np.abs(p.astype(np.float64) - ref)[diff] <=
+                          np.spacing(np.abs(ref[diff])) + 2 ** -22 * upd[diff] + 1e-12)
+
+
+def test_pool_and_data_spec():
+    meta = json.load(open(os.path.join(GOLDEN, "meta.json")))
+    imgs, labels = O.make_pool(0)
+    assert hashlib.sha256(imgs.tobytes()).hexdigest() == meta["pool_sha"]
+    a, b = O.class_lists(labels)
+    assert len(a) == 40000 and len(b) == 10000
+    assert set(labels[b]) == {1, 9}
+
+
+def _stats_close(st, ref, rtol, atol=0.0):
+    # [sum, sumsq, min, max]
+    return np.allclose(st, ref, rtol=rtol, atol=atol)
+
+
+def test_single_worker_grad(golden):
+    g = golden.grad
+    imgs, labels = O.make_pool(0)
+    lists = O.class_lists(labels)
+    sim = MR.OracleSim(4, delay=2, pool=(imgs, labels))
+    x, y = sim.batch(0, 0, 0)
+    assert _sha(x.numpy()) == g["f32_x_sha"].tobytes()
+    grad, losses = sim.grad_of(sim.theta, [(0, 0, 0)])
+    assert abs(losses[0] - float(g["f32_loss"])) < 1e-6
+    off = 0
+    samp = []
+    for (_, shp) in MR._shapes():
+        n = int(np.prod(shp))
+        a = grad[off:off + n].astype(np.float64)
+        off += n
+        rs = np.random.RandomState(123 + n)
+        idx = np.arange(n) if n <= 256 else np.sort(rs.choice(n, 256, replace=False))
+        samp.append(a[idx])
+    samp = np.concatenate(samp)
+    np.testing.assert_allclose(samp, g["f32_samp"], rtol=1e-4, atol=1e-7)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("thr", [0, 1])
+def test_training_trajectory(golden, thr):
+    g = golden.train
+    key = f"n4_d2_thr{thr}_f32"
+    imgs, labels = O.make_pool(0)
+    sim = MR.OracleSim(4, delay=2, throttle=bool(thr), pool=(imgs, labels))
+    assert _sha(sim.theta) == g[key + "_theta0_sha"].tobytes()
+    ref_losses = g[key + "_losses"]
+    for t in range(len(ref_losses)):
+        loss = sim.epoch()
+        assert abs(loss - ref_losses[t]) <= 1e-5, (t, loss, ref_losses[t])
+        n_entries, n_distinct = g[f"{key}_comp{t}"]
+        assert len(sim.trace[-1]["appended"]) == n_entries
+        ts = []
+        off = 0
+        for (_, shp) in MR._shapes():
+            n = int(np.prod(shp))
+            a = sim.theta[off:off + n].astype(np.float64)
+            off += n
+            ts.append([a.sum(), (a * a).sum(), a.min(), a.max()])
+        np.testing.assert_allclose(np.asarray(ts)[:, 1], g[f"{key}_theta{t}_stats"][:, 1],
+                                   rtol=1e-3)  # Adam amplifies 1-ulp sqrt diffs
