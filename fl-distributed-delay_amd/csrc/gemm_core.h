@@ -1,0 +1,170 @@
+// fp32 MFMA GEMM core for gfx950 (v_mfma_f32_16x16x4_f32), LDS-tiled, register-staged
+// double buffer, one barrier per 16-deep K step.
+//
+// C[m][n] = sum_k A[m][k] * B[k][n]; each operand is produced by a Loader that knows the
+// implicit-GEMM address math (im2col for convolutions, plain rows for the linear layers) and
+// which LDS orientation it uses:
+//   KC ("k-contiguous"): LDS tile [rows][16] (64-B rows, 16-B chunks XOR-swizzled so that the
+//       ds_read_b128 fragment reads of 16 distinct rows are bank-conflict free)
+//   KM ("k-major"):      LDS tile [16][rows + 4] (row stride = 4 mod 8 floats: the two 16-lane
+//       halves of a ds_read_b32 land on disjoint banks)
+//
+// MFMA operand mapping (16x16x4 f32): lane l holds A[i = l&15][kslot = l>>4] and
+// B[kslot = l>>4][j = l&15]. For one 16-deep K step a lane owns k = 4*(l>>4) + j, j = 0..3, and
+// MFMA j consumes element j of that 4-vector, so A and B agree on which k each slot holds.
+// C/D: col = l&15, row = 4*(l>>4) + reg.
+#pragma once
+#include "common.h"
+
+namespace flsim {
+
+constexpr int GK = 16;  // K depth per LDS stage
+
+__device__ __forceinline__ int kc_swz(int row) { return (4 - ((row >> 2) & 3)) & 3; }
+
+// byte-free helpers for LDS addressing (float units)
+template <int ROWS>
+struct KCTile {
+    static constexpr int FLOATS = ROWS * GK;
+    __device__ static inline int chunk_off(int row, int chunk) {
+        return row * GK + 4 * (chunk ^ kc_swz(row));
+    }
+};
+template <int ROWS>
+struct KMTile {
+    static constexpr int STRIDE = ROWS + 4;
+    static constexpr int FLOATS = GK * STRIDE;
+};
+
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// Read one operand fragment (16 rows x 4 k per lane) for rows [r0, r0+16).
+template <bool KC, int ROWS>
+__device__ __forceinline__ f32x4 read_frag(const float* lds, int r0, int lane) {
+    if constexpr (KC) {
+        const int row = r0 + (lane & 15);
+        return *reinterpret_cast<const f32x4*>(lds + KCTile<ROWS>::chunk_off(row, lane >> 4));
+    } else {
+        constexpr int S = KMTile<ROWS>::STRIDE;
+        const int col = r0 + (lane & 15);
+        const int k0 = 4 * (lane >> 4);
+        f32x4 v;
+        v.x = lds[(k0 + 0) * S + col];
+        v.y = lds[(k0 + 1) * S + col];
+        v.z = lds[(k0 + 2) * S + col];
+        v.w = lds[(k0 + 3) * S + col];
+        return v;
+    }
+}
+
+// Store a staged vec4 unit into the LDS tile.
+//   KC: unit = (row, chunk) holding k = 4*chunk..4*chunk+3 of that row
+//   KM: unit = (krow, col4) holding rows krow, cols 4*col4..4*col4+3
+template <bool KC, int ROWS>
+__device__ __forceinline__ void store_unit(float* lds, int a, int b, f32x4 v) {
+    if constexpr (KC) {
+        *reinterpret_cast<f32x4*>(lds + KCTile<ROWS>::chunk_off(a, b)) = v;
+    } else {
+        *reinterpret_cast<f32x4*>(lds + a * KMTile<ROWS>::STRIDE + 4 * b) = v;
+    }
+}
+
+template <bool KC, int ROWS>
+constexpr int tile_floats() {
+    if constexpr (KC) return KCTile<ROWS>::FLOATS;
+    else return KMTile<ROWS>::FLOATS;
+}
+
+// Loader concept (all device functions):
+//   static constexpr bool KC; static constexpr int ROWS; static constexpr int UNITS;
+//   void setup(int tile_row0, int tid)           -- per-thread precompute (rows fixed per tile)
+//   void load(int kstep, f32x4 (&r)[UNITS])      -- global loads of the K step into registers
+//   void store(float* lds, const f32x4 (&r)[UNITS])
+//
+// Epilogue concept:  void operator()(int m, int n, float v)   (m, n global; bounds checked inside)
+//                    or apply4(m0, n, f32x4) for 4 consecutive rows of one column.
+
+template <int FM, int FN, int WAVES_M, int WAVES_N, class AL, class BL, class EPI>
+__global__ void __launch_bounds__(64 * WAVES_M * WAVES_N)
+gemm_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split) {
+    constexpr int BM = 16 * FM * WAVES_M;
+    constexpr int BN = 16 * FN * WAVES_N;
+    static_assert(AL::ROWS == BM, "A loader rows != BM");
+    static_assert(BL::ROWS == BN, "B loader rows != BN");
+    constexpr int A_FL = tile_floats<AL::KC, BM>();
+    constexpr int B_FL = tile_floats<BL::KC, BN>();
+    __shared__ __attribute__((aligned(16))) float lds[2 * (A_FL + B_FL)];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wm = wave / WAVES_N;
+    const int wn = wave % WAVES_N;
+    const int m0 = blockIdx.x * BM;
+    const int n0 = blockIdx.y * BN;
+    const int ks0 = blockIdx.z * ksteps_per_split;
+    int ks1 = ks0 + ksteps_per_split;
+    if (ks1 > ksteps_total) ks1 = ksteps_total;
+
+    al.setup(m0, tid);
+    bl.setup(n0, tid);
+
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    f32x4 ra[AL::UNITS];
+    f32x4 rb[BL::UNITS];
+    constexpr int BUF = A_FL + B_FL;
+
+    if (ks0 < ks1) {
+        al.load(ks0, ra);
+        bl.load(ks0, rb);
+        al.store(lds, ra);
+        bl.store(lds + A_FL, rb);
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int ks = ks0; ks < ks1; ++ks) {
+        const bool more = ks + 1 < ks1;
+        if (more) {
+            al.load(ks + 1, ra);
+            bl.load(ks + 1, rb);
+        }
+        const float* A = lds + cur * BUF;
+        const float* B = A + A_FL;
+        f32x4 af[FM], bf[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) af[i] = read_frag<AL::KC, BM>(A, wm * 16 * FM + 16 * i, lane);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bf[j] = read_frag<BL::KC, BN>(B, wn * 16 * FN + 16 * j, lane);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(af[i][kk], bf[j][kk], acc[i][j]);
+        if (more) {
+            al.store(lds + (cur ^ 1) * BUF, ra);
+            bl.store(lds + (cur ^ 1) * BUF + A_FL, rb);
+        }
+        __syncthreads();
+        cur ^= 1;
+    }
+
+    // epilogue: lane holds rows 4*(lane>>4)+r, col lane&15 of each 16x16 tile
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+            const int m = m0 + wm * 16 * FM + 16 * i + 4 * (lane >> 4);
+            const int n = n0 + wn * 16 * FN + 16 * j + (lane & 15);
+            epi.apply4(m, n, acc[i][j]);
+        }
+}
+
+}  // namespace flsim

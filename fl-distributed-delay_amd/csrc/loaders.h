@@ -1,0 +1,294 @@
+// Operand loaders and epilogues for gemm_kernel (gemm_core.h).
+#pragma once
+#include "gemm_core.h"
+
+namespace flsim {
+
+__device__ __forceinline__ f32x4 ldg4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+__device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+
+// ---------------------------------------------------------------------------------------------
+// A operand of a 3x3 / stride-1 convolution run as implicit GEMM (forward, or data-gradient as
+// a "valid" convolution of dZ with the flipped weights).  Rows = output pixels m = (n, oh, ow);
+// k = (kh*3 + kw) * CI + ci (CI >= 16 and a multiple of 16, or CI == 4 for the padded input).
+// Input X is NHWC.  Output spatial OH = IH + 2*PAD - 2.
+// ---------------------------------------------------------------------------------------------
+template <int IH, int IW, int CI, int PAD, int TR, int NT>
+struct Im2colKC {
+    static constexpr int ROWS = TR;
+    static constexpr bool KC = true;
+    static constexpr int OH = IH + 2 * PAD - 2;
+    static constexpr int OW = IW + 2 * PAD - 2;
+    static constexpr int TOTAL = ROWS * 4;
+    static constexpr int UNITS = (TOTAL + NT - 1) / NT;
+    static_assert(NT % 4 == 0, "");
+    static_assert(CI == 4 || CI % 16 == 0, "");
+
+    const float* X;
+    int M;
+    int base[UNITS];
+    short oh[UNITS], ow[UNITS];
+    short row[UNITS];
+    int q;
+
+    __device__ void setup(int m0, int tid) {
+        q = tid & 3;
+#pragma unroll
+        for (int j = 0; j < UNITS; ++j) {
+            const int u = tid + j * NT;
+            const int r = u >> 2;
+            row[j] = (short)r;
+            const int m = m0 + r;
+            if (u < TOTAL && m < M) {
+                const int nimg = m / (OH * OW);
+                const int rem = m - nimg * (OH * OW);
+                oh[j] = (short)(rem / OW);
+                ow[j] = (short)(rem - (rem / OW) * OW);
+                base[j] = nimg * (IH * IW * CI);
+            } else {
+                base[j] = -1;
+                oh[j] = 0;
+                ow[j] = 0;
+            }
+        }
+    }
+    __device__ void load(int ks, f32x4 (&r)[UNITS]) const {
+        const int k = ks * GK + 4 * q;
+        const int khkw = k / CI;
+        const int ci = k - khkw * CI;
+        const int kh = khkw / 3;
+        const int kw = khkw - kh * 3;
+#pragma unroll
+        for (int j = 0; j < UNITS; ++j) {
+            const int ih = oh[j] + kh - PAD;
+            const int iw = ow[j] + kw - PAD;
+            const bool ok = base[j] >= 0 && khkw < 9 && (unsigned)ih < (unsigned)IH &&
+                            (unsigned)iw < (unsigned)IW;
+            r[j] = ok ? ldg4(X + base[j] + (ih * IW + iw) * CI + ci) : zero4();
+        }
+    }
+    __device__ void store(float* lds, const f32x4 (&r)[UNITS]) const {
+#pragma unroll
+        for (int j = 0; j < UNITS; ++j)
+            if (TOTAL % NT == 0 || row[j] < ROWS) store_unit<true, ROWS>(lds, row[j], q, r[j]);
+    }
+};
+
+// ---------------------------------------------------------------------------------------------
+// Row-major matrix whose rows are the tile rows and whose reduction index is contiguous (KC):
+// element (row, k) at P[row * ld + k].  Rows >= NR read as zero.  K must be a multiple of 16.
+// ---------------------------------------------------------------------------------------------
+template <int TR, int NT>
+struct RowsKC {
+    static constexpr int ROWS = TR;
+    static constexpr bool KC = true;
+    static constexpr int TOTAL = ROWS * 4;
+    static constexpr int UNITS = (TOTAL + NT - 1) / NT;
+    static_assert(NT % 4 == 0, "");
+    const float* P;
+    long ld;
+    int NR;
+    const float* rowp[UNITS];
+    short row[UNITS];
+    int q;
+    __device__ void setup(int r0, int tid) {
+        q = tid & 3;
+#pragma unroll
+        for (int j = 0; j < UNITS; ++j) {
+            const int u = tid + j * NT;
+            const int r = u >> 2;
+            row[j] = (short)r;
+            rowp[j] = (u < TOTAL && r0 + r < NR) ? P + (long)(r0 + r) * ld + 4 * q : nullptr;
+        }
+    }
+    __device__ void load(int ks, f32x4 (&r)[UNITS]) const {
+#pragma unroll
+        for (int j = 0; j < UNITS; ++j) r[j] = rowp[j] ? ldg4(rowp[j] + ks * GK) : zero4();
+    }
+    __device__ void store(float* lds, const f32x4 (&r)[UNITS]) const {
+#pragma unroll
+        for (int j = 0; j < UNITS; ++j)
+            if (TOTAL % NT == 0 || row[j] < ROWS) store_unit<true, ROWS>(lds, row[j], q, r[j]);
+    }
+};
+
+// ---------------------------------------------------------------------------------------------
+// Row-major matrix whose ROWS are the reduction index (KM): element (k, col) at P[k * ld + col];
+// the tile spans columns [c0, c0 + ROWS).  k >= NK or col >= NC read as zero (NC % 4 == 0).
+// ---------------------------------------------------------------------------------------------
+template <int TR, int NT>
+struct RowsKM {
+    static constexpr int ROWS = TR;
+    static constexpr bool KC = false;
+    static constexpr int C4 = ROWS / 4;
+    static constexpr int TOTAL = GK * C4;
+    static constexpr int UNITS = (TOTAL + NT - 1) / NT;
+    const float* P;
+    long ld;
+    int NK;
+    int NC;
+    int c_off[UNITS];
+    short krow[UNITS], c4[UNITS];
+    __device__ void setup(int c0, int tid) {
+#pragma unroll
+        for (int j = 0; j < UNITS; ++j) {
+            const int u = tid + j * NT;
+            krow[j] = (short)(u / C4);
+            c4[j] = (short)(u % C4);
+            const int col = c0 + 4 * (u % C4);
+            c_off[j] = (u < TOTAL && col < NC) ? col : -1;
+        }
+    }
+    __device__ void load(int ks, f32x4 (&r)[UNITS]) const {
+#pragma unroll
+        for (int j = 0; j < UNITS; ++j) {
+            const int k = ks * GK + krow[j];
+            r[j] = (c_off[j] >= 0 && k < NK) ? ldg4(P + (long)k * ld + c_off[j]) : zero4();
+        }
+    }
+    __device__ void store(float* lds, const f32x4 (&r)[UNITS]) const {
+#pragma unroll
+        for (int j = 0; j < UNITS; ++j)
+            if (TOTAL % NT == 0 || krow[j] < GK) store_unit<false, ROWS>(lds, krow[j], c4[j], r[j]);
+    }
+};
+
+// ---------------------------------------------------------------------------------------------
+// B operand of the weight gradient: im2col(X) with the pixel as the reduction index (KM).
+// Tile columns = kk = (kh*3 + kw) * CI + ci in [c0, c0 + ROWS); reduction rows = pixels p.
+// ---------------------------------------------------------------------------------------------
+template <int IH, int IW, int CI, int PAD, int TR, int NT>
+struct Im2colKM {
+    static constexpr int ROWS = TR;
+    static constexpr bool KC = false;
+    static constexpr int OH = IH + 2 * PAD - 2;
+    static constexpr int OW = IW + 2 * PAD - 2;
+    static constexpr int C4 = ROWS / 4;
+    static constexpr int TOTAL = GK * C4;
+    static constexpr int UNITS = (TOTAL + NT - 1) / NT;
+    const float* X;
+    int M;  // total pixels
+    int coff[UNITS];   // ci, or -1 when the column is padding / out of range
+    short kh[UNITS], kw[UNITS];
+    short krow[UNITS], c4[UNITS];
+    __device__ void setup(int c0, int tid) {
+#pragma unroll
+        for (int j = 0; j < UNITS; ++j) {
+            const int u = tid + j * NT;
+            krow[j] = (short)(u / C4);
+            c4[j] = (short)(u % C4);
+            const int kk = c0 + 4 * (u % C4);
+            const int khkw = kk / CI;
+            const int ci = kk - khkw * CI;
+            kh[j] = (short)(khkw / 3);
+            kw[j] = (short)(khkw % 3);
+            coff[j] = (u < TOTAL && khkw < 9) ? ci : -1;
+        }
+    }
+    __device__ void load(int ks, f32x4 (&r)[UNITS]) const {
+#pragma unroll
+        for (int j = 0; j < UNITS; ++j) {
+            const int p = ks * GK + krow[j];
+            f32x4 v = zero4();
+            if (coff[j] >= 0 && p < M) {
+                const int nimg = p / (OH * OW);
+                const int rem = p - nimg * (OH * OW);
+                const int oh = rem / OW;
+                const int ow = rem - oh * OW;
+                const int ih = oh + kh[j] - PAD;
+                const int iw = ow + kw[j] - PAD;
+                if ((unsigned)ih < (unsigned)IH && (unsigned)iw < (unsigned)IW)
+                    v = ldg4(X + ((long)nimg * IH * IW + ih * IW + iw) * CI + coff[j]);
+            }
+            r[j] = v;
+        }
+    }
+    __device__ void store(float* lds, const f32x4 (&r)[UNITS]) const {
+#pragma unroll
+        for (int j = 0; j < UNITS; ++j)
+            if (TOTAL % NT == 0 || krow[j] < GK) store_unit<false, ROWS>(lds, krow[j], c4[j], r[j]);
+    }
+};
+
+// ---------------------------------------------------------------------------------------------
+// Epilogues
+// ---------------------------------------------------------------------------------------------
+// conv forward: Y[m][n] = relu(acc + bias[n])  (NHWC, row length N)
+struct EpiBiasRelu {
+    float* Y;
+    const float* bias;
+    int M, N;
+    __device__ void apply4(int m, int n, f32x4 v) const {
+        if (n >= N) return;
+        const float b = bias[n];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (m + r < M) Y[(long)(m + r) * N + n] = fmaxf(v[r] + b, 0.f);
+    }
+};
+
+// data gradient: Y[m][n] = acc * (act[m][n] > 0)  (MASK) or acc
+template <bool MASK>
+struct EpiMask {
+    float* Y;
+    const float* act;
+    int M, N;
+    __device__ void apply4(int m, int n, f32x4 v) const {
+        if (n >= N) return;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (m + r < M) {
+                const long o = (long)(m + r) * N + n;
+                float x = v[r];
+                if (MASK) x = act[o] > 0.f ? x : 0.f;
+                Y[o] = x;
+            }
+    }
+};
+
+// gradient of a dropout(relu(.)) output: Y = acc * scale * (act > 0)  (act = dropped output)
+struct EpiDropMask {
+    float* Y;
+    const float* act;
+    float scale;
+    int M, N;
+    __device__ void apply4(int m, int n, f32x4 v) const {
+        if (n >= N) return;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (m + r < M) {
+                const long o = (long)(m + r) * N + n;
+                Y[o] = act[o] > 0.f ? v[r] * scale : 0.f;
+            }
+    }
+};
+
+// split-K partial slab, accumulated across chunks: S[z][m][n] += acc   (one owner per element)
+struct EpiSlabAcc {
+    float* S;
+    int M, N;
+    long zstride;
+    __device__ void apply4(int m, int n, f32x4 v) const {
+        if (n >= N) return;
+        float* base = S + blockIdx.z * zstride;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (m + r < M) base[(long)(m + r) * N + n] += v[r];
+    }
+};
+
+// split-K partial, overwritten: S[z][m][n] = acc
+struct EpiSlabStore {
+    float* S;
+    int M, N;
+    long zstride;
+    __device__ void apply4(int m, int n, f32x4 v) const {
+        if (n >= N) return;
+        float* base = S + blockIdx.z * zstride;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (m + r < M) base[(long)(m + r) * N + n] = v[r];
+    }
+};
+
+}  // namespace flsim

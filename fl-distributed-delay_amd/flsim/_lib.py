@@ -1,0 +1,87 @@
+"""ctypes binding of libflsim.so (the C-ABI declared in include/flsim.h).
+
+The library is built in-tree by `make -C fl-distributed-delay_amd` (or __graft_entry__.build()).
+torch is imported first so that libflsim.so binds to the HIP runtime torch already loaded
+(same soname libamdhip64.so.7).  There is no fallback: a missing library raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must be loaded before libflsim.so, see module docstring)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libflsim.so")
+
+EXPORTS = [
+    "flsim_last_error", "flsim_sched_create", "flsim_sched_destroy", "flsim_sched_epoch",
+    "flsim_sched_state", "flsim_pn1_param_count", "flsim_pn1_gradstate_bytes",
+    "flsim_pn1_workspace_bytes", "flsim_pn1_workspace_offset", "flsim_pn1_begin_epoch",
+    "flsim_pn1_fwd_bwd_chunk", "flsim_pn1_fwd_bwd_input", "flsim_pn1_end_epoch",
+    "flsim_aggregate_adam",
+]
+
+
+class FLSimError(RuntimeError):
+    pass
+
+
+class WorkerRec(ctypes.Structure):
+    _fields_ = [("t", ctypes.c_uint32), ("i", ctypes.c_uint32), ("k", ctypes.c_uint32),
+                ("pad", ctypes.c_uint32)]
+
+
+_L = None
+vp = ctypes.c_void_p
+
+
+def lib():
+    global _L
+    if _L is not None:
+        return _L
+    if not os.path.exists(LIB_PATH):
+        raise FLSimError(f"{LIB_PATH} not built: run `make -C fl-distributed-delay_amd` "
+                         "(no CPU fallback exists)")
+    L = ctypes.CDLL(LIB_PATH)
+    L.flsim_last_error.restype = ctypes.c_char_p
+    L.flsim_sched_create.restype = vp
+    L.flsim_sched_create.argtypes = [ctypes.c_int32, vp, ctypes.c_int32, ctypes.c_int32]
+    L.flsim_sched_destroy.argtypes = [vp]
+    L.flsim_sched_epoch.argtypes = [vp] * 6
+    L.flsim_sched_state.argtypes = [vp, vp]
+    L.flsim_pn1_param_count.restype = ctypes.c_long
+    L.flsim_pn1_gradstate_bytes.restype = ctypes.c_long
+    L.flsim_pn1_workspace_bytes.restype = ctypes.c_long
+    L.flsim_pn1_workspace_bytes.argtypes = [ctypes.c_int]
+    L.flsim_pn1_workspace_offset.argtypes = [ctypes.c_int, ctypes.c_int, vp]
+    L.flsim_pn1_begin_epoch.argtypes = [vp, vp, vp]
+    L.flsim_pn1_fwd_bwd_chunk.argtypes = [
+        vp, vp, ctypes.c_int, vp, vp, vp, vp, ctypes.c_int, vp, ctypes.c_int, vp, vp,
+        ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, vp, vp]
+    L.flsim_pn1_fwd_bwd_input.argtypes = [
+        vp, vp, ctypes.c_int, vp, vp, vp, ctypes.c_int, vp, ctypes.c_uint64, ctypes.c_int,
+        ctypes.c_int, vp, vp]
+    L.flsim_pn1_end_epoch.argtypes = [vp, vp, vp]
+    L.flsim_aggregate_adam.argtypes = [
+        vp, ctypes.c_int, vp, ctypes.c_int, vp, vp, vp, ctypes.c_long, vp, ctypes.c_int,
+        ctypes.c_long, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp]
+    _L = L
+    return L
+
+
+def check(rc):
+    if rc != 0:
+        msg = lib().flsim_last_error().decode(errors="replace")
+        if rc == 1:
+            if "IndexError" in msg:
+                raise IndexError(msg)
+            raise ValueError(msg)
+        raise FLSimError(msg)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def stream_ptr(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

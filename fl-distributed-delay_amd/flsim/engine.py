@@ -1,0 +1,109 @@
+"""PerformantNet1 engine: device buffers + the C-ABI calls of one epoch.
+
+  begin_epoch(theta)      pack theta_t, zero the gradient slabs        (start of main.py:126)
+  run_chunk(...)          worker-batched fwd/bwd of a chunk of workers (agents.py:32-40, xN)
+  end_epoch(S)            S_t = sum of the epoch's gradients           (agents.py:35 accumulation)
+  aggregate_adam(...)     fused rule() + Central.update_model          (main.py:23-25,184,188)
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from ._lib import WorkerRec, check, lib, ptr, stream_ptr
+
+# named_parameters() order of models.py:PerformantNet1 (models.py:13-25)
+PN1_SHAPES = [
+    ("conv1.weight", (48, 3, 3, 3)), ("conv1.bias", (48,)),
+    ("conv2.weight", (48, 48, 3, 3)), ("conv2.bias", (48,)),
+    ("conv3.weight", (96, 48, 3, 3)), ("conv3.bias", (96,)),
+    ("conv4.weight", (96, 96, 3, 3)), ("conv4.bias", (96,)),
+    ("conv5.weight", (192, 96, 3, 3)), ("conv5.bias", (192,)),
+    ("conv6.weight", (192, 192, 3, 3)), ("conv6.bias", (192,)),
+    ("linear1.weight", (512, 9408)), ("linear1.bias", (512,)),
+    ("linear2.weight", (256, 512)), ("linear2.bias", (256,)),
+    ("linear3.weight", (10, 256)), ("linear3.bias", (10,)),
+]
+PN1_SIZES = [int(np.prod(s)) for _, s in PN1_SHAPES]
+SAMPLES_PER_WORKER = 128
+
+
+def padded(n, q=64):
+    return (n + q - 1) // q * q
+
+
+def split_views(flat):
+    out, off = [], 0
+    for (_, shp), n in zip(PN1_SHAPES, PN1_SIZES):
+        out.append(flat[off:off + n].view(shp))
+        off += n
+    return out
+
+
+class PN1Engine:
+    def __init__(self, device, chunk_workers=32):
+        L = lib()
+        self.device = torch.device(device)
+        self.P = int(L.flsim_pn1_param_count())
+        assert self.P == sum(PN1_SIZES)
+        self.chunk_workers = int(chunk_workers)
+        self.max_samples = self.chunk_workers * SAMPLES_PER_WORKER
+        self.gradstate = torch.empty(int(L.flsim_pn1_gradstate_bytes()), dtype=torch.uint8,
+                                     device=self.device)
+        self.workspace = torch.empty(int(L.flsim_pn1_workspace_bytes(self.max_samples)),
+                                     dtype=torch.uint8, device=self.device)
+        self.sizes = (ctypes.c_long * len(PN1_SIZES))(*PN1_SIZES)
+
+    # -- per-epoch gradient --------------------------------------------------------------------
+    def begin_epoch(self, theta):
+        check(lib().flsim_pn1_begin_epoch(ptr(self.gradstate), ptr(theta), stream_ptr()))
+
+    def run_chunk(self, theta, pool, workers_dev, n_chunk, n_workers_total, seed, dropout,
+                  loss_out, backward=True):
+        check(lib().flsim_pn1_fwd_bwd_chunk(
+            ptr(self.gradstate), ptr(self.workspace), self.max_samples, ptr(theta),
+            ptr(pool.imgs), ptr(pool.labels), ptr(pool.list_a), int(pool.list_a.numel()),
+            ptr(pool.list_b), int(pool.list_b.numel()), ptr(pool.lut), ptr(workers_dev),
+            int(n_chunk), int(n_workers_total), ctypes.c_uint64(seed), int(bool(dropout)),
+            int(bool(backward)), ptr(loss_out), stream_ptr()))
+
+    def run_input(self, theta, x, y, workers_dev, seed, dropout, loss_out, backward=True):
+        x = x.contiguous()
+        y = y.to(torch.int64).contiguous()
+        check(lib().flsim_pn1_fwd_bwd_input(
+            ptr(self.gradstate), ptr(self.workspace), self.max_samples, ptr(theta), ptr(x), ptr(y),
+            int(x.shape[0]), ptr(workers_dev), ctypes.c_uint64(seed), int(bool(dropout)),
+            int(bool(backward)), ptr(loss_out), stream_ptr()))
+
+    def end_epoch(self, grad_out):
+        check(lib().flsim_pn1_end_epoch(ptr(self.gradstate), ptr(grad_out), stream_ptr()))
+
+    def workspace_view(self, which, shape, dtype=torch.float32, samples=None):
+        """Debug view of a workspace tensor (ids: x0 a1 a2 d1 a3 a4 d2 a5 a6 d3 e1 e2 dh1 dh2
+        gx gy loss_s dlog y i1 i2 i3 = 0..21)."""
+        off = ctypes.c_long()
+        check(lib().flsim_pn1_workspace_offset(which, self.max_samples, ctypes.byref(off)))
+        n = int(np.prod(shape)) * torch.tensor([], dtype=dtype).element_size()
+        return self.workspace[off.value:off.value + n].view(dtype).view(shape)
+
+    # -- server step ------------------------------------------------------------------------------
+    def aggregate_adam(self, S, c, stale, theta, m, v, step, lr=1e-3, betas=(0.9, 0.999),
+                       eps=1e-8):
+        """stale: list of device tensors (or None = zero entry)."""
+        ns = len(stale)
+        arr = (ctypes.c_void_p * max(1, ns))(*[(t.data_ptr() if t is not None else None)
+                                               for t in stale])
+        check(lib().flsim_aggregate_adam(
+            ptr(S), int(c), arr, ns, ptr(theta), ptr(m), ptr(v), self.P, self.sizes,
+            len(PN1_SIZES), int(step), float(lr), float(betas[0]), float(betas[1]), float(eps),
+            stream_ptr()))
+
+
+def worker_table(recs, device):
+    """recs: sequence of (t, i, k) -> device tensor of WorkerRec (uint32 x4)."""
+    a = np.zeros((len(recs), 4), np.uint32)
+    if len(recs):
+        a[:, :3] = np.asarray(recs, np.int64).astype(np.uint32)
+    return torch.from_numpy(a).to(device, non_blocking=True)

@@ -1,0 +1,168 @@
+"""FLSimulation: the server loop of main.py:126-188 on MI355X.
+
+Per epoch t (one "server step"):
+  1. schedule scan on the host (flsim_sched_epoch; main.py:137-181) and the dataset draws
+     k_i = np.random.randint(0, n) for every worker (main.py:138, seeded stream);
+  2. the workers that compute this epoch are split into contiguous blocks, one per rank
+     (torch.distributed; one process per GPU), and each rank runs its block as worker-batched
+     chunks of `chunk_workers` x 128 samples through the HIP forward/backward; all of them use
+     theta_t, so their gradients simply add (agents.py:35) -- S_t;
+  3. world > 1: ONE all-reduce (RCCL) of [S_t partial | per-worker losses];
+  4. a slow worker that computed stores S_t in its FIFO (main.py:156,161: the entry is an alias
+     of the epoch's .grad tensors, so under torch >= 2 it holds S_t); popped entries (main.py:162)
+     are the stale gradients S_{t-d};
+  5. fused rule() + Adam on the device: c_t copies of S_t and the stale entries (main.py:184,188);
+  6. 'Avg. Loss' = np.mean of the fast workers' losses (main.py:172,185).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .data import DevicePool
+from .engine import PN1Engine, PN1_SIZES, padded, worker_table
+from .schedule import Schedule, reference_delays
+
+SEMANTICS = ("reference", "torch1")
+
+
+def default_theta(seed=0):
+    """torch default init of PerformantNet1 under torch.manual_seed(seed) (CPU RNG, like main.py:97
+    with a seed), flattened in named_parameters order."""
+    from FL.models import PerformantNet1
+    torch.manual_seed(seed)
+    m = PerformantNet1()
+    return torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+
+
+class FLSimulation:
+    def __init__(self, n_workers, delay=100, delays=None, throttle=False, lr=1e-3, seed=0,
+                 semantics="reference", dropout=True, chunk_workers=32, device=None, theta0=None,
+                 group=None, max_throttle=32, pool=None, betas=(0.9, 0.999), eps=1e-8):
+        if semantics not in SEMANTICS:
+            raise NotImplementedError(f"semantics {semantics!r} (supported: {SEMANTICS})")
+        self.n = int(n_workers)
+        if self.n < 1:
+            raise ValueError("n_workers must be >= 1")
+        self.delays = np.asarray(delays if delays is not None else reference_delays(self.n, delay),
+                                 np.int32)
+        self.delay_arg = delay
+        self.throttle = bool(throttle)
+        self.lr, self.betas, self.eps = float(lr), tuple(betas), float(eps)
+        self.seed = int(seed)
+        self.semantics = semantics
+        self.dropout = bool(dropout)
+        self.group = group
+        dist = torch.distributed
+        if dist.is_available() and dist.is_initialized():
+            self.rank = dist.get_rank(group)
+            self.world = dist.get_world_size(group)
+        else:
+            self.rank, self.world = 0, 1
+        self.device = torch.device(device) if device is not None else \
+            torch.device("cuda", torch.cuda.current_device())
+        self.engine = PN1Engine(self.device, chunk_workers)
+        self.pool = DevicePool(self.device, self.seed, pool)
+        self.sched = Schedule(self.n, self.delays, self.throttle, max_throttle)
+        self.rs = np.random.RandomState(self.seed)   # main.py:138 np.random stream
+        P = self.engine.P
+        self.P = P
+        self.Ppad = padded(P)
+        th = default_theta(self.seed) if theta0 is None else torch.as_tensor(theta0)
+        self.theta = th.to(self.device, torch.float32).contiguous().clone()
+        self.m = torch.zeros_like(self.theta)
+        self.v = torch.zeros_like(self.theta)
+        self.step = 0
+        # [S_t | losses of the computing workers]; one all-reduce per epoch when world > 1
+        self.comm = torch.zeros(self.Ppad + padded(self.n), device=self.device)
+        self.stale_store = {}     # epoch -> [slot tensor, refcount]
+        self.free_slots = []
+        self.trace = []
+        self.loss_log = []        # per epoch: float (synced) or (device tensor, fast mask)
+
+    # ---------------------------------------------------------------------------------------------
+    def _slot(self):
+        return self.free_slots.pop() if self.free_slots else \
+            torch.empty(self.Ppad, device=self.device)
+
+    def shard(self, active):
+        lo = (len(active) * self.rank) // self.world
+        hi = (len(active) * (self.rank + 1)) // self.world
+        return lo, hi
+
+    def epoch(self, sync_loss=True):
+        plan = self.sched.next_epoch()          # raises IndexError like rule() on empty weight_ups
+        t = plan.t
+        if t >= 1 and self.delay_arg == 0 and self.delays[self.n - 1] == 0:
+            raise ZeroDivisionError("integer division or modulo by zero")   # main.py:158
+        ks = self.rs.randint(0, self.n, size=self.n)
+        active = np.nonzero(plan.computes)[0]
+        lo, hi = self.shard(active)
+        eng = self.engine
+        S = self.comm[:self.P]
+        losses = self.comm[self.Ppad:self.Ppad + len(active)]
+        if self.world > 1:
+            losses.zero_()
+        eng.begin_epoch(self.theta)
+        cw = eng.chunk_workers
+        for c0 in range(lo, hi, cw):
+            c1 = min(hi, c0 + cw)
+            recs = [(t, int(i), int(ks[i])) for i in active[c0:c1]]
+            wt = worker_table(recs, self.device)
+            eng.run_chunk(self.theta, self.pool, wt, c1 - c0, self.n, self.seed, self.dropout,
+                          losses[c0:c1])
+        eng.end_epoch(S)
+        if self.world > 1:
+            torch.distributed.all_reduce(self.comm[:self.Ppad + len(active)], group=self.group)
+        if plan.pushed and self.semantics == "reference":
+            n_push = int(sum(1 for i in range(self.n) if self.delays[i] != 0 and plan.computes[i]))
+            slot = self._slot()
+            slot[:self.P].copy_(S)
+            self.stale_store[t] = [slot, n_push]
+        stale = []
+        for (_, src) in plan.stale:
+            if self.semantics == "reference":
+                entry = self.stale_store[src]
+                stale.append(entry[0])
+            else:
+                stale.append(None)
+        self.step += 1
+        eng.aggregate_adam(S, plan.c_t, stale, self.theta, self.m, self.v, self.step, self.lr,
+                           self.betas, self.eps)
+        for (_, src) in plan.stale:
+            if self.semantics == "reference":
+                entry = self.stale_store[src]
+                entry[1] -= 1
+                if entry[1] == 0:
+                    self.free_slots.append(entry[0])
+                    del self.stale_store[src]
+        fast_pos = np.nonzero(plan.fast[active])[0]
+        self.trace.append(plan)
+        if sync_loss:
+            lv = losses.detach().cpu().numpy()[fast_pos]
+            val = float(np.mean(lv.astype(np.float32))) if len(lv) else float("nan")
+            self.loss_log.append(val)
+            return val
+        self.loss_log.append((losses.detach().clone(), fast_pos))
+        return None
+
+    def losses(self):
+        out = []
+        for e in self.loss_log:
+            if isinstance(e, tuple):
+                lv = e[0].cpu().numpy()[e[1]]
+                out.append(float(np.mean(lv.astype(np.float32))) if len(lv) else float("nan"))
+            else:
+                out.append(e)
+        self.loss_log = list(out)
+        return out
+
+    def executed_worker_steps(self, plan):
+        return int(plan.computes.sum())
+
+    def param_views(self):
+        from .engine import split_views
+        return split_views(self.theta)
+
+
+__all__ = ["FLSimulation", "default_theta", "PN1_SIZES"]

@@ -1,0 +1,96 @@
+/*
+ * flsim.h -- C-ABI of libflsim.so, the MI355X (gfx950) engine for the federated-learning
+ * simulation hot path of grossmanlev/FL-distributed-delay.
+ *
+ * The reference is pure Python; its "interface" for this path is the call sites below.  Each
+ * entry point names the reference code it replaces.  All device pointers are raw HIP device
+ * addresses (e.g. torch tensor data_ptr()), all work is enqueued on `stream` and is
+ * asynchronous; no entry point allocates device memory or synchronises.  Status: 0 = OK,
+ * 1 = invalid argument / the reference would raise, 2 = HIP error; flsim_last_error() gives the
+ * message (thread-local).
+ */
+#ifndef FLSIM_H
+#define FLSIM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* flsim_stream_t; /* == hipStream_t */
+
+/* one simulated worker-step of a chunk: epoch t, worker i, dataset index k (main.py:138) */
+typedef struct WorkerRec {
+    uint32_t t;
+    uint32_t i;
+    uint32_t k;
+    uint32_t pad;
+} WorkerRec;
+
+const char* flsim_last_error(void);
+
+/* ---------------------------------------------------------------------------------------------
+ * Schedule (host): replaces the integer scan of main.py:119-123 (state), :150-166 (slow worker
+ * + pesky_worker_grads FIFO), :167-178 (fast worker + throttle), :180-181 (window decrement).
+ * delays[i] != 0 marks a slow worker (reference: only i = n-1, delay = --delay).
+ * ------------------------------------------------------------------------------------------- */
+typedef struct flsim_sched flsim_sched;
+flsim_sched* flsim_sched_create(int32_t n, const int32_t* delays, int32_t throttle,
+                                int32_t max_throttle);
+void flsim_sched_destroy(flsim_sched* s);
+/* computes[n], fast[n]: u8 flags; stale_worker[n], stale_src[n]: popped FIFO entries in append
+ * order; info[4] = {c_t, s_t, pushed, t}.  Returns 1 where main.py would raise IndexError in
+ * rule() (empty weight_ups). */
+int flsim_sched_epoch(flsim_sched* s, uint8_t* computes, uint8_t* fast, int32_t* stale_worker,
+                      int64_t* stale_src, int64_t* info);
+void flsim_sched_state(const flsim_sched* s, int64_t* out3);
+
+/* ---------------------------------------------------------------------------------------------
+ * PerformantNet1 worker-batched forward/backward: replaces Worker.fwd_bkwd (agents.py:32-40)
+ * for every worker of a chunk at once, on models.py:11-47, including the batch draw of
+ * main.py:138-142 (synthetic CIFAR-shaped u8 pool, ToTensor + Normalize via `lut`).
+ * Gradients of all chunks of an epoch accumulate (agents.py:35 in-place .grad accumulation)
+ * into split-K slabs inside `gradstate`; flsim_pn1_end_epoch sums them into S_t (torch
+ * named_parameters layout, P = flsim_pn1_param_count() floats).
+ * ------------------------------------------------------------------------------------------- */
+long flsim_pn1_param_count(void);
+long flsim_pn1_gradstate_bytes(void);
+long flsim_pn1_workspace_bytes(int max_samples);
+int flsim_pn1_workspace_offset(int which, int samples, long* offset_bytes);
+/* packs theta_t into the kernel layouts and zeroes the slabs (start of main.py:126 epoch) */
+int flsim_pn1_begin_epoch(void* gradstate, const float* theta, flsim_stream_t stream);
+/* workers: device array of n_chunk_workers WorkerRec; worker_loss: device float per worker
+ * (agents.py:40 lossval); backward_pass 0 = forward + loss only (eval / debugging) */
+int flsim_pn1_fwd_bwd_chunk(void* gradstate, void* workspace, int max_samples, const float* theta,
+                            const uint8_t* pool, const int32_t* labels, const int32_t* list_a,
+                            int len_a, const int32_t* list_b, int len_b, const float* lut,
+                            const WorkerRec* workers, int n_chunk_workers, int n_workers_total,
+                            uint64_t seed, int dropout, int backward_pass, float* worker_loss,
+                            flsim_stream_t stream);
+/* explicit batch variant (Worker.fwd_bkwd(inp, outp), agents.py:32): x NCHW fp32 [n][3][32][32],
+ * y int64 [n], n a multiple of 128; workers[n/128] give the dropout RNG keys */
+int flsim_pn1_fwd_bwd_input(void* gradstate, void* workspace, int max_samples, const float* theta,
+                            const float* x, const int64_t* y, int n_samples,
+                            const WorkerRec* workers, uint64_t seed, int dropout,
+                            int backward_pass, float* worker_loss, flsim_stream_t stream);
+int flsim_pn1_end_epoch(void* gradstate, float* grad_out, flsim_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Fused server step: replaces Agg.rule = rule() (main.py:23-25, agents.py:43-45: per-tensor
+ * torch.stack(weight_ups).mean(0)) + Central.update_model (agents.py:9-21: Adam step,
+ * main.py:106).  weight_ups = c copies of S (the aliased fast entries) followed by n_stale stale
+ * entries (nullptr entry = zeros, the torch-1.x semantics).  Bit-exact with torch 2.10 CPU
+ * except sqrt rounding.  step = Adam step count after increment.
+ * ------------------------------------------------------------------------------------------- */
+int flsim_aggregate_adam(const float* S, int c, const float* const* stale, int n_stale,
+                         float* p, float* m, float* v, long P, const long* tensor_sizes,
+                         int n_tensors, long step, double lr, double beta1, double beta2,
+                         double eps, flsim_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FLSIM_H */

@@ -1,0 +1,94 @@
+"""CPU-only checks of the product library: it loads, exports every symbol include/flsim.h
+declares, and its host-side schedule (C-ABI) is bit-exact with traces of the reference's loop."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "flsim.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(flsim_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    from flsim import _lib
+    L = _lib.lib()
+    names = _declared()
+    assert len(names) >= 13
+    for n in names:
+        assert hasattr(L, n), n
+    assert set(names) == set(_lib.EXPORTS)
+    assert L.flsim_pn1_param_count() == 5596090
+
+
+def test_workspace_sizes():
+    from flsim import _lib
+    L = _lib.lib()
+    assert L.flsim_pn1_workspace_bytes(4096) > 4096 * 1_500_000
+    assert L.flsim_pn1_gradstate_bytes() > 0
+
+
+def _parse(key):
+    n, d, thr, ep = re.match(r"n(\d+)_d(\d+)_thr(\d)_e(\d+)", key).groups()
+    return int(n), int(d), int(thr), int(ep)
+
+
+def test_schedule_abi_matches_reference_traces(golden):
+    from flsim.schedule import Schedule, reference_delays
+    g = golden.schedule
+    keys = sorted({re.match(r"(n\d+_d\d+_thr\d_e\d+)_", k).group(1) for k in g.files})
+    for key in keys:
+        n, d, thr, ep = _parse(key)
+        if n > 20:
+            ep = min(ep, 300)
+        s = Schedule(n, reference_delays(n, d), thr)
+        comp = np.zeros((ep, n), np.uint8)
+        c_t = np.zeros(ep, np.int32)
+        stale = np.full(ep, -1, np.int64)
+        for t in range(ep):
+            p = s.next_epoch()
+            comp[t] = p.computes
+            c_t[t] = p.c_t
+            if p.stale:
+                assert len(p.stale) == 1 and p.stale[0][0] == n - 1
+                stale[t] = p.stale[0][1]
+            assert np.array_equal(p.fast, p.computes * (np.arange(n) != n - 1))
+        ref = np.unpackbits(g[key + "_computes"], axis=1)[:ep, :n]
+        assert np.array_equal(comp, ref), key
+        assert np.array_equal(c_t, g[key + "_c_t"][:ep]), key
+        assert np.array_equal(stale, g[key + "_stale"][:ep]), key
+
+
+def test_schedule_heterogeneous_matches_oracle():
+    """Config-4 extension: several slow workers with their own delays."""
+    from flsim.schedule import Schedule
+    from oracle import oracle as O
+    rs = np.random.RandomState(3)
+    n = 64
+    delays = np.where(rs.rand(n) < 0.3, rs.geometric(0.05, n), 0).astype(np.int32)
+    ep = 200
+    for thr in (0, 1):
+        ref = O.schedule(n, delays, thr, ep)
+        s = Schedule(n, delays, thr)
+        for t in range(ep):
+            p = s.next_epoch()
+            assert np.array_equal(p.computes, ref.computes[t])
+            assert p.c_t == ref.c_t[t] and p.s_t == ref.s_t[t]
+            srcs = [src for (_, src) in p.stale]
+            assert srcs == [int(x) for x in ref.stale_src[t][ref.stale_src[t] >= 0]]
+
+
+def test_schedule_empty_epoch_raises_like_rule():
+    from flsim.schedule import Schedule
+    # n=1: the only worker is the slow one; at t=1 (not a tick for d=5) weight_ups is empty ->
+    # the reference raises IndexError in rule() (main.py:25)
+    s = Schedule(1, np.array([5], np.int32), False)
+    with pytest.raises(IndexError):
+        s.next_epoch()      # t=0: slow worker computes and pushes, nothing appended
