@@ -365,22 +365,53 @@ __global__ void k_fin_plain(const float* __restrict__ slab, int Z, long n, float
 // =============================================================================================
 // GEMM launch helper
 // =============================================================================================
+// ---- live kernel timing probe (bench.py): HIP events recorded on the launch stream around each
+// GEMM launch, tagged with the launch id and its algorithmic FLOPs ----
+enum KernelId {
+    K_FWD1 = 0, K_FWD2, K_FWD3, K_FWD4, K_FWD5, K_FWD6, K_L1F, K_L2F,
+    K_DG2, K_DG3, K_DG4, K_DG5, K_DG6,
+    K_WG1, K_WG2, K_WG3, K_WG4, K_WG5, K_WG6,
+    K_L1W, K_L1D, K_L2W, K_L2D, K_COUNT
+};
+static const char* KNAME[K_COUNT] = {
+    "conv1_fwd", "conv2_fwd", "conv3_fwd", "conv4_fwd", "conv5_fwd", "conv6_fwd", "linear1_fwd",
+    "linear2_fwd", "conv2_dgrad", "conv3_dgrad", "conv4_dgrad", "conv5_dgrad", "conv6_dgrad",
+    "conv1_wgrad", "conv2_wgrad", "conv3_wgrad", "conv4_wgrad", "conv5_wgrad", "conv6_wgrad",
+    "linear1_wgrad", "linear1_dgrad", "linear2_wgrad", "linear2_dgrad"};
+
+struct Probe {
+    bool on = false;
+    int cap = 0, used = 0;
+    hipEvent_t* ev = nullptr;
+    int* kid = nullptr;
+    double* flops = nullptr;
+};
+static Probe g_probe;
+
 template <int FM, int FN, int WM, int WN, class AL, class BL, class EPI>
 static int launch_gemm(const AL& al, const BL& bl, const EPI& epi, int M, int N, int ksteps, int Z,
-                       hipStream_t st) {
+                       hipStream_t st, int kid, double alg_flops) {
     constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
     const int per = (ksteps + Z - 1) / Z;
     dim3 grid(ceil_div(M, BM), ceil_div(N, BN), Z);
+    const bool probe = g_probe.on && g_probe.used < g_probe.cap;
+    if (probe) FLSIM_CHECK_HIP(hipEventRecord(g_probe.ev[2 * g_probe.used], st));
     hipLaunchKernelGGL((gemm_kernel<FM, FN, WM, WN, AL, BL, EPI>), grid, dim3(64 * WM * WN), 0, st,
                        al, bl, epi, ksteps, per);
     FLSIM_LAUNCH_CHECK();
+    if (probe) {
+        FLSIM_CHECK_HIP(hipEventRecord(g_probe.ev[2 * g_probe.used + 1], st));
+        g_probe.kid[g_probe.used] = kid;
+        g_probe.flops[g_probe.used] = alg_flops;
+        g_probe.used++;
+    }
     return 0;
 }
 
 // forward conv (also the data-gradient conv): out[m][n] for m < S*OH*OW, n < N
 template <int IH, int IW, int CI, int PAD, int FM, int FN, int WM, int WN, class EPI>
 static int conv_like(const float* X, int S, const float* Wpk, int N, int KP, const EPI& epi,
-                     hipStream_t st) {
+                     hipStream_t st, int kid, int kreal) {
     constexpr int NT = 64 * WM * WN;
     constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
     using AL = Im2colKC<IH, IW, CI, PAD, BM, NT>;
@@ -392,13 +423,14 @@ static int conv_like(const float* X, int S, const float* Wpk, int N, int KP, con
     bl.P = Wpk;
     bl.ld = KP;
     bl.NR = N;
-    return launch_gemm<FM, FN, WM, WN>(al, bl, epi, al.M, N, KP / GK, 1, st);
+    return launch_gemm<FM, FN, WM, WN>(al, bl, epi, al.M, N, KP / GK, 1, st, kid,
+                                       2.0 * al.M * N * kreal);
 }
 
 // weight gradient: slab[z][co][kk] += sum_p dz[p][co] * im2col(X)[p][kk]
 template <int IH, int IW, int CI, int FM, int FN, int WM, int WN>
 static int conv_wgrad(const float* dz, const float* X, int S, int CO, int KP, float* slab, int Z,
-                      hipStream_t st) {
+                      hipStream_t st, int kid, int kreal) {
     constexpr int NT = 64 * WM * WN;
     constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
     using AL = RowsKM<BM, NT>;
@@ -413,7 +445,8 @@ static int conv_wgrad(const float* dz, const float* X, int S, int CO, int KP, fl
     bl.X = X;
     bl.M = M;
     EpiSlabAcc epi{slab, CO, KP, (long)CO * KP};
-    return launch_gemm<FM, FN, WM, WN>(al, bl, epi, CO, KP, ceil_div(M, GK), Z, st);
+    return launch_gemm<FM, FN, WM, WN>(al, bl, epi, CO, KP, ceil_div(M, GK), Z, st, kid,
+                                       2.0 * M * CO * kreal);
 }
 
 // =============================================================================================
@@ -536,9 +569,9 @@ static int forward(const GradState& g, const WS& w, const float* theta, int S,
                    const WorkerRec* workers, uint64_t seed, int dropout, hipStream_t st) {
     // conv1, conv2 (+ReLU)  models.py:29-30
     RC((conv_like<32, 32, 4, 2, 4, 3, 4, 1>(w.x0, S, g.wf[0], 48, 48,
-        EpiBiasRelu{w.a1, theta + P_OFF[1], S * 34 * 34, 48}, st)));
+        EpiBiasRelu{w.a1, theta + P_OFF[1], S * 34 * 34, 48}, st, K_FWD1, 27)));
     RC((conv_like<34, 34, 48, 2, 4, 3, 4, 1>(w.a1, S, g.wf[1], 48, 432,
-        EpiBiasRelu{w.a2, theta + P_OFF[3], S * 36 * 36, 48}, st)));
+        EpiBiasRelu{w.a2, theta + P_OFF[3], S * 36 * 36, 48}, st, K_FWD2, 432)));
     {   // pool1 + dropout1  models.py:31-32
         const long tot = (long)S * 18 * 18 * 48;
         hipLaunchKernelGGL((k_pool_drop_fwd<36, 36, 48, false>), dim3(ceil_div(tot, 256)), dim3(256),
@@ -547,9 +580,9 @@ static int forward(const GradState& g, const WS& w, const float* theta, int S,
         FLSIM_LAUNCH_CHECK();
     }
     RC((conv_like<18, 18, 48, 2, 4, 3, 2, 2>(w.d1, S, g.wf[2], 96, 432,
-        EpiBiasRelu{w.a3, theta + P_OFF[5], S * 20 * 20, 96}, st)));
+        EpiBiasRelu{w.a3, theta + P_OFF[5], S * 20 * 20, 96}, st, K_FWD3, 432)));
     RC((conv_like<20, 20, 96, 2, 4, 3, 2, 2>(w.a3, S, g.wf[3], 96, 864,
-        EpiBiasRelu{w.a4, theta + P_OFF[7], S * 22 * 22, 96}, st)));
+        EpiBiasRelu{w.a4, theta + P_OFF[7], S * 22 * 22, 96}, st, K_FWD4, 864)));
     {
         const long tot = (long)S * 11 * 11 * 96;
         hipLaunchKernelGGL((k_pool_drop_fwd<22, 22, 96, false>), dim3(ceil_div(tot, 256)), dim3(256),
@@ -558,9 +591,9 @@ static int forward(const GradState& g, const WS& w, const float* theta, int S,
         FLSIM_LAUNCH_CHECK();
     }
     RC((conv_like<11, 11, 96, 2, 4, 3, 2, 2>(w.d2, S, g.wf[4], 192, 864,
-        EpiBiasRelu{w.a5, theta + P_OFF[9], S * 13 * 13, 192}, st)));
+        EpiBiasRelu{w.a5, theta + P_OFF[9], S * 13 * 13, 192}, st, K_FWD5, 864)));
     RC((conv_like<13, 13, 192, 2, 4, 3, 2, 2>(w.a5, S, g.wf[5], 192, 1728,
-        EpiBiasRelu{w.a6, theta + P_OFF[11], S * 15 * 15, 192}, st)));
+        EpiBiasRelu{w.a6, theta + P_OFF[11], S * 15 * 15, 192}, st, K_FWD6, 1728)));
     {
         const long tot = (long)S * 7 * 7 * 192;
         hipLaunchKernelGGL((k_pool_drop_fwd<15, 15, 192, true>), dim3(ceil_div(tot, 256)), dim3(256),
@@ -576,7 +609,7 @@ static int forward(const GradState& g, const WS& w, const float* theta, int S,
         RowsKC<128, NT> bl{};
         bl.P = theta + P_OFF[12]; bl.ld = 9408; bl.NR = 512;
         EpiSlabStore epi{w.part, S, 512, (long)S * 512};
-        RC((launch_gemm<4, 4, 2, 2>(al, bl, epi, S, 512, 9408 / GK, ZL1F, st)));
+        RC((launch_gemm<4, 4, 2, 2>(al, bl, epi, S, 512, 9408 / GK, ZL1F, st, K_L1F, 2.0 * S * 512 * 9408)));
         const long tot = (long)S * 512;
         hipLaunchKernelGGL(k_linear_finish, dim3(ceil_div(tot, 256)), dim3(256), 0, st, w.part, ZL1F,
                            theta + P_OFF[13], w.e1, S, 512, workers, seed, SITE_DROP4, THR_P50,
@@ -590,7 +623,7 @@ static int forward(const GradState& g, const WS& w, const float* theta, int S,
         RowsKC<64, NT> bl{};
         bl.P = theta + P_OFF[14]; bl.ld = 512; bl.NR = 256;
         EpiSlabStore epi{w.part, S, 256, (long)S * 256};
-        RC((launch_gemm<2, 2, 2, 2>(al, bl, epi, S, 256, 512 / GK, 1, st)));
+        RC((launch_gemm<2, 2, 2, 2>(al, bl, epi, S, 256, 512 / GK, 1, st, K_L2F, 2.0 * S * 256 * 512)));
         const long tot = (long)S * 256;
         hipLaunchKernelGGL(k_linear_finish, dim3(ceil_div(tot, 256)), dim3(256), 0, st, w.part, 1,
                            theta + P_OFF[15], w.e2, S, 256, workers, seed, SITE_DROP5, THR_P50,
@@ -615,7 +648,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
         RowsKM<128, NT> bl{};
         bl.P = w.e1; bl.ld = 512; bl.NK = S; bl.NC = 512;
         EpiSlabAcc epi{g.l2w, 256, 512, 256L * 512};
-        RC((launch_gemm<4, 4, 2, 2>(al, bl, epi, 256, 512, ceil_div(S, GK), ZL2W, st)));
+        RC((launch_gemm<4, 4, 2, 2>(al, bl, epi, 256, 512, ceil_div(S, GK), ZL2W, st, K_L2W, 2.0 * S * 256 * 512)));
         hipLaunchKernelGGL(k_colsum_acc, dim3(ZB), dim3(256), 0, st, w.dh2, (long)S, 256, g.l2b, ZB);
         FLSIM_LAUNCH_CHECK();
         RowsKC<64, NT> dl{};
@@ -623,7 +656,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
         RowsKM<64, NT> wl{};
         wl.P = theta + P_OFF[14]; wl.ld = 512; wl.NK = 256; wl.NC = 512;
         EpiDropMask de{w.dh1, w.e1, s50, S, 512};
-        RC((launch_gemm<2, 2, 2, 2>(dl, wl, de, S, 512, 256 / GK, 1, st)));
+        RC((launch_gemm<2, 2, 2, 2>(dl, wl, de, S, 512, 256 / GK, 1, st, K_L2D, 2.0 * S * 256 * 512)));
     }
     // ---- linear1: wgrad, bias, dgrad (-> gradient wrt d3 through dropout1 site 3) ----
     {
@@ -633,7 +666,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
         RowsKM<128, NT> bl{};
         bl.P = w.d3; bl.ld = 9408; bl.NK = S; bl.NC = 9408;
         EpiSlabAcc epi{g.l1w, 512, 9408, 512L * 9408};
-        RC((launch_gemm<4, 4, 2, 2>(al, bl, epi, 512, 9408, ceil_div(S, GK), ZL1W, st)));
+        RC((launch_gemm<4, 4, 2, 2>(al, bl, epi, 512, 9408, ceil_div(S, GK), ZL1W, st, K_L1W, 2.0 * S * 512 * 9408)));
         hipLaunchKernelGGL(k_colsum_acc, dim3(ZB), dim3(256), 0, st, w.dh1, (long)S, 512, g.l1b, ZB);
         FLSIM_LAUNCH_CHECK();
         RowsKC<128, NT> dl{};
@@ -641,7 +674,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
         RowsKM<128, NT> wl{};
         wl.P = theta + P_OFF[12]; wl.ld = 9408; wl.NK = 512; wl.NC = 9408;
         EpiDropMask de{w.gy, w.d3, s25, S, 9408};
-        RC((launch_gemm<4, 4, 2, 2>(dl, wl, de, S, 9408, 512 / GK, 1, st)));
+        RC((launch_gemm<4, 4, 2, 2>(dl, wl, de, S, 9408, 512 / GK, 1, st, K_L1D, 2.0 * S * 512 * 9408)));
     }
     // ---- pool3 backward -> dz6 (a6 buffer) ----
     {
@@ -652,18 +685,18 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     }
     float* dz6 = w.a6;
     // ---- conv6: wgrad (input a5), bias, dgrad -> dz5 = . * (a5 > 0) into gx ----
-    RC((conv_wgrad<13, 13, 192, 3, 3, 2, 3>(dz6, w.a5, S, 192, 1728, g.sw[5], GEO[5].ZW, st)));
+    RC((conv_wgrad<13, 13, 192, 3, 3, 2, 3>(dz6, w.a5, S, 192, 1728, g.sw[5], GEO[5].ZW, st, K_WG6, 1728)));
     hipLaunchKernelGGL(k_colsum_acc, dim3(ZB), dim3(256), 0, st, dz6, (long)S * 225, 192, g.sb[5], ZB);
     FLSIM_LAUNCH_CHECK();
     RC((conv_like<15, 15, 192, 0, 4, 3, 2, 2>(dz6, S, g.wd[5], 192, 1728,
-        EpiMask<true>{w.gx, w.a5, S * 13 * 13, 192}, st)));
+        EpiMask<true>{w.gx, w.a5, S * 13 * 13, 192}, st, K_DG6, 1728)));
     float* dz5 = w.gx;
     // ---- conv5: wgrad (input d2), bias, dgrad -> grad wrt d2 (dropout site 2) into gy ----
-    RC((conv_wgrad<11, 11, 96, 3, 3, 2, 3>(dz5, w.d2, S, 192, 864, g.sw[4], GEO[4].ZW, st)));
+    RC((conv_wgrad<11, 11, 96, 3, 3, 2, 3>(dz5, w.d2, S, 192, 864, g.sw[4], GEO[4].ZW, st, K_WG5, 864)));
     hipLaunchKernelGGL(k_colsum_acc, dim3(ZB), dim3(256), 0, st, dz5, (long)S * 169, 192, g.sb[4], ZB);
     FLSIM_LAUNCH_CHECK();
     RC((conv_like<13, 13, 192, 0, 4, 3, 2, 2>(dz5, S, g.wd[4], 96, 1728,
-        EpiDropMask{w.gy, w.d2, s25, S * 11 * 11, 96}, st)));
+        EpiDropMask{w.gy, w.d2, s25, S * 11 * 11, 96}, st, K_DG5, 1728)));
     {
         const long tot = (long)S * 22 * 22 * 96;
         hipLaunchKernelGGL((k_pool_bwd<22, 22, 96, false>), dim3(ceil_div(tot, 256)), dim3(256), 0, st,
@@ -672,18 +705,18 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     }
     float* dz4 = w.a4;
     // ---- conv4: wgrad (input a3), bias, dgrad -> dz3 = . * (a3 > 0) into gx ----
-    RC((conv_wgrad<20, 20, 96, 3, 3, 2, 3>(dz4, w.a3, S, 96, 864, g.sw[3], GEO[3].ZW, st)));
+    RC((conv_wgrad<20, 20, 96, 3, 3, 2, 3>(dz4, w.a3, S, 96, 864, g.sw[3], GEO[3].ZW, st, K_WG4, 864)));
     hipLaunchKernelGGL(k_colsum_acc, dim3(ZB), dim3(256), 0, st, dz4, (long)S * 484, 96, g.sb[3], ZB);
     FLSIM_LAUNCH_CHECK();
     RC((conv_like<22, 22, 96, 0, 4, 3, 2, 2>(dz4, S, g.wd[3], 96, 864,
-        EpiMask<true>{w.gx, w.a3, S * 20 * 20, 96}, st)));
+        EpiMask<true>{w.gx, w.a3, S * 20 * 20, 96}, st, K_DG4, 864)));
     float* dz3 = w.gx;
     // ---- conv3: wgrad (input d1), bias, dgrad -> grad wrt d1 (site 1) into gy ----
-    RC((conv_wgrad<18, 18, 48, 3, 3, 2, 3>(dz3, w.d1, S, 96, 432, g.sw[2], GEO[2].ZW, st)));
+    RC((conv_wgrad<18, 18, 48, 3, 3, 2, 3>(dz3, w.d1, S, 96, 432, g.sw[2], GEO[2].ZW, st, K_WG3, 432)));
     hipLaunchKernelGGL(k_colsum_acc, dim3(ZB), dim3(256), 0, st, dz3, (long)S * 400, 96, g.sb[2], ZB);
     FLSIM_LAUNCH_CHECK();
     RC((conv_like<20, 20, 96, 0, 4, 3, 4, 1>(dz3, S, g.wd[2], 48, 864,
-        EpiDropMask{w.gy, w.d1, s25, S * 18 * 18, 48}, st)));
+        EpiDropMask{w.gy, w.d1, s25, S * 18 * 18, 48}, st, K_DG3, 864)));
     {
         const long tot = (long)S * 36 * 36 * 48;
         hipLaunchKernelGGL((k_pool_bwd<36, 36, 48, false>), dim3(ceil_div(tot, 256)), dim3(256), 0, st,
@@ -692,14 +725,14 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     }
     float* dz2 = w.a2;
     // ---- conv2: wgrad (input a1), bias, dgrad -> dz1 = . * (a1 > 0) into gx ----
-    RC((conv_wgrad<34, 34, 48, 3, 3, 1, 3>(dz2, w.a1, S, 48, 432, g.sw[1], GEO[1].ZW, st)));
+    RC((conv_wgrad<34, 34, 48, 3, 3, 1, 3>(dz2, w.a1, S, 48, 432, g.sw[1], GEO[1].ZW, st, K_WG2, 432)));
     hipLaunchKernelGGL(k_colsum_acc, dim3(ZB), dim3(256), 0, st, dz2, (long)S * 1296, 48, g.sb[1], ZB);
     FLSIM_LAUNCH_CHECK();
     RC((conv_like<36, 36, 48, 0, 4, 3, 4, 1>(dz2, S, g.wd[1], 48, 432,
-        EpiMask<true>{w.gx, w.a1, S * 34 * 34, 48}, st)));
+        EpiMask<true>{w.gx, w.a1, S * 34 * 34, 48}, st, K_DG2, 432)));
     float* dz1 = w.gx;
     // ---- conv1: wgrad (input x0), bias ----
-    RC((conv_wgrad<32, 32, 4, 3, 3, 1, 1>(dz1, w.x0, S, 48, 48, g.sw[0], GEO[0].ZW, st)));
+    RC((conv_wgrad<32, 32, 4, 3, 3, 1, 1>(dz1, w.x0, S, 48, 48, g.sw[0], GEO[0].ZW, st, K_WG1, 27)));
     hipLaunchKernelGGL(k_colsum_acc, dim3(ZB), dim3(256), 0, st, dz1, (long)S * 1156, 48, g.sb[0], ZB);
     FLSIM_LAUNCH_CHECK();
     return 0;
@@ -715,6 +748,50 @@ using namespace flsim;
 extern "C" {
 
 const char* flsim_last_error(void) { return last_error(); }
+
+// Live per-kernel timing of the GEMM launches (bench.py).  capacity = launches to record.
+int flsim_probe_enable(int capacity) {
+    if (g_probe.on) return 0;
+    FLSIM_REQUIRE(capacity > 0, "capacity must be > 0");
+    g_probe.ev = new hipEvent_t[2 * capacity];
+    for (int i = 0; i < 2 * capacity; ++i) FLSIM_CHECK_HIP(hipEventCreate(&g_probe.ev[i]));
+    g_probe.kid = new int[capacity];
+    g_probe.flops = new double[capacity];
+    g_probe.cap = capacity;
+    g_probe.used = 0;
+    g_probe.on = true;
+    return 0;
+}
+
+// Synchronises on the recorded events; per kernel id: launches, total ms, total alg. FLOPs.
+// Resets the record.  Arrays have flsim_probe_kernel_count() entries.
+int flsim_probe_read(int* launches, double* total_ms, double* total_flops) {
+    for (int k = 0; k < K_COUNT; ++k) { launches[k] = 0; total_ms[k] = 0; total_flops[k] = 0; }
+    if (!g_probe.on) return 0;
+    for (int u = 0; u < g_probe.used; ++u) {
+        FLSIM_CHECK_HIP(hipEventSynchronize(g_probe.ev[2 * u + 1]));
+        float ms = 0.f;
+        FLSIM_CHECK_HIP(hipEventElapsedTime(&ms, g_probe.ev[2 * u], g_probe.ev[2 * u + 1]));
+        launches[g_probe.kid[u]] += 1;
+        total_ms[g_probe.kid[u]] += ms;
+        total_flops[g_probe.kid[u]] += g_probe.flops[u];
+    }
+    g_probe.used = 0;
+    return 0;
+}
+
+int flsim_probe_disable(void) {
+    if (!g_probe.on) return 0;
+    for (int i = 0; i < 2 * g_probe.cap; ++i) (void)hipEventDestroy(g_probe.ev[i]);
+    delete[] g_probe.ev;
+    delete[] g_probe.kid;
+    delete[] g_probe.flops;
+    g_probe = Probe();
+    return 0;
+}
+
+int flsim_probe_kernel_count(void) { return K_COUNT; }
+const char* flsim_probe_kernel_name(int kid) { return (kid >= 0 && kid < K_COUNT) ? KNAME[kid] : ""; }
 
 long flsim_pn1_param_count(void) { return P_TOTAL; }
 

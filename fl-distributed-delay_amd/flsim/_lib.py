@@ -18,7 +18,8 @@ EXPORTS = [
     "flsim_sched_state", "flsim_pn1_param_count", "flsim_pn1_gradstate_bytes",
     "flsim_pn1_workspace_bytes", "flsim_pn1_workspace_offset", "flsim_pn1_begin_epoch",
     "flsim_pn1_fwd_bwd_chunk", "flsim_pn1_fwd_bwd_input", "flsim_pn1_end_epoch",
-    "flsim_aggregate_adam",
+    "flsim_aggregate_adam", "flsim_probe_enable", "flsim_probe_read", "flsim_probe_disable",
+    "flsim_probe_kernel_count", "flsim_probe_kernel_name",
 ]
 
 
@@ -65,6 +66,10 @@ def lib():
     L.flsim_aggregate_adam.argtypes = [
         vp, ctypes.c_int, vp, ctypes.c_int, vp, vp, vp, ctypes.c_long, vp, ctypes.c_int,
         ctypes.c_long, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp]
+    L.flsim_probe_enable.argtypes = [ctypes.c_int]
+    L.flsim_probe_read.argtypes = [vp, vp, vp]
+    L.flsim_probe_kernel_name.restype = ctypes.c_char_p
+    L.flsim_probe_kernel_name.argtypes = [ctypes.c_int]
     _L = L
     return L
 
@@ -85,3 +90,25 @@ def ptr(t):
 
 def stream_ptr(device=None):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class KernelProbe:
+    """HIP events around every worker-batched GEMM launch (recorded by libflsim.so on the launch
+    stream).  read() -> {kernel name: (launches, total_ms, total_algorithmic_flops)}."""
+
+    def __init__(self, capacity=20000):
+        check(lib().flsim_probe_enable(capacity))
+
+    def read(self):
+        import numpy as np
+        n = lib().flsim_probe_kernel_count()
+        cnt = np.zeros(n, np.int32)
+        ms = np.zeros(n, np.float64)
+        fl = np.zeros(n, np.float64)
+        check(lib().flsim_probe_read(cnt.ctypes.data_as(vp), ms.ctypes.data_as(vp),
+                                     fl.ctypes.data_as(vp)))
+        return {lib().flsim_probe_kernel_name(k).decode(): (int(cnt[k]), float(ms[k]), float(fl[k]))
+                for k in range(n) if cnt[k]}
+
+    def close(self):
+        check(lib().flsim_probe_disable())

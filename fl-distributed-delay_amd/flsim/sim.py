@@ -38,7 +38,8 @@ def default_theta(seed=0):
 class FLSimulation:
     def __init__(self, n_workers, delay=100, delays=None, throttle=False, lr=1e-3, seed=0,
                  semantics="reference", dropout=True, chunk_workers=32, device=None, theta0=None,
-                 group=None, max_throttle=32, pool=None, betas=(0.9, 0.999), eps=1e-8):
+                 group=None, max_throttle=32, pool=None, betas=(0.9, 0.999), eps=1e-8,
+                 engine=None, device_pool=None):
         if semantics not in SEMANTICS:
             raise NotImplementedError(f"semantics {semantics!r} (supported: {SEMANTICS})")
         self.n = int(n_workers)
@@ -61,8 +62,11 @@ class FLSimulation:
             self.rank, self.world = 0, 1
         self.device = torch.device(device) if device is not None else \
             torch.device("cuda", torch.cuda.current_device())
-        self.engine = PN1Engine(self.device, chunk_workers)
-        self.pool = DevicePool(self.device, self.seed, pool)
+        # engine / device_pool are injectable only so tests can drive the sharding and
+        # collective logic with a CPU stand-in (gloo); the product path always builds PN1Engine
+        self.engine = engine if engine is not None else PN1Engine(self.device, chunk_workers)
+        self.pool = device_pool if device_pool is not None else \
+            DevicePool(self.device, self.seed, pool)
         self.sched = Schedule(self.n, self.delays, self.throttle, max_throttle)
         self.rs = np.random.RandomState(self.seed)   # main.py:138 np.random stream
         P = self.engine.P
@@ -79,6 +83,7 @@ class FLSimulation:
         self.free_slots = []
         self.trace = []
         self.loss_log = []        # per epoch: float (synced) or (device tensor, fast mask)
+        self.agg_timing = None    # list -> (start event, end event, algorithmic bytes) per step
 
     # ---------------------------------------------------------------------------------------------
     def _slot(self):
@@ -127,8 +132,17 @@ class FLSimulation:
             else:
                 stale.append(None)
         self.step += 1
+        if self.agg_timing is not None:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
         eng.aggregate_adam(S, plan.c_t, stale, self.theta, self.m, self.v, self.step, self.lr,
                            self.betas, self.eps)
+        if self.agg_timing is not None:
+            e1.record()
+            n_stale_arrays = len({id(x) for x in stale if x is not None})
+            # read S_t + distinct stale slots + p, m, v; write p, m, v  
+            self.agg_timing.append((e0, e1, 4 * self.P * (1 + n_stale_arrays + 3 + 3)))
         for (_, src) in plan.stale:
             if self.semantics == "reference":
                 entry = self.stale_store[src]

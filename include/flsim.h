@@ -89,6 +89,17 @@ int flsim_aggregate_adam(const float* S, int c, const float* const* stale, int n
                          int n_tensors, long step, double lr, double beta1, double beta2,
                          double eps, flsim_stream_t stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Measurement (no reference counterpart): HIP events around every worker-batched GEMM launch on
+ * its stream, for bench.py's live roofline figure.  read() fills flsim_probe_kernel_count()
+ * entries per kernel id (launches, total ms, total algorithmic FLOPs) and resets the record.
+ * ------------------------------------------------------------------------------------------- */
+int flsim_probe_enable(int capacity);
+int flsim_probe_read(int* launches, double* total_ms, double* total_flops);
+int flsim_probe_disable(void);
+int flsim_probe_kernel_count(void);
+const char* flsim_probe_kernel_name(int kid);
+
 #ifdef __cplusplus
 }
 #endif

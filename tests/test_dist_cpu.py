@@ -1,0 +1,89 @@
+"""world_size-2 gloo test of the worker sharding + one all-reduce per server step (CPU).
+
+The HIP engine is replaced by a deterministic CPU stand-in (each worker-step contributes a
+vector that depends on (t, i, k, theta)); the test checks that 2 ranks, each computing only its
+contiguous block of the epoch's computing workers, end every epoch with the same parameters,
+staleness trace and per-worker losses as a single-process run.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+P = 5596090
+
+
+class StandInEngine:
+    """CPU stand-in with PN1Engine's interface (not a model: a fixed function of the inputs)."""
+
+    def __init__(self):
+        self.P = P
+        self.chunk_workers = 3
+        self.acc = torch.zeros(P, dtype=torch.float64)
+
+    def begin_epoch(self, theta):
+        self.acc.zero_()
+        self.theta_sum = float(theta[:1000].double().sum())
+
+    def run_chunk(self, theta, pool, workers_dev, n_chunk, n_total, seed, dropout, loss_out,
+                  backward=True):
+        for j, (t, i, k, _) in enumerate(workers_dev.tolist()):
+            g = torch.arange(P, dtype=torch.float64).mul_(1e-7 * (i + 1)).sin_()
+            self.acc += g * (1 + 0.01 * k) + 1e-3 * self.theta_sum
+            loss_out[j] = float(t + 0.001 * i + 0.0001 * k)
+
+    def end_epoch(self, S):
+        S.copy_(self.acc.float())
+
+    def aggregate_adam(self, S, c, stale, theta, m, v, step, lr=1e-3, betas=(0.9, 0.999),
+                       eps=1e-8):
+        tot = S * c
+        for s in stale:
+            if s is not None:
+                tot = tot + s[:P]
+        theta -= lr * tot / (c + len(stale))
+
+
+def _run(rank, world, n, d, thr, epochs, out, port):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.dirname(here))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "fl-distributed-delay_amd"))
+    if world > 1:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    from flsim.sim import FLSimulation
+    sim = FLSimulation(n, delay=d, throttle=thr, device="cpu", engine=StandInEngine(),
+                       device_pool=object(), theta0=torch.zeros(P))
+    losses = [sim.epoch() for _ in range(epochs)]
+    res = dict(theta=sim.theta.numpy().copy(), losses=losses,
+               trace=[(p.t, p.computes.tobytes(), p.stale) for p in sim.trace])
+    if world > 1:
+        dist.destroy_process_group()
+    out[rank] = res
+
+
+@pytest.mark.parametrize("thr", [False, True])
+def test_two_rank_sharding_matches_single(thr):
+    n, d, epochs = 11, 3, 7
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
+    single = mgr.dict()
+    _run(0, 1, n, d, thr, epochs, single, 0)
+    out = mgr.dict()
+    port = 29500 + (os.getpid() % 1000)
+    procs = [ctx.Process(target=_run, args=(r, 2, n, d, thr, epochs, out, port)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+        assert p.exitcode == 0
+    for r in range(2):
+        assert out[r]["trace"] == single[0]["trace"]
+        np.testing.assert_allclose(out[r]["losses"], single[0]["losses"], rtol=0, atol=1e-6)
+        np.testing.assert_allclose(out[r]["theta"], single[0]["theta"], rtol=1e-5, atol=1e-7)
+    assert np.array_equal(out[0]["theta"], out[1]["theta"])
