@@ -1,0 +1,204 @@
+"""Drop-in for the reference's FL/agents.py (agents.py:1-45) on MI355X.
+
+Same classes, signatures and aliasing semantics; the arithmetic runs in libflsim.so:
+
+  Worker.fwd_bkwd(inp, outp)   agents.py:32-40 -> flsim_pn1_fwd_bwd_input (HIP fwd/bwd of the
+                               central PerformantNet1); gradients accumulate over the workers of
+                               an epoch exactly like .grad (agents.py:35) and the returned list
+                               holds views of ONE flat buffer (every worker of the epoch gets the
+                               same tensors, as in the reference)
+  Agg(rule)                    agents.py:43-45; use FL.agents.rule (== main.py:23-25's mean) to
+                               get the fused path: it returns a lazy mean that Central consumes
+  Central.update_model(ups)    agents.py:9-21 -> flsim_aggregate_adam (fused cascade mean + Adam
+                               with the optimizer's lr/betas/eps); parameters live in one flat
+                               device buffer, model.parameters() are views of it
+
+Requirements (raise otherwise): the model is FL.models.PerformantNet1 on a HIP device, the
+optimizer is torch.optim.Adam without weight decay / amsgrad / maximize, batches are multiples
+of 128 samples.  There is no CPU fallback.
+"""
+from __future__ import annotations
+
+import itertools
+
+import numpy as np
+import torch
+
+from flsim.engine import PN1Engine, PN1_SHAPES, PN1_SIZES, split_views, worker_table, padded
+
+_CONTEXTS = {}
+_WORKER_IDS = itertools.count()
+
+
+class _ModelContext:
+    """Flat parameter / optimizer-state buffers and the engine of one central model."""
+
+    def __init__(self, model, seed=0):
+        names = [n for n, _ in model.named_parameters()]
+        if names != [n for n, _ in PN1_SHAPES]:
+            raise NotImplementedError("the HIP engine implements FL.models.PerformantNet1 only")
+        dev = next(model.parameters()).device
+        if dev.type != "cuda":
+            raise RuntimeError("move the model to the GPU first (main.py:105 model.to(device))")
+        self.device = dev
+        with torch.no_grad():
+            flat = torch.cat([p.detach().reshape(-1).float() for p in model.parameters()])
+        self.P = flat.numel()
+        self.theta = torch.zeros(padded(self.P), device=dev)
+        self.theta[:self.P].copy_(flat)
+        for p, view in zip(model.parameters(), split_views(self.theta[:self.P])):
+            p.data = view                       # parameters alias the flat buffer
+        self.m = torch.zeros_like(self.theta)
+        self.v = torch.zeros_like(self.theta)
+        self.engine = PN1Engine(dev, chunk_workers=1)
+        self.seed = seed
+        self.t = 0               # epoch counter (dropout RNG key)
+        self.G = None            # flat gradient buffer of the current epoch (p.grad views)
+        self.packed = False
+        self.step = 0
+        self.loss_buf = torch.zeros(64, device=dev)
+
+    def ensure_capacity(self, n_samples):
+        cw = n_samples // 128
+        if cw > self.engine.chunk_workers:
+            self.engine = PN1Engine(self.device, chunk_workers=cw)
+            self.packed = False
+        if cw > self.loss_buf.numel():
+            self.loss_buf = torch.zeros(cw, device=self.device)
+
+    def new_epoch(self):
+        self.t += 1
+        self.G = None
+        self.packed = False
+
+
+def _context(model):
+    ctx = _CONTEXTS.get(id(model))
+    if ctx is None:
+        ctx = _ModelContext(model)
+        _CONTEXTS[id(model)] = ctx
+    return ctx
+
+
+class _LazyMean(list):
+    """What FL.agents.rule returns: the weight_ups list, reduced inside Central.update_model."""
+
+    def __init__(self, ups_list):
+        super().__init__()
+        self.ups_list = ups_list
+
+
+def rule(ups_list):
+    """main.py:23-25 (element-wise mean of the gradient lists), evaluated lazily and fused with
+    the Adam step in Central.update_model."""
+    if len(ups_list) == 0:
+        raise IndexError("list index out of range")        # main.py:25 ups_list[0]
+    return _LazyMean(ups_list)
+
+
+class Central:
+    """agents.py:4-24."""
+
+    def __init__(self, model, optim, encryption=False):
+        self.model = model
+        self.optim = optim
+        g = optim.param_groups[0]
+        if not isinstance(optim, torch.optim.Adam) or g.get("weight_decay", 0) != 0 or \
+                g.get("amsgrad", False) or g.get("maximize", False):
+            raise NotImplementedError("fused update implements torch.optim.Adam "
+                                      "(main.py:106: Adam(lr), no weight decay / amsgrad)")
+        self.ctx = _context(model)
+
+    def _sync_optimizer_state(self):
+        ctx = self.ctx
+        for p, mv, vv in zip(self.model.parameters(), split_views(ctx.m[:ctx.P]),
+                             split_views(ctx.v[:ctx.P])):
+            self.optim.state[p] = {"step": torch.tensor(float(ctx.step)), "exp_avg": mv,
+                                   "exp_avg_sq": vv}
+
+    def update_model(self, ups):
+        """agents.py:9-21: install the aggregated gradient, Adam step, clear .grad."""
+        ctx = self.ctx
+        g = self.optim.param_groups[0]
+        eng = ctx.engine
+        if isinstance(ups, _LazyMean):
+            entries = [u[0] for u in ups.ups_list]
+            bases = [e.untyped_storage().data_ptr() for e in entries]
+            first = bases[0]
+            c = 0
+            while c < len(bases) and bases[c] == first:
+                c += 1
+            stale = []
+            for e, b in zip(entries[c:], bases[c:]):
+                if b == first:
+                    raise NotImplementedError("fused rule: fresh entries after stale ones")
+                stale.append(_flat_of(e, ctx))
+            S = _flat_of(entries[0], ctx)
+        else:
+            if len(ups) != len(PN1_SIZES):
+                raise IndexError("list index out of range")
+            S = torch.cat([u.detach().reshape(-1).float() for u in ups])
+            S = torch.nn.functional.pad(S, (0, padded(ctx.P) - ctx.P))
+            c, stale = 1, []
+        ctx.step += 1
+        eng.aggregate_adam(S, c, stale, ctx.theta, ctx.m, ctx.v, ctx.step, lr=g["lr"],
+                           betas=g["betas"], eps=g["eps"])
+        for p in self.model.parameters():        # optim.zero_grad() (set_to_none, torch >= 2)
+            p.grad = None
+        self._sync_optimizer_state()
+        ctx.new_epoch()
+
+    def init_adv(self, model):
+        self.adv = model
+
+
+def _flat_of(view, ctx):
+    """The flat gradient buffer a returned .grad view belongs to."""
+    st = view.untyped_storage()
+    n = st.nbytes() // 4
+    flat = torch.empty(0, device=ctx.device).set_(st, 0, (n,), (1,))
+    if n < ctx.P:
+        raise ValueError("gradient entry is not a flsim gradient buffer")
+    return flat
+
+
+class Worker:
+    """agents.py:27-40."""
+
+    def __init__(self, loss, key=None):
+        self.model = None
+        self.loss = loss
+        self.index = next(_WORKER_IDS)    # creation order == worker_list index (main.py:112-113)
+
+    def fwd_bkwd(self, inp, outp):
+        if not isinstance(self.loss, torch.nn.CrossEntropyLoss) or \
+                getattr(self.loss, "reduction", "mean") != "mean":
+            raise NotImplementedError("fused loss implements nn.CrossEntropyLoss(mean)")
+        ctx = _context(self.model)
+        n = int(inp.shape[0])
+        ctx.ensure_capacity(n)
+        eng = ctx.engine
+        theta = ctx.theta
+        if not ctx.packed:
+            eng.begin_epoch(theta)
+            ctx.packed = True
+        if ctx.G is None:
+            ctx.G = torch.zeros(padded(ctx.P), device=ctx.device)
+        recs = [(ctx.t, self.index, 0)] * (n // 128)
+        wt = worker_table(recs, ctx.device)
+        lb = ctx.loss_buf[:n // 128]
+        eng.run_input(theta, inp.to(ctx.device, torch.float32), outp.to(ctx.device), wt,
+                      ctx.seed, self.model.training, lb)
+        eng.end_epoch(ctx.G)                     # running sum of the epoch's gradients
+        grads = split_views(ctx.G[:ctx.P])
+        for p, gv in zip(self.model.parameters(), grads):
+            p.grad = gv                          # agents.py:35: accumulated in place
+        lossval = lb.mean().detach().cpu().numpy()
+        return list(grads), lossval.astype(np.float32)
+
+
+class Agg:
+    """agents.py:43-45."""
+
+    def __init__(self, rule):
+        self.rule = rule
