@@ -164,3 +164,67 @@ def test_simulation_matches_oracle_trajectory(pool, thr):
         assert abs(lg - lo) <= (1e-4 if t == 0 else 1e-3), (t, lg, lo)
     th = gsim.theta.cpu().numpy()
     assert _rel_l2(th.astype(np.float64), osim.theta.astype(np.float64)) < 1e-3
+
+
+def test_reference_api_facade_loop(pool):
+    """The reference's own loop structure (main.py:126-188) written against the drop-in FL.agents
+    API (Worker.fwd_bkwd / Agg(rule) / Central.update_model), fed the spec's batches, against
+    the oracle: same losses (tolerance), same aliasing (every fast entry is the same buffer)."""
+    import torch.nn as nn
+    from FL.agents import Agg, Central, Worker, rule
+    from FL.models import PerformantNet1
+    from oracle import model_ref as MR
+    from oracle import oracle as O
+    n, d, ep = 4, 2, 4
+    osim = MR.OracleSim(n, delay=d, throttle=True, pool=pool)
+    torch.manual_seed(0)
+    model = PerformantNet1().to(DEV)
+    optimizer = torch.optim.Adam(model.parameters(), lr=0.001)
+    central = Central(model, optimizer)
+    workers = [Worker(nn.CrossEntropyLoss()) for _ in range(n)]
+    for i, w in enumerate(workers):
+        w.index = i
+    agg = Agg(rule)
+    rs = np.random.RandomState(0)
+    lists = O.class_lists(pool[1])
+    lut = O.normalize_lut()
+    pesky, window, gone = [], 0, False
+    for t in range(ep):
+        weight_ups, losses = [], []
+        model.train()
+        for i in range(n):
+            k = rs.randint(0, n)
+            idx = O.batch_indices(0, t, i, k, n, lists)
+            x = torch.from_numpy(lut[pool[0][idx]]).to(DEV)
+            y = torch.from_numpy(pool[1][idx]).to(DEV)
+            if i == n - 1:
+                gone = False
+                ups = None
+                if t == 0:
+                    workers[i].model = central.model
+                    ups, _ = workers[i].fwd_bkwd(x, y)
+                    pesky.append(ups)
+                    ups = None
+                elif t % d == 0:
+                    workers[i].model = central.model
+                    ups, _ = workers[i].fwd_bkwd(x, y)
+                    pesky.append(ups)
+                    ups = pesky.pop(0)
+                if ups is not None:
+                    weight_ups.append(ups)
+                    gone = True
+            elif window <= 0:
+                workers[i].model = central.model
+                ups, lv = workers[i].fwd_bkwd(x, y)
+                weight_ups.append(ups)
+                losses.append(lv)
+                window = 1 if gone else 2
+            if window > 0:
+                window -= 1
+        fin = agg.rule(weight_ups)
+        central.update_model(fin)
+        lo = osim.epoch()
+        assert abs(float(np.mean(losses)) - lo) <= (1e-4 if t == 0 else 1e-3), (t, lo)
+        assert len({u[0].data_ptr() for u in weight_ups[:len(losses)]}) == 1
+    th = torch.cat([p.detach().reshape(-1) for p in model.parameters()]).cpu().numpy()
+    assert _rel_l2(th.astype(np.float64), osim.theta.astype(np.float64)) < 1e-3
