@@ -800,12 +800,13 @@ long flsim_pn1_gradstate_bytes(void) { return gs_layout(nullptr).total_floats * 
 long flsim_pn1_workspace_bytes(int max_samples) { return ws_layout(nullptr, max_samples).bytes; }
 
 int flsim_pn1_workspace_offset(int which, int samples, long* offset_bytes) {
-    WS w = ws_layout(nullptr, samples);
+    char* const fake = reinterpret_cast<char*>(4096);   // layout only; never dereferenced
+    WS w = ws_layout(fake, samples);
     const void* p[] = {w.x0, w.a1, w.a2, w.d1, w.a3, w.a4, w.d2, w.a5, w.a6, w.d3,
                        w.e1, w.e2, w.dh1, w.dh2, w.gx, w.gy, w.loss_s, w.dlog, w.y,
                        w.i1, w.i2, w.i3};
     FLSIM_REQUIRE(which >= 0 && which < (int)(sizeof(p) / sizeof(p[0])), "bad workspace id %d", which);
-    *offset_bytes = (long)(const char*)p[which];
+    *offset_bytes = (long)((const char*)p[which] - fake);
     return 0;
 }
 

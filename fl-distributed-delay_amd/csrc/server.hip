@@ -131,11 +131,30 @@ __device__ __forceinline__ float row_sum_rep(float x, const float (&y)[MAX_STALE
     return ps[0];
 }
 
+// Correctly rounded fp32 sqrt.  v_sqrt_f32 is within 1 ulp; the exact residuals x - s'*s of the
+// two neighbours s' = s -/+ 1 ulp (single-rounding fma: its sign is exact) pick the correctly
+// rounded root.  Tiny inputs are scaled by 2^32 (root by 2^-16) so the residuals stay normal.
+__device__ __forceinline__ float sqrt_rn(float x) {
+    const bool tiny = x < 0x1p-96f;
+    const float xs = tiny ? x * 0x1p+32f : x;
+    float s = __builtin_amdgcn_sqrtf(xs);
+    const int si = __float_as_int(s);
+    const float s_dn = __int_as_float(si - 1);
+    const float s_up = __int_as_float(si + 1);
+    const float r_dn = __fmaf_rn(-s_dn, s, xs);
+    const float r_up = __fmaf_rn(-s_up, s, xs);
+    s = (r_dn <= 0.f) ? s_dn : s;
+    s = (r_up > 0.f) ? s_up : s;
+    s = tiny ? s * 0x1p-16f : s;
+    // 0, +inf and NaN pass through unchanged (the correction above is only for finite x > 0)
+    return (xs == 0.f || xs == __builtin_inff() || xs != xs) ? x : s;
+}
+
 __device__ __forceinline__ void adam_elem(const AggArgs& A, float g, float& p, float& m, float& v) {
     const float mi = __fmaf_rn(A.w1, g - m, m);
     float vi = v * A.b2;
     vi = __fmaf_rn(A.w2 * g, g, vi);
-    const float den = __fdiv_rn(__fsqrt_rn(vi), A.bc2s) + A.eps;
+    const float den = __fdiv_rn(sqrt_rn(vi), A.bc2s) + A.eps;
     p = p + __fdiv_rn(A.neg_ss * mi, den);
     m = mi;
     v = vi;
