@@ -90,6 +90,36 @@ class FLSimulation:
         return self.free_slots.pop() if self.free_slots else \
             torch.empty(self.Ppad, device=self.device)
 
+    def _worker_table(self, t, workers, ks):
+        """WorkerRec (t, i, k, 0) of this rank's computing workers, copied host->device from a
+        pinned staging buffer (asynchronous: the host never waits for the GPU here)."""
+        n = len(workers)
+        if getattr(self, "_wt_cap", 0) < max(1, n):
+            cap = max(1, n)
+            pin = self.device.type == "cuda"
+            self._wt_host = [torch.empty((cap, 4), dtype=torch.int32, pin_memory=pin)
+                             for _ in range(2)]
+            self._wt_dev = torch.empty((cap, 4), dtype=torch.int32, device=self.device)
+            self._wt_ev = [None, None]
+            self._wt_cap = cap
+            self._wt_i = 0
+        j = self._wt_i = self._wt_i ^ 1
+        if self._wt_ev[j] is not None:
+            self._wt_ev[j].synchronize()          # staging buffer j free again (2 epochs ago)
+        h = self._wt_host[j][:n].numpy()
+        h[:, 0] = t
+        h[:, 1] = workers
+        h[:, 2] = ks[workers]
+        h[:, 3] = 0
+        dev = self._wt_dev[:n]
+        if n:
+            dev.copy_(self._wt_host[j][:n], non_blocking=True)
+        if self.device.type == "cuda":
+            ev = torch.cuda.Event()
+            ev.record()
+            self._wt_ev[j] = ev
+        return dev
+
     def shard(self, active):
         lo = (len(active) * self.rank) // self.world
         hi = (len(active) * (self.rank + 1)) // self.world
@@ -110,12 +140,11 @@ class FLSimulation:
             losses.zero_()
         eng.begin_epoch(self.theta)
         cw = eng.chunk_workers
+        wt = self._worker_table(t, active[lo:hi], ks)      # one async upload per epoch
         for c0 in range(lo, hi, cw):
             c1 = min(hi, c0 + cw)
-            recs = [(t, int(i), int(ks[i])) for i in active[c0:c1]]
-            wt = worker_table(recs, self.device)
-            eng.run_chunk(self.theta, self.pool, wt, c1 - c0, self.n, self.seed, self.dropout,
-                          losses[c0:c1])
+            eng.run_chunk(self.theta, self.pool, wt[c0 - lo:c1 - lo], c1 - c0, self.n, self.seed,
+                          self.dropout, losses[c0:c1])
         eng.end_epoch(S)
         if self.world > 1:
             torch.distributed.all_reduce(self.comm[:self.Ppad + len(active)], group=self.group)
