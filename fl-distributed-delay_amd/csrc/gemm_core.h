@@ -88,7 +88,8 @@ constexpr int tile_floats() {
 
 template <int FM, int FN, int WAVES_M, int WAVES_N, class AL, class BL, class EPI>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N)
-gemm_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split) {
+gemm_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, int tiles_m,
+            int tiles_n) {
     constexpr int BM = 16 * FM * WAVES_M;
     constexpr int BN = 16 * FN * WAVES_N;
     static_assert(AL::ROWS == BM, "A loader rows != BM");
@@ -102,9 +103,20 @@ gemm_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split) {
     const int wave = tid >> 6;
     const int wm = wave / WAVES_N;
     const int wn = wave % WAVES_N;
-    const int m0 = blockIdx.x * BM;
-    const int n0 = blockIdx.y * BN;
-    const int ks0 = blockIdx.z * ksteps_per_split;
+    // 1-D grid.  Hardware deals block b to XCD (b % 8); remap so that each XCD gets a contiguous
+    // range of logical tiles, ordered n-tile fastest, then m-tile, then split: the tiles that
+    // share an operand panel (all n-tiles of an m-tile; all tiles of a K split) share one L2.
+    const int gx = tiles_m, gy = tiles_n;
+    const int nb = gridDim.x;
+    const int b = blockIdx.x;
+    const int q = nb / 8, r = nb % 8, xcd = b % 8;
+    const int L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
+    const int tn = L % gy;
+    const int tm = (L / gy) % gx;
+    const int tz = L / (gx * gy);
+    const int m0 = tm * BM;
+    const int n0 = tn * BN;
+    const int ks0 = tz * ksteps_per_split;
     int ks1 = ks0 + ksteps_per_split;
     if (ks1 > ksteps_total) ks1 = ksteps_total;
 
@@ -117,6 +129,7 @@ gemm_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    float asum = 0.f;
     f32x4 ra[AL::UNITS];
     f32x4 rb[BL::UNITS];
     constexpr int BUF = A_FL + B_FL;
@@ -137,6 +150,15 @@ gemm_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split) {
         }
         const float* A = lds + cur * BUF;
         const float* B = A + A_FL;
+        if constexpr (EPI::ASUM) {
+            // bias gradient fused into the weight gradient: column sums of the KM dZ tile
+            // (rows = reduction index), accumulated by the n-tile-0 blocks in K order
+            static_assert(!AL::KC, "ASUM needs a k-major A tile");
+            if (tn == 0 && tid < BM) {
+#pragma unroll
+                for (int k = 0; k < GK; ++k) asum += A[k * KMTile<BM>::STRIDE + tid];
+            }
+        }
         f32x4 af[FM], bf[FN];
 #pragma unroll
         for (int i = 0; i < FM; ++i) af[i] = read_frag<AL::KC, BM>(A, wm * 16 * FM + 16 * i, lane);
@@ -156,6 +178,9 @@ gemm_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split) {
         cur ^= 1;
     }
 
+    if constexpr (EPI::ASUM) {
+        if (tn == 0 && tid < BM) epi.asum(m0 + tid, tz, asum);
+    }
     // epilogue: lane holds rows 4*(lane>>4)+r, col lane&15 of each 16x16 tile
 #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -163,7 +188,7 @@ gemm_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split) {
         for (int j = 0; j < FN; ++j) {
             const int m = m0 + wm * 16 * FM + 16 * i + 4 * (lane >> 4);
             const int n = n0 + wn * 16 * FN + 16 * j + (lane & 15);
-            epi.apply4(m, n, acc[i][j]);
+            epi.apply4(m, n, tz, acc[i][j]);
         }
 }
 

@@ -215,10 +215,11 @@ struct Im2colKM {
 // ---------------------------------------------------------------------------------------------
 // conv forward: Y[m][n] = relu(acc + bias[n])  (NHWC, row length N)
 struct EpiBiasRelu {
+    static constexpr bool ASUM = false;
     float* Y;
     const float* bias;
     int M, N;
-    __device__ void apply4(int m, int n, f32x4 v) const {
+    __device__ void apply4(int m, int n, int z, f32x4 v) const {
         if (n >= N) return;
         const float b = bias[n];
 #pragma unroll
@@ -230,10 +231,11 @@ struct EpiBiasRelu {
 // data gradient: Y[m][n] = acc * (act[m][n] > 0)  (MASK) or acc
 template <bool MASK>
 struct EpiMask {
+    static constexpr bool ASUM = false;
     float* Y;
     const float* act;
     int M, N;
-    __device__ void apply4(int m, int n, f32x4 v) const {
+    __device__ void apply4(int m, int n, int z, f32x4 v) const {
         if (n >= N) return;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -248,11 +250,12 @@ struct EpiMask {
 
 // gradient of a dropout(relu(.)) output: Y = acc * scale * (act > 0)  (act = dropped output)
 struct EpiDropMask {
+    static constexpr bool ASUM = false;
     float* Y;
     const float* act;
     float scale;
     int M, N;
-    __device__ void apply4(int m, int n, f32x4 v) const {
+    __device__ void apply4(int m, int n, int z, f32x4 v) const {
         if (n >= N) return;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -263,14 +266,20 @@ struct EpiDropMask {
     }
 };
 
-// split-K partial slab, accumulated across chunks: S[z][m][n] += acc   (one owner per element)
+// split-K partial slab, accumulated across chunks: S[z][m][n] += acc   (one owner per element);
+// with Bsl != nullptr also the bias gradient Bsl[z][m] += column sum of the dZ tile (ASUM)
 struct EpiSlabAcc {
+    static constexpr bool ASUM = true;
     float* S;
     int M, N;
     long zstride;
-    __device__ void apply4(int m, int n, f32x4 v) const {
+    float* Bsl;
+    __device__ void asum(int m, int z, float v) const {
+        if (Bsl && m < M) Bsl[(long)z * M + m] += v;
+    }
+    __device__ void apply4(int m, int n, int z, f32x4 v) const {
         if (n >= N) return;
-        float* base = S + blockIdx.z * zstride;
+        float* base = S + z * zstride;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
             if (m + r < M) base[(long)(m + r) * N + n] += v[r];
@@ -279,12 +288,13 @@ struct EpiSlabAcc {
 
 // split-K partial, overwritten: S[z][m][n] = acc
 struct EpiSlabStore {
+    static constexpr bool ASUM = false;
     float* S;
     int M, N;
     long zstride;
-    __device__ void apply4(int m, int n, f32x4 v) const {
+    __device__ void apply4(int m, int n, int z, f32x4 v) const {
         if (n >= N) return;
-        float* base = S + blockIdx.z * zstride;
+        float* base = S + z * zstride;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
             if (m + r < M) base[(long)(m + r) * N + n] = v[r];

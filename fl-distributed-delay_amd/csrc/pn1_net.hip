@@ -264,51 +264,6 @@ k_head_wgrad(const float* __restrict__ dlog, const float* __restrict__ e2, float
     if (k == 0) slab_b[z * 10 + j] += accb;
 }
 
-// bias gradient: column sums of dz [M][C], accumulated into slab[z][C].  Block z sums rows
-// [z*per, (z+1)*per); RP = 256 / C row phases in parallel, combined in a fixed order via LDS.
-__global__ void __launch_bounds__(256)
-k_colsum_acc(const float* __restrict__ dz, long M, int C, float* __restrict__ slab, int Z) {
-    __shared__ float sh[256];
-    const int z = blockIdx.x;
-    const long per = (M + Z - 1) / Z;
-    const long r0 = z * per;
-    const long r1 = min(M, r0 + per);
-    const int t = threadIdx.x;
-    if (C <= 256) {
-        const int RP = 256 / C;
-        const int c = t % C, rp = t / C;
-        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-        if (rp < RP) {
-            long r = r0 + rp;
-            for (; r + 3 * RP < r1; r += 4 * RP) {
-                a0 += dz[r * C + c];
-                a1 += dz[(r + RP) * C + c];
-                a2 += dz[(r + 2 * RP) * C + c];
-                a3 += dz[(r + 3 * RP) * C + c];
-            }
-            for (; r < r1; r += RP) a0 += dz[r * C + c];
-        }
-        sh[t] = (a0 + a1) + (a2 + a3);
-        __syncthreads();
-        if (t < C) {
-            float acc = sh[t];
-            for (int q = 1; q < RP; ++q) acc += sh[q * C + t];
-            slab[(long)z * C + t] += acc;
-        }
-    } else {
-        for (int c = t; c < C; c += 256) {
-            float a0 = 0.f, a1 = 0.f;
-            long r = r0;
-            for (; r + 1 < r1; r += 2) {
-                a0 += dz[r * C + c];
-                a1 += dz[(r + 1) * C + c];
-            }
-            if (r < r1) a0 += dz[r * C + c];
-            slab[(long)z * C + c] += a0 + a1;
-        }
-    }
-}
-
 // =============================================================================================
 // per-epoch weight packing (theta in torch layout -> kernel layouts)
 // =============================================================================================
@@ -393,11 +348,12 @@ static int launch_gemm(const AL& al, const BL& bl, const EPI& epi, int M, int N,
                        hipStream_t st, int kid, double alg_flops) {
     constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
     const int per = (ksteps + Z - 1) / Z;
-    dim3 grid(ceil_div(M, BM), ceil_div(N, BN), Z);
+    const int tm = ceil_div(M, BM), tn = ceil_div(N, BN);
+    dim3 grid(tm * tn * Z);
     const bool probe = g_probe.on && g_probe.used < g_probe.cap;
     if (probe) FLSIM_CHECK_HIP(hipEventRecord(g_probe.ev[2 * g_probe.used], st));
     hipLaunchKernelGGL((gemm_kernel<FM, FN, WM, WN, AL, BL, EPI>), grid, dim3(64 * WM * WN), 0, st,
-                       al, bl, epi, ksteps, per);
+                       al, bl, epi, ksteps, per, tm, tn);
     FLSIM_LAUNCH_CHECK();
     if (probe) {
         FLSIM_CHECK_HIP(hipEventRecord(g_probe.ev[2 * g_probe.used + 1], st));
@@ -429,8 +385,8 @@ static int conv_like(const float* X, int S, const float* Wpk, int N, int KP, con
 
 // weight gradient: slab[z][co][kk] += sum_p dz[p][co] * im2col(X)[p][kk]
 template <int IH, int IW, int CI, int FM, int FN, int WM, int WN>
-static int conv_wgrad(const float* dz, const float* X, int S, int CO, int KP, float* slab, int Z,
-                      hipStream_t st, int kid, int kreal) {
+static int conv_wgrad(const float* dz, const float* X, int S, int CO, int KP, float* slab,
+                      float* bslab, int Z, hipStream_t st, int kid, int kreal) {
     constexpr int NT = 64 * WM * WN;
     constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
     using AL = RowsKM<BM, NT>;
@@ -444,7 +400,7 @@ static int conv_wgrad(const float* dz, const float* X, int S, int CO, int KP, fl
     BL bl;
     bl.X = X;
     bl.M = M;
-    EpiSlabAcc epi{slab, CO, KP, (long)CO * KP};
+    EpiSlabAcc epi{slab, CO, KP, (long)CO * KP, bslab};
     return launch_gemm<FM, FN, WM, WN>(al, bl, epi, CO, KP, ceil_div(M, GK), Z, st, kid,
                                        2.0 * M * CO * kreal);
 }
@@ -465,7 +421,6 @@ static const long P_OFF[18] = {0,       1296,    1344,    22080,   22128,   6360
                                63696,   146640,  146736,  312624,  312816,  644592,
                                644784,  5461680, 5462192, 5593264, 5593520, 5596080};
 constexpr long P_TOTAL = 5596090;
-constexpr int ZB = 256;     // bias colsum split
 constexpr int ZL1F = 4;     // linear1 forward split-K
 constexpr int ZL1W = 4;     // linear1 wgrad split
 constexpr int ZL2W = 64;    // linear2 wgrad split
@@ -476,11 +431,11 @@ struct GradState {
     float* wf[6];
     float* wd[6];  // wd[0] unused
     float* sw[6];  // conv weight slabs [ZW][CO][KP]
-    float* sb[6];  // conv bias slabs [ZB][CO]
+    float* sb[6];  // conv bias slabs [ZW][CO] (fused into the weight-gradient GEMM)
     float* l1w;    // [ZL1W][512][9408]
-    float* l1b;    // [ZB][512]
+    float* l1b;    // [ZL1W][512]
     float* l2w;    // [ZL2W][256][512]
-    float* l2b;    // [ZB][256]
+    float* l2b;    // [ZL2W][256]
     float* l3w;    // [ZH][10][256]
     float* l3b;    // [ZH][10]
     float* slab_begin;
@@ -504,12 +459,12 @@ static GradState gs_layout(float* base) {
     g.slab_begin = base ? base + o : nullptr;
     for (int l = 0; l < 6; ++l) {
         g.sw[l] = take((long)GEO[l].ZW * GEO[l].CO * GEO[l].KP);
-        g.sb[l] = take((long)ZB * GEO[l].CO);
+        g.sb[l] = take((long)GEO[l].ZW * GEO[l].CO);
     }
     g.l1w = take((long)ZL1W * 512 * 9408);
-    g.l1b = take((long)ZB * 512);
+    g.l1b = take((long)ZL1W * 512);
     g.l2w = take((long)ZL2W * 256 * 512);
-    g.l2b = take((long)ZB * 256);
+    g.l2b = take((long)ZL2W * 256);
     g.l3w = take((long)ZH * 10 * 256);
     g.l3b = take((long)ZH * 10);
     g.slab_floats = o - slab0;
@@ -647,10 +602,8 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
         al.P = w.dh2; al.ld = 256; al.NK = S; al.NC = 256;
         RowsKM<128, NT> bl{};
         bl.P = w.e1; bl.ld = 512; bl.NK = S; bl.NC = 512;
-        EpiSlabAcc epi{g.l2w, 256, 512, 256L * 512};
+        EpiSlabAcc epi{g.l2w, 256, 512, 256L * 512, g.l2b};
         RC((launch_gemm<4, 4, 2, 2>(al, bl, epi, 256, 512, ceil_div(S, GK), ZL2W, st, K_L2W, 2.0 * S * 256 * 512)));
-        hipLaunchKernelGGL(k_colsum_acc, dim3(ZB), dim3(256), 0, st, w.dh2, (long)S, 256, g.l2b, ZB);
-        FLSIM_LAUNCH_CHECK();
         RowsKC<64, NT> dl{};
         dl.P = w.dh2; dl.ld = 256; dl.NR = S;
         RowsKM<64, NT> wl{};
@@ -665,10 +618,8 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
         al.P = w.dh1; al.ld = 512; al.NK = S; al.NC = 512;
         RowsKM<128, NT> bl{};
         bl.P = w.d3; bl.ld = 9408; bl.NK = S; bl.NC = 9408;
-        EpiSlabAcc epi{g.l1w, 512, 9408, 512L * 9408};
+        EpiSlabAcc epi{g.l1w, 512, 9408, 512L * 9408, g.l1b};
         RC((launch_gemm<4, 4, 2, 2>(al, bl, epi, 512, 9408, ceil_div(S, GK), ZL1W, st, K_L1W, 2.0 * S * 512 * 9408)));
-        hipLaunchKernelGGL(k_colsum_acc, dim3(ZB), dim3(256), 0, st, w.dh1, (long)S, 512, g.l1b, ZB);
-        FLSIM_LAUNCH_CHECK();
         RowsKC<128, NT> dl{};
         dl.P = w.dh1; dl.ld = 512; dl.NR = S;
         RowsKM<128, NT> wl{};
@@ -685,16 +636,12 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     }
     float* dz6 = w.a6;
     // ---- conv6: wgrad (input a5), bias, dgrad -> dz5 = . * (a5 > 0) into gx ----
-    RC((conv_wgrad<13, 13, 192, 3, 3, 2, 3>(dz6, w.a5, S, 192, 1728, g.sw[5], GEO[5].ZW, st, K_WG6, 1728)));
-    hipLaunchKernelGGL(k_colsum_acc, dim3(ZB), dim3(256), 0, st, dz6, (long)S * 225, 192, g.sb[5], ZB);
-    FLSIM_LAUNCH_CHECK();
+    RC((conv_wgrad<13, 13, 192, 3, 3, 2, 3>(dz6, w.a5, S, 192, 1728, g.sw[5], g.sb[5], GEO[5].ZW, st, K_WG6, 1728)));
     RC((conv_like<15, 15, 192, 0, 4, 3, 2, 2>(dz6, S, g.wd[5], 192, 1728,
         EpiMask<true>{w.gx, w.a5, S * 13 * 13, 192}, st, K_DG6, 1728)));
     float* dz5 = w.gx;
     // ---- conv5: wgrad (input d2), bias, dgrad -> grad wrt d2 (dropout site 2) into gy ----
-    RC((conv_wgrad<11, 11, 96, 3, 3, 2, 3>(dz5, w.d2, S, 192, 864, g.sw[4], GEO[4].ZW, st, K_WG5, 864)));
-    hipLaunchKernelGGL(k_colsum_acc, dim3(ZB), dim3(256), 0, st, dz5, (long)S * 169, 192, g.sb[4], ZB);
-    FLSIM_LAUNCH_CHECK();
+    RC((conv_wgrad<11, 11, 96, 3, 3, 2, 3>(dz5, w.d2, S, 192, 864, g.sw[4], g.sb[4], GEO[4].ZW, st, K_WG5, 864)));
     RC((conv_like<13, 13, 192, 0, 4, 3, 2, 2>(dz5, S, g.wd[4], 96, 1728,
         EpiDropMask{w.gy, w.d2, s25, S * 11 * 11, 96}, st, K_DG5, 1728)));
     {
@@ -705,16 +652,12 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     }
     float* dz4 = w.a4;
     // ---- conv4: wgrad (input a3), bias, dgrad -> dz3 = . * (a3 > 0) into gx ----
-    RC((conv_wgrad<20, 20, 96, 3, 3, 2, 3>(dz4, w.a3, S, 96, 864, g.sw[3], GEO[3].ZW, st, K_WG4, 864)));
-    hipLaunchKernelGGL(k_colsum_acc, dim3(ZB), dim3(256), 0, st, dz4, (long)S * 484, 96, g.sb[3], ZB);
-    FLSIM_LAUNCH_CHECK();
+    RC((conv_wgrad<20, 20, 96, 3, 3, 2, 3>(dz4, w.a3, S, 96, 864, g.sw[3], g.sb[3], GEO[3].ZW, st, K_WG4, 864)));
     RC((conv_like<22, 22, 96, 0, 4, 3, 2, 2>(dz4, S, g.wd[3], 96, 864,
         EpiMask<true>{w.gx, w.a3, S * 20 * 20, 96}, st, K_DG4, 864)));
     float* dz3 = w.gx;
     // ---- conv3: wgrad (input d1), bias, dgrad -> grad wrt d1 (site 1) into gy ----
-    RC((conv_wgrad<18, 18, 48, 3, 3, 2, 3>(dz3, w.d1, S, 96, 432, g.sw[2], GEO[2].ZW, st, K_WG3, 432)));
-    hipLaunchKernelGGL(k_colsum_acc, dim3(ZB), dim3(256), 0, st, dz3, (long)S * 400, 96, g.sb[2], ZB);
-    FLSIM_LAUNCH_CHECK();
+    RC((conv_wgrad<18, 18, 48, 3, 3, 2, 3>(dz3, w.d1, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW, st, K_WG3, 432)));
     RC((conv_like<20, 20, 96, 0, 4, 3, 4, 1>(dz3, S, g.wd[2], 48, 864,
         EpiDropMask{w.gy, w.d1, s25, S * 18 * 18, 48}, st, K_DG3, 864)));
     {
@@ -725,16 +668,12 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     }
     float* dz2 = w.a2;
     // ---- conv2: wgrad (input a1), bias, dgrad -> dz1 = . * (a1 > 0) into gx ----
-    RC((conv_wgrad<34, 34, 48, 3, 3, 1, 3>(dz2, w.a1, S, 48, 432, g.sw[1], GEO[1].ZW, st, K_WG2, 432)));
-    hipLaunchKernelGGL(k_colsum_acc, dim3(ZB), dim3(256), 0, st, dz2, (long)S * 1296, 48, g.sb[1], ZB);
-    FLSIM_LAUNCH_CHECK();
+    RC((conv_wgrad<34, 34, 48, 3, 3, 1, 3>(dz2, w.a1, S, 48, 432, g.sw[1], g.sb[1], GEO[1].ZW, st, K_WG2, 432)));
     RC((conv_like<36, 36, 48, 0, 4, 3, 4, 1>(dz2, S, g.wd[1], 48, 432,
         EpiMask<true>{w.gx, w.a1, S * 34 * 34, 48}, st, K_DG2, 432)));
     float* dz1 = w.gx;
     // ---- conv1: wgrad (input x0), bias ----
-    RC((conv_wgrad<32, 32, 4, 3, 3, 1, 1>(dz1, w.x0, S, 48, 48, g.sw[0], GEO[0].ZW, st, K_WG1, 27)));
-    hipLaunchKernelGGL(k_colsum_acc, dim3(ZB), dim3(256), 0, st, dz1, (long)S * 1156, 48, g.sb[0], ZB);
-    FLSIM_LAUNCH_CHECK();
+    RC((conv_wgrad<32, 32, 4, 3, 3, 1, 1>(dz1, w.x0, S, 48, 48, g.sw[0], g.sb[0], GEO[0].ZW, st, K_WG1, 27)));
     return 0;
 }
 
@@ -886,13 +825,13 @@ int flsim_pn1_end_epoch(void* gradstate, float* grad_out, hipStream_t stream) {
         hipLaunchKernelGGL(k_fin_conv, dim3(ceil_div(n, 256)), dim3(256), 0, stream, g.sw[l], c.ZW,
                            c.CO, c.CI, c.CIP, c.KP, grad_out + P_OFF[2 * l]);
         FLSIM_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_fin_plain, dim3(ceil_div(c.CO, 256)), dim3(256), 0, stream, g.sb[l], ZB,
+        hipLaunchKernelGGL(k_fin_plain, dim3(ceil_div(c.CO, 256)), dim3(256), 0, stream, g.sb[l], c.ZW,
                            (long)c.CO, grad_out + P_OFF[2 * l + 1]);
         FLSIM_LAUNCH_CHECK();
     }
     struct { float* s; int z; long n; long off; } lin[6] = {
-        {g.l1w, ZL1W, 512L * 9408, P_OFF[12]}, {g.l1b, ZB, 512, P_OFF[13]},
-        {g.l2w, ZL2W, 256L * 512, P_OFF[14]},  {g.l2b, ZB, 256, P_OFF[15]},
+        {g.l1w, ZL1W, 512L * 9408, P_OFF[12]}, {g.l1b, ZL1W, 512, P_OFF[13]},
+        {g.l2w, ZL2W, 256L * 512, P_OFF[14]},  {g.l2b, ZL2W, 256, P_OFF[15]},
         {g.l3w, ZH, 2560, P_OFF[16]},          {g.l3b, ZH, 10, P_OFF[17]}};
     for (auto& L : lin) {
         hipLaunchKernelGGL(k_fin_plain, dim3(ceil_div(L.n, 256)), dim3(256), 0, stream, L.s, L.z, L.n,
