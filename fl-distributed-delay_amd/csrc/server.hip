@@ -56,31 +56,7 @@ __device__ __forceinline__ float entry(float x, const float (&y)[MAX_STALE], int
     return r;
 }
 
-// multi_row_sum over rows r = 0..size-1 whose value is entry(first + r*stride)
-__device__ float multi_row_sum_generic(float x, const float (&y)[MAX_STALE], int c, int first,
-                                       int stride, int size) {
-    int lp = ceil_log2_i(size) / 4;
-    if (lp < 4) lp = 4;
-    const int L = 1 << lp;
-    const int mask = L - 1;
-    float a[4] = {0.f, 0.f, 0.f, 0.f};
-    int i = 0;
-    for (; i + L <= size;) {
-        for (int j = 0; j < L; ++j, ++i) a[0] += entry(x, y, c, first + i * stride);
-        for (int j = 1; j < 4; ++j) {
-            a[j] += a[j - 1];
-            a[j - 1] = 0.f;
-            if ((i & (mask << (j * lp))) != 0) break;
-        }
-    }
-    for (; i < size; ++i) a[0] += entry(x, y, c, first + i * stride);
-    a[0] += a[1];
-    a[0] += a[2];
-    a[0] += a[3];
-    return a[0];
-}
-
-// Fast path for the contiguous case (stride 1): the first c entries are all x.  Blocks made only
+// multi_row_sum over k rows whose first c are x and whose rows c.. are y[0..]: blocks made only
 // of x are summed once; whole level-1 / level-2 groups of such blocks likewise.
 __device__ __forceinline__ float multi_row_sum_rep(float x, const float (&y)[MAX_STALE], int c,
                                                    int k) {
@@ -119,11 +95,24 @@ __device__ __forceinline__ float multi_row_sum_rep(float x, const float (&y)[MAX
     return a0;
 }
 
+// row_sum: the k entries viewed as (k/4, 4) -> stream q holds entries 4r+q.  Its first cq rows
+// are S_t copies and the rest are stale entries, so each stream is itself a "c copies then a few
+// others" multi_row_sum (memoised); leftovers (k % 4) go into stream 0, then s0 + s1 + s2 + s3.
 __device__ __forceinline__ float row_sum_rep(float x, const float (&y)[MAX_STALE], int c, int k) {
     const int sz = k / 4;
     float ps[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) ps[q] = multi_row_sum_generic(x, y, c, q, 4, sz);
+    for (int q = 0; q < 4; ++q) {
+        int cq = (c - q + 3) / 4;                 // rows r with 4r + q < c
+        cq = cq < 0 ? 0 : (cq > sz ? sz : cq);
+        float z[MAX_STALE];
+#pragma unroll
+        for (int j = 0; j < MAX_STALE; ++j) {
+            const int i = 4 * (cq + j) + q;      // entry index (>= c when cq + j < sz)
+            z[j] = (cq + j < sz) ? entry(x, y, c, i) : 0.f;
+        }
+        ps[q] = multi_row_sum_rep(x, z, cq, sz);
+    }
     for (int i = sz * 4; i < k; ++i) ps[0] += entry(x, y, c, i);
     ps[0] += ps[1];
     ps[0] += ps[2];
