@@ -413,16 +413,18 @@ struct ConvGeo {
     int KP;              // packed forward K (9*CIP rounded to 16)
     int ZW;              // wgrad split
 };
+// ZW (pixel splits of the weight gradient) sized so each wgrad launch has ~3-6k blocks: several
+// rounds of resident blocks on 256 CUs (no half-empty last round, enough waves per SIMD).
 static const ConvGeo GEO[6] = {
-    {3, 4, 48, 32, 48, 512},   {48, 48, 48, 34, 432, 256},   {48, 48, 96, 18, 432, 256},
-    {96, 96, 96, 20, 864, 128}, {96, 96, 192, 11, 864, 64}, {192, 192, 192, 13, 1728, 48},
+    {3, 4, 48, 32, 48, 4096},    {48, 48, 48, 34, 432, 2048},   {48, 48, 96, 18, 432, 1024},
+    {96, 96, 96, 20, 864, 512},  {96, 96, 192, 11, 864, 256},  {192, 192, 192, 13, 1728, 128},
 };
 static const long P_OFF[18] = {0,       1296,    1344,    22080,   22128,   63600,
                                63696,   146640,  146736,  312624,  312816,  644592,
                                644784,  5461680, 5462192, 5593264, 5593520, 5596080};
 constexpr long P_TOTAL = 5596090;
 constexpr int ZL1F = 4;     // linear1 forward split-K
-constexpr int ZL1W = 4;     // linear1 wgrad split
+constexpr int ZL1W = 8;     // linear1 wgrad split
 constexpr int ZL2W = 64;    // linear2 wgrad split
 constexpr int ZH = 32;      // head wgrad split
 
