@@ -97,10 +97,12 @@ def _grad_checks(g_gpu, g32, g64):
         off += n
         r = _rel_l2(a, b64)
         assert r <= 5e-3, (name, r)
-    # whole gradient: within 1e-4 of |g| (measured: 1e-5 .. 6e-5; the CPU's own fp32 error is
-    # ~4e-6 -- the GPU sums in a different order, which flips a few more ReLU / argmax decisions)
+    # whole gradient: within 2.5e-4 of |g|.  Measured on MI355X: 1e-5 .. 1.2e-4 (1.2e-4 for the
+    # 3-worker chunk); the CPU's own fp32 error is 4e-6 .. 3.4e-5.  The excess is discrete ReLU /
+    # argmax flips at near-zero pre-activations (a different summation order flips different
+    # ones); test_gradient_teacher_forced_decisions pins the arithmetic itself to 2e-5.
     e_gpu = np.linalg.norm(g_gpu - g64)
-    assert e_gpu <= 1e-4 * np.linalg.norm(g64), (e_gpu, np.linalg.norm(g32 - g64))
+    assert e_gpu <= 2.5e-4 * np.linalg.norm(g64), (e_gpu, np.linalg.norm(g32 - g64))
 
 
 @pytest.mark.parametrize("dropout", [False, True])
@@ -254,58 +256,63 @@ def _gather_pool(z, idx_nhwc):
     return z[n, c, rows, cols]
 
 
-@pytest.mark.parametrize("dropout", [False, True])
-def test_gradient_teacher_forced_decisions(pool, dropout):
+@pytest.mark.parametrize("dropout,items", [
+    (False, [(0, 1, 2)]), (True, [(0, 1, 2)]), (True, [(1, 0, 3), (1, 2, 0)])])
+def test_gradient_teacher_forced_decisions(pool, dropout, items):
     """Backward kernels checked tightly: an fp64 reference that takes the GPU's own forward
     decisions (ReLU signs, max-pool argmax, dropout masks) must give the GPU's gradient to fp32
     accumulation accuracy (per-tensor rel-L2 <= 2e-5).  Decision flips at near-zero
-    pre-activations are what the looser rel-L2 <= 5e-3 of test_single_worker_step_gradient covers."""
+    pre-activations are what the looser rel-L2 <= 5e-3 of test_single_worker_step_gradient covers.
+    The two-item case runs both workers as ONE chunk (256 samples): the chunk's gradient must be
+    the sum of the per-worker mean-CE gradients (agents.py:35 accumulation)."""
     import torch.nn.functional as F
     from flsim.data import DevicePool
     from flsim.engine import PN1Engine, PN1_SHAPES, worker_table
     from oracle import model_ref as MR
+    nw = len(items)
+    NS = 128 * nw
     sim = MR.OracleSim(4, delay=2, pool=pool, dropout=dropout)
-    items = [(0, 1, 2)]
-    eng = PN1Engine(DEV, chunk_workers=1)
+    eng = PN1Engine(DEV, chunk_workers=nw)
     dpool = DevicePool(DEV, 0, pool)
     theta = torch.from_numpy(sim.theta.copy()).to(DEV)
     eng.begin_epoch(theta)
-    loss = torch.zeros(1, device=DEV)
-    eng.run_chunk(theta, dpool, worker_table(items, DEV), 1, 4, 0, dropout, loss)
+    loss = torch.zeros(nw, device=DEV)
+    eng.run_chunk(theta, dpool, worker_table(items, DEV), nw, 4, 0, dropout, loss)
     S = torch.zeros(eng.P, device=DEV)
     eng.end_epoch(S)
     torch.cuda.synchronize()
     W = lambda i, shp, dt=torch.float32: eng.workspace_view(i, shp, dt).cpu().numpy()
     nchw = lambda a: torch.from_numpy(np.ascontiguousarray(a.transpose(0, 3, 1, 2)))
-    a1 = nchw(W(1, (128, 34, 34, 48)))
-    d1 = nchw(W(3, (128, 18, 18, 48)))
-    a3 = nchw(W(4, (128, 20, 20, 96)))
-    d2 = nchw(W(6, (128, 11, 11, 96)))
-    a5 = nchw(W(7, (128, 13, 13, 192)))
-    d3 = torch.from_numpy(W(9, (128, 9408)))
-    e1 = torch.from_numpy(W(10, (128, 512)))
-    e2 = torch.from_numpy(W(11, (128, 256)))
-    i1 = W(19, (128, 18, 18, 48), torch.uint8)
-    i2 = W(20, (128, 11, 11, 96), torch.uint8)
-    i3 = W(21, (128, 7, 7, 192), torch.uint8)
-    x, y = sim.batch(*items[0], dtype=torch.float64)
-    noise = MR.dropout_noise(0, items[0][0], items[0][1], 128, torch.float64) if dropout else \
-        [torch.ones(1, dtype=torch.float64)] * 5
+    A = dict(a1=nchw(W(1, (NS, 34, 34, 48))), d1=nchw(W(3, (NS, 18, 18, 48))),
+             a3=nchw(W(4, (NS, 20, 20, 96))), d2=nchw(W(6, (NS, 11, 11, 96))),
+             a5=nchw(W(7, (NS, 13, 13, 192))), d3=torch.from_numpy(W(9, (NS, 9408))),
+             e1=torch.from_numpy(W(10, (NS, 512))), e2=torch.from_numpy(W(11, (NS, 256))),
+             i1=W(19, (NS, 18, 18, 48), torch.uint8), i2=W(20, (NS, 11, 11, 96), torch.uint8),
+             i3=W(21, (NS, 7, 7, 192), torch.uint8))
     P = [torch.tensor(a, requires_grad=True) for a in MR.split_flat(sim.theta.astype(np.float64))]
     (w1, b1, w2, b2, w3, b3, w4, b4, w5, b5, w6, b6, l1w, l1b, l2w, l2b, l3w, l3b) = P
     m = lambda t: (t > 0).to(torch.float64)
-    h = F.conv2d(x, w1, b1, padding=2) * m(a1)
-    h = _gather_pool(F.conv2d(h, w2, b2, padding=2), i1) * m(d1) * noise[0]
-    h = F.conv2d(h, w3, b3, padding=2) * m(a3)
-    h = _gather_pool(F.conv2d(h, w4, b4, padding=2), i2) * m(d2) * noise[1]
-    h = F.conv2d(h, w5, b5, padding=2) * m(a5)
-    h = _gather_pool(F.conv2d(h, w6, b6, padding=2), i3).reshape(128, -1) * m(d3)
-    h = h * noise[2].reshape(128, -1) if dropout else h
     s50 = 2.0 if dropout else 1.0
-    h = F.linear(h, l1w, l1b) * m(e1) * s50
-    h = F.linear(h, l2w, l2b) * m(e2) * s50
-    lref = F.cross_entropy(F.linear(h, l3w, l3b), y)
-    lref.backward()
+    lrefs = []
+    for wi, it in enumerate(items):
+        sl = slice(128 * wi, 128 * (wi + 1))
+        a = {k: v[sl] for k, v in A.items()}
+        x, y = sim.batch(*it, dtype=torch.float64)
+        noise = MR.dropout_noise(0, it[0], it[1], 128, torch.float64) if dropout else None
+        h = F.conv2d(x, w1, b1, padding=2) * m(a["a1"])
+        h = _gather_pool(F.conv2d(h, w2, b2, padding=2), a["i1"]) * m(a["d1"])
+        h = h * noise[0] if dropout else h
+        h = F.conv2d(h, w3, b3, padding=2) * m(a["a3"])
+        h = _gather_pool(F.conv2d(h, w4, b4, padding=2), a["i2"]) * m(a["d2"])
+        h = h * noise[1] if dropout else h
+        h = F.conv2d(h, w5, b5, padding=2) * m(a["a5"])
+        h = _gather_pool(F.conv2d(h, w6, b6, padding=2), a["i3"]).reshape(128, -1) * m(a["d3"])
+        h = h * noise[2].reshape(128, -1) if dropout else h
+        h = F.linear(h, l1w, l1b) * m(a["e1"]) * s50
+        h = F.linear(h, l2w, l2b) * m(a["e2"]) * s50
+        lref = F.cross_entropy(F.linear(h, l3w, l3b), y)
+        lref.backward()
+        lrefs.append(lref.item())
     g = S.cpu().numpy().astype(np.float64)
     off = 0
     worst = {}
@@ -313,5 +320,5 @@ def test_gradient_teacher_forced_decisions(pool, dropout):
         n = p.numel()
         worst[name] = _rel_l2(g[off:off + n], p.grad.reshape(-1).numpy())
         off += n
-    assert abs(loss.item() - lref.item()) < 1e-5
+    np.testing.assert_allclose(loss.cpu().numpy(), lrefs, atol=1e-5)
     assert max(worst.values()) <= 2e-5, worst

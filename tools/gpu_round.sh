@@ -1,0 +1,14 @@
+#!/bin/bash
+# One GPU call: parity tests, a bench line, then the rocprofv3 trace + PMC passes.
+# Usage (repo root, on the GPU box):  bash tools/gpu_round.sh <tag>
+set -u
+TAG=${1:-r01}
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+    > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { echo "pytest failed $?"; tail -30 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
+tail -3 gpurun_out/pytest_gpu_$TAG.log
+timeout -k 10 400 python -u bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err \
+    || { echo "bench failed $?"; tail -20 gpurun_out/bench_$TAG.err; exit 1; }
+cat gpurun_out/bench_$TAG.json
+bash tools/gpu_profile.sh $TAG
