@@ -36,6 +36,21 @@ HBM_PEAK_GBPS = 8000.0           # MI355X_MICROARCH.md: HBM3E spec
 FLOP_PER_WORKER_STEP = 147_641_499_648   # SURVEY 8d (fwd + dgrad + wgrad, B = 128)
 
 
+def _load_traffic():
+    """HBM bytes per launch from the PMC passes of tools/gpu_profile.sh (FETCH_SIZE x 2 per the
+    gfx950 correction + WRITE_SIZE, MI355X_MICROARCH.md), written by tools/pmc_traffic.py into
+    profiles/traffic.json.  {kernel: {"bytes_per_launch": B, "source": "..."}}; {} if absent."""
+    path = os.path.join(REPO, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return {}
+
+
+TRAFFIC = _load_traffic()
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -45,7 +60,8 @@ def parse():
     ap.add_argument("--delay", type=int, default=50)
     ap.add_argument("--no-throttle", action="store_true")
     ap.add_argument("--chunk", type=int, default=32, help="workers per worker-batched launch")
-    ap.add_argument("--cpu-sample", type=int, default=24, help="worker-steps in the CPU sample")
+    ap.add_argument("--cpu-sample", type=int, default=160,
+                    help="worker-steps in the CPU sample (~10-30 s of host work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true")
     return ap.parse_args()
@@ -104,7 +120,6 @@ def main():
         sim.epoch(sync_loss=False)
     torch.cuda.synchronize()
     probe = None if args.no_probe else KernelProbe(capacity=64 * 1024)
-    sim.agg_timing = []
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -126,6 +141,7 @@ def main():
     kern = probe.read() if probe else {}
     if probe:
         probe.close()
+    agg_rec = kern.pop("aggregate_adam", None)
     roofline = None
     if kern:
         name, (cnt, ms, fl) = max(kern.items(), key=lambda kv: kv[1][1])
@@ -133,9 +149,12 @@ def main():
         achieved = fl / cnt / avg_s / 1e12
         gemm_ms = sum(v[1] for v in kern.values())
         gemm_fl = sum(v[2] for v in kern.values())
+        traffic = TRAFFIC.get(name)
         roofline = dict(bound="mfma", kernel=name, achieved=round(achieved, 2),
                         peak=MFMA_F32_PEAK_TFLOPS, unit="TFLOP/s",
-                        frac=round(achieved / MFMA_F32_PEAK_TFLOPS, 4), traffic=None,
+                        frac=round(achieved / MFMA_F32_PEAK_TFLOPS, 4),
+                        traffic=traffic["bytes_per_launch"] if traffic else None,
+                        traffic_source=traffic["source"] if traffic else None,
                         launches=cnt, avg_launch_ms=round(ms / cnt, 4),
                         alg_flop_per_launch=fl / cnt,
                         all_gemms=dict(achieved=round(gemm_fl / (gemm_ms / 1e3) / 1e12, 2),
@@ -144,14 +163,16 @@ def main():
                                             tflops=round(f / (m / 1e3) / 1e12, 1))
                                     for k, (c, m, f) in sorted(kern.items())})
     agg = None
-    if sim.agg_timing:
-        durs = [e0.elapsed_time(e1) for (e0, e1, _) in sim.agg_timing]
-        byts = [b for (_, _, b) in sim.agg_timing]
-        gbps = float(np.mean([b / (d / 1e3) / 1e9 for b, d in zip(byts, durs)]))
-        agg = dict(kernel="k_aggregate_adam", achieved=round(gbps, 1), peak=HBM_PEAK_GBPS,
-                   unit="GB/s", frac=round(gbps / HBM_PEAK_GBPS, 4),
-                   avg_launch_us=round(float(np.mean(durs)) * 1e3, 2),
-                   alg_bytes_per_launch=int(np.mean(byts)), traffic=None)
+    if agg_rec:
+        cnt, ms, byts = agg_rec
+        gbps = byts / (ms / 1e3) / 1e9
+        traffic = TRAFFIC.get("aggregate_adam")
+        agg = dict(kernel="k_aggregate_adam", bound="hbm", achieved=round(gbps, 1),
+                   peak=HBM_PEAK_GBPS, unit="GB/s", frac=round(gbps / HBM_PEAK_GBPS, 4),
+                   launches=cnt, avg_launch_us=round(ms / cnt * 1e3, 2),
+                   alg_bytes_per_launch=int(byts / cnt),
+                   traffic=traffic["bytes_per_launch"] if traffic else None,
+                   traffic_source=traffic["source"] if traffic else None)
 
     value = ws / elapsed
     cpu = None

@@ -14,6 +14,7 @@
 
 #include "loaders.h"
 #include "pn1.h"
+#include "probe.h"
 
 namespace flsim {
 
@@ -320,29 +321,6 @@ __global__ void k_fin_plain(const float* __restrict__ slab, int Z, long n, float
 // =============================================================================================
 // GEMM launch helper
 // =============================================================================================
-// ---- live kernel timing probe (bench.py): HIP events recorded on the launch stream around each
-// GEMM launch, tagged with the launch id and its algorithmic FLOPs ----
-enum KernelId {
-    K_FWD1 = 0, K_FWD2, K_FWD3, K_FWD4, K_FWD5, K_FWD6, K_L1F, K_L2F,
-    K_DG2, K_DG3, K_DG4, K_DG5, K_DG6,
-    K_WG1, K_WG2, K_WG3, K_WG4, K_WG5, K_WG6,
-    K_L1W, K_L1D, K_L2W, K_L2D, K_COUNT
-};
-static const char* KNAME[K_COUNT] = {
-    "conv1_fwd", "conv2_fwd", "conv3_fwd", "conv4_fwd", "conv5_fwd", "conv6_fwd", "linear1_fwd",
-    "linear2_fwd", "conv2_dgrad", "conv3_dgrad", "conv4_dgrad", "conv5_dgrad", "conv6_dgrad",
-    "conv1_wgrad", "conv2_wgrad", "conv3_wgrad", "conv4_wgrad", "conv5_wgrad", "conv6_wgrad",
-    "linear1_wgrad", "linear1_dgrad", "linear2_wgrad", "linear2_dgrad"};
-
-struct Probe {
-    bool on = false;
-    int cap = 0, used = 0;
-    hipEvent_t* ev = nullptr;
-    int* kid = nullptr;
-    double* flops = nullptr;
-};
-static Probe g_probe;
-
 template <int FM, int FN, int WM, int WN, class AL, class BL, class EPI>
 static int launch_gemm(const AL& al, const BL& bl, const EPI& epi, int M, int N, int ksteps, int Z,
                        hipStream_t st, int kid, double alg_flops) {
@@ -350,18 +328,11 @@ static int launch_gemm(const AL& al, const BL& bl, const EPI& epi, int M, int N,
     const int per = (ksteps + Z - 1) / Z;
     const int tm = ceil_div(M, BM), tn = ceil_div(N, BN);
     dim3 grid(tm * tn * Z);
-    const bool probe = g_probe.on && g_probe.used < g_probe.cap;
-    if (probe) FLSIM_CHECK_HIP(hipEventRecord(g_probe.ev[2 * g_probe.used], st));
+    const int slot = probe_begin(st);
     hipLaunchKernelGGL((gemm_kernel<FM, FN, WM, WN, AL, BL, EPI>), grid, dim3(64 * WM * WN), 0, st,
                        al, bl, epi, ksteps, per, tm, tn);
     FLSIM_LAUNCH_CHECK();
-    if (probe) {
-        FLSIM_CHECK_HIP(hipEventRecord(g_probe.ev[2 * g_probe.used + 1], st));
-        g_probe.kid[g_probe.used] = kid;
-        g_probe.flops[g_probe.used] = alg_flops;
-        g_probe.used++;
-    }
-    return 0;
+    return probe_end(slot, st, kid, alg_flops);
 }
 
 // forward conv (also the data-gradient conv): out[m][n] for m < S*OH*OW, n < N
@@ -689,50 +660,6 @@ using namespace flsim;
 extern "C" {
 
 const char* flsim_last_error(void) { return last_error(); }
-
-// Live per-kernel timing of the GEMM launches (bench.py).  capacity = launches to record.
-int flsim_probe_enable(int capacity) {
-    if (g_probe.on) return 0;
-    FLSIM_REQUIRE(capacity > 0, "capacity must be > 0");
-    g_probe.ev = new hipEvent_t[2 * capacity];
-    for (int i = 0; i < 2 * capacity; ++i) FLSIM_CHECK_HIP(hipEventCreate(&g_probe.ev[i]));
-    g_probe.kid = new int[capacity];
-    g_probe.flops = new double[capacity];
-    g_probe.cap = capacity;
-    g_probe.used = 0;
-    g_probe.on = true;
-    return 0;
-}
-
-// Synchronises on the recorded events; per kernel id: launches, total ms, total alg. FLOPs.
-// Resets the record.  Arrays have flsim_probe_kernel_count() entries.
-int flsim_probe_read(int* launches, double* total_ms, double* total_flops) {
-    for (int k = 0; k < K_COUNT; ++k) { launches[k] = 0; total_ms[k] = 0; total_flops[k] = 0; }
-    if (!g_probe.on) return 0;
-    for (int u = 0; u < g_probe.used; ++u) {
-        FLSIM_CHECK_HIP(hipEventSynchronize(g_probe.ev[2 * u + 1]));
-        float ms = 0.f;
-        FLSIM_CHECK_HIP(hipEventElapsedTime(&ms, g_probe.ev[2 * u], g_probe.ev[2 * u + 1]));
-        launches[g_probe.kid[u]] += 1;
-        total_ms[g_probe.kid[u]] += ms;
-        total_flops[g_probe.kid[u]] += g_probe.flops[u];
-    }
-    g_probe.used = 0;
-    return 0;
-}
-
-int flsim_probe_disable(void) {
-    if (!g_probe.on) return 0;
-    for (int i = 0; i < 2 * g_probe.cap; ++i) (void)hipEventDestroy(g_probe.ev[i]);
-    delete[] g_probe.ev;
-    delete[] g_probe.kid;
-    delete[] g_probe.flops;
-    g_probe = Probe();
-    return 0;
-}
-
-int flsim_probe_kernel_count(void) { return K_COUNT; }
-const char* flsim_probe_kernel_name(int kid) { return (kid >= 0 && kid < K_COUNT) ? KNAME[kid] : ""; }
 
 long flsim_pn1_param_count(void) { return P_TOTAL; }
 

@@ -1,0 +1,85 @@
+// Kernel timing probe (probe.h) and its C-ABI (include/flsim.h).
+#include "probe.h"
+
+#include "flsim.h"
+
+namespace flsim {
+
+static const char* KNAME[K_COUNT] = {
+    "conv1_fwd", "conv2_fwd", "conv3_fwd", "conv4_fwd", "conv5_fwd", "conv6_fwd", "linear1_fwd",
+    "linear2_fwd", "conv2_dgrad", "conv3_dgrad", "conv4_dgrad", "conv5_dgrad", "conv6_dgrad",
+    "conv1_wgrad", "conv2_wgrad", "conv3_wgrad", "conv4_wgrad", "conv5_wgrad", "conv6_wgrad",
+    "linear1_wgrad", "linear1_dgrad", "linear2_wgrad", "linear2_dgrad", "aggregate_adam"};
+
+struct Probe {
+    bool on = false;
+    int cap = 0, used = 0;
+    hipEvent_t* ev = nullptr;
+    int* kid = nullptr;
+    double* work = nullptr;
+};
+static Probe g_probe;
+
+int probe_begin(hipStream_t st) {
+    if (!g_probe.on || g_probe.used >= g_probe.cap) return -1;
+    if (hipEventRecord(g_probe.ev[2 * g_probe.used], st) != hipSuccess) return -1;
+    return g_probe.used;
+}
+
+int probe_end(int slot, hipStream_t st, int kid, double work) {
+    if (slot < 0) return 0;
+    FLSIM_CHECK_HIP(hipEventRecord(g_probe.ev[2 * slot + 1], st));
+    g_probe.kid[slot] = kid;
+    g_probe.work[slot] = work;
+    g_probe.used = slot + 1;
+    return 0;
+}
+
+}  // namespace flsim
+
+using namespace flsim;
+
+extern "C" {
+
+int flsim_probe_enable(int capacity) {
+    if (g_probe.on) return 0;
+    FLSIM_REQUIRE(capacity > 0, "capacity must be > 0");
+    g_probe.ev = new hipEvent_t[2 * capacity];
+    for (int i = 0; i < 2 * capacity; ++i) FLSIM_CHECK_HIP(hipEventCreate(&g_probe.ev[i]));
+    g_probe.kid = new int[capacity];
+    g_probe.work = new double[capacity];
+    g_probe.cap = capacity;
+    g_probe.used = 0;
+    g_probe.on = true;
+    return 0;
+}
+
+int flsim_probe_read(int* launches, double* total_ms, double* total_work) {
+    for (int k = 0; k < K_COUNT; ++k) { launches[k] = 0; total_ms[k] = 0; total_work[k] = 0; }
+    if (!g_probe.on) return 0;
+    for (int u = 0; u < g_probe.used; ++u) {
+        FLSIM_CHECK_HIP(hipEventSynchronize(g_probe.ev[2 * u + 1]));
+        float ms = 0.f;
+        FLSIM_CHECK_HIP(hipEventElapsedTime(&ms, g_probe.ev[2 * u], g_probe.ev[2 * u + 1]));
+        launches[g_probe.kid[u]] += 1;
+        total_ms[g_probe.kid[u]] += ms;
+        total_work[g_probe.kid[u]] += g_probe.work[u];
+    }
+    g_probe.used = 0;
+    return 0;
+}
+
+int flsim_probe_disable(void) {
+    if (!g_probe.on) return 0;
+    for (int i = 0; i < 2 * g_probe.cap; ++i) (void)hipEventDestroy(g_probe.ev[i]);
+    delete[] g_probe.ev;
+    delete[] g_probe.kid;
+    delete[] g_probe.work;
+    g_probe = Probe();
+    return 0;
+}
+
+int flsim_probe_kernel_count(void) { return K_COUNT; }
+const char* flsim_probe_kernel_name(int kid) { return (kid >= 0 && kid < K_COUNT) ? KNAME[kid] : ""; }
+
+}  // extern "C"

@@ -1,0 +1,21 @@
+// Live kernel timing for bench.py: HIP events recorded on the launch stream right before and
+// after selected launches (the worker-batched GEMMs and the fused aggregation), tagged with the
+// launch's kernel id and its algorithmic work (FLOPs for the GEMMs, HBM bytes for aggregation).
+#pragma once
+#include "common.h"
+
+namespace flsim {
+
+enum KernelId {
+    K_FWD1 = 0, K_FWD2, K_FWD3, K_FWD4, K_FWD5, K_FWD6, K_L1F, K_L2F,
+    K_DG2, K_DG3, K_DG4, K_DG5, K_DG6,
+    K_WG1, K_WG2, K_WG3, K_WG4, K_WG5, K_WG6,
+    K_L1W, K_L1D, K_L2W, K_L2D, K_AGG, K_COUNT
+};
+
+// slot for the launch that follows, or -1 when the probe is off or full
+int probe_begin(hipStream_t st);
+// records the stop event; returns a C-ABI status
+int probe_end(int slot, hipStream_t st, int kid, double work);
+
+}  // namespace flsim

@@ -15,105 +15,146 @@
 // Compiled with -ffp-contract=off: the only fused multiply-adds are the explicit ones.
 #include "common.h"
 #include "flsim.h"
+#include "probe.h"
 
 namespace flsim {
 
 constexpr int MAX_STALE = 8;
-constexpr int MAX_TAILS = 64;
+constexpr int MAX_TAILS = 8;                  // tail ranges per launch (host splits longer lists)
+constexpr int MAX_EDGE = 4 * (2 * MAX_TAILS + 2);  // 256-element pieces on the element path
+
+// Memoised multi_row_sum of k = c + ns rows whose first c rows are the same value x (S_t) and
+// whose last ns rows are stale entries.  ATen's cascade: 4 accumulators, level step
+// L = 2^lp with lp = max(4, ceil_log2(k) / 4); rows go into acc0; each full block of L rows
+// closes with acc1 += acc0, every L blocks acc2 += acc1, every L^2 blocks acc3 += acc2; the last
+// k % L rows stay in acc0; result acc0 + acc1 + acc2 + acc3.  Blocks made only of x give the
+// same partial sums, so the first nbp = c >> lp blocks are summed once per element (bx = L
+// copies of x, g1 = L copies of bx, ...) and only the remaining < L + ns rows are fed one by one.
+// Every field is uniform, so all control flow below is scalar.
+struct Casc {
+    int c, ns, lp, nb, nbp, q1, q2, q3;
+    int sbase;                      // row_sum streams: stale index of this stream's first stale
+};                                  // row (stride 4); 0 for the plain multi_row_sum
 
 struct AggArgs {
     const float* S;                 // running sum S_t (the c_t fast entries all alias it)
     const float* stale[MAX_STALE];  // stale entries (nullptr = zeros: torch-1.x semantics)
-    int c;                          // copies of S_t
-    int ns;                         // number of stale entries
     float* p;
     float* m;
     float* v;
-    long P;
+    long g0;                        // first float4 group of this launch
+    long lo, hi;                    // element range [lo, hi) of this launch
     int ntail;
-    long tail_lo[MAX_TAILS];        // [lo, hi) element ranges summed with row_sum
-    long tail_hi[MAX_TAILS];
-    float w1, b2, w2, bc2s, eps, neg_ss;
+    int tail_lo[MAX_TAILS];         // [lo, hi) element ranges summed with row_sum
+    int tail_hi[MAX_TAILS];
+    int nedge;                      // blocks 0..nedge-1: 256-element edge pieces starting at
+    long edge_lo[MAX_EDGE];         // edge_lo[b] (the 4 quarters of each edge block)
+    int c, k;
+    Casc main;                      // multi_row_sum over all k rows (tensor body)
+    Casc rs[4];                     // row_sum: stream q = rows 4r + q, r < k / 4 (tensor tail)
+    float w1, b2, w2, bc2s, rbc2s, eps, neg_ss, fk, rk;
 };
 
-__device__ __forceinline__ int ceil_log2_i(int x) {
-    if (x <= 1) return 0;
-    return 32 - __clz(x - 1);
-}
-
-__device__ __forceinline__ float seq_sum(float v, int n) {
-    float a = 0.f;
+template <class T>
+__device__ __forceinline__ T seq_sum(T v, int n) {
+    T a = T(0.f);
     for (int j = 0; j < n; ++j) a += v;
     return a;
 }
 
-// k-entry value for one element: x for i < c, y[i - c] afterwards
-__device__ __forceinline__ float entry(float x, const float (&y)[MAX_STALE], int c, int i) {
-    if (i < c) return x;
+// T = float (one element) or f32x4 (four elements in lock step: the loop and branch overhead
+// of the uniform block structure is paid once per four elements)
+template <int LP, class T = float>
+struct CascAcc {
+    T a0 = T(0.f), a1 = T(0.f), a2 = T(0.f), a3 = T(0.f);
+    int i, lp, L;
+    // the first nbp full blocks, all made of x
+    __device__ __forceinline__ CascAcc(T x, const Casc& C) {
+        lp = LP ? LP : C.lp;
+        L = 1 << lp;
+        T bx = T(0.f);
+        if constexpr (LP != 0) {
+#pragma unroll
+            for (int j = 0; j < (1 << LP); ++j) bx += x;
+        } else {
+            bx = seq_sum(x, L);
+        }
+        a1 = seq_sum(bx, C.q1);
+        if (C.q2 | C.q3) {
+            T g1 = T(0.f);
+            if constexpr (LP != 0) {
+#pragma unroll
+                for (int j = 0; j < (1 << LP); ++j) g1 += bx;
+            } else {
+                g1 = seq_sum(bx, L);
+            }
+            a2 = seq_sum(g1, C.q2);
+            if (C.q3) a3 = seq_sum(seq_sum(g1, L), C.q3);
+        }
+        i = C.nbp << lp;
+    }
+    __device__ __forceinline__ void feed(T val) {
+        a0 += val;
+        ++i;
+        if ((i & (L - 1)) == 0) {   // never true past the last full block (k < (nb + 1) L)
+            const int b = i >> lp;
+            a1 += a0;
+            a0 = T(0.f);
+            if ((b & (L - 1)) == 0) {
+                a2 += a1;
+                a1 = T(0.f);
+                if (((b >> lp) & (L - 1)) == 0) {
+                    a3 += a2;
+                    a2 = T(0.f);
+                }
+            }
+        }
+    }
+    __device__ __forceinline__ T finish() {
+        a0 += a1;
+        a0 += a2;
+        a0 += a3;
+        return a0;
+    }
+};
+
+// streaming path: four elements, stale values already in registers
+template <int LP, int NSR>
+__device__ __forceinline__ f32x4 multi_row_sum_regs4(f32x4 x, const f32x4 (&y)[NSR],
+                                                     const Casc& C) {
+    CascAcc<LP, f32x4> acc(x, C);
+    while (acc.i < C.c) acc.feed(x);
+#pragma unroll
+    for (int q = 0; q < NSR; ++q)
+        if (q < C.ns) acc.feed(y[q]);
+    return acc.finish();
+}
+
+// y[q] for a uniform run-time q (select chain: keeps y in registers)
+__device__ __forceinline__ float pick(const float (&y)[MAX_STALE], int q) {
     float r = 0.f;
 #pragma unroll
-    for (int q = 0; q < MAX_STALE; ++q) r = (i - c == q) ? y[q] : r;
+    for (int j = 0; j < MAX_STALE; ++j) r = (j == q) ? y[j] : r;
     return r;
 }
 
-// multi_row_sum over k rows whose first c are x and whose rows c.. are y[0..]: blocks made only
-// of x are summed once; whole level-1 / level-2 groups of such blocks likewise.
-__device__ __forceinline__ float multi_row_sum_rep(float x, const float (&y)[MAX_STALE], int c,
-                                                   int k) {
-    int lp = ceil_log2_i(k) / 4;
-    if (lp < 4) lp = 4;
-    const int L = 1 << lp;
-    const int nb = k >> lp;              // full blocks
-    int nbp = c >> lp;                   // blocks made only of x
-    if (nbp > nb) nbp = nb;
-    const float bx = seq_sum(x, L);      // acc0 after a pure block (acc0 is 0 at block start)
-    const float g1 = seq_sum(bx, L);     // a1 total of a pure level-1 group
-    const float g2 = seq_sum(g1, L);     // a2 total of a pure level-2 group
-    const int q1 = nbp & (L - 1);
-    const int q2 = (nbp >> lp) & (L - 1);
-    const int q3 = nbp >> (2 * lp);
-    float a0 = 0.f;
-    float a1 = seq_sum(bx, q1);
-    float a2 = seq_sum(g1, q2);
-    float a3 = seq_sum(g2, q3);
-    int i = nbp << lp;
-    for (int b = nbp; b < nb; ++b) {
-        for (int j = 0; j < L; ++j, ++i) a0 += entry(x, y, c, i);
-        a1 += a0;
-        a0 = 0.f;
-        if (((b + 1) & (L - 1)) != 0) continue;
-        a2 += a1;
-        a1 = 0.f;
-        if ((((b + 1) >> lp) & (L - 1)) != 0) continue;
-        a3 += a2;
-        a2 = 0.f;
-    }
-    for (; i < k; ++i) a0 += entry(x, y, c, i);
-    a0 += a1;
-    a0 += a2;
-    a0 += a3;
-    return a0;
+// element path: the stale rows of a stream are y[sbase], y[sbase + stride], ...
+__device__ __forceinline__ float multi_row_sum_strided(float x, const float (&y)[MAX_STALE],
+                                                       const Casc& C, int stride) {
+    CascAcc<0> acc(x, C);
+    while (acc.i < C.c) acc.feed(x);
+    for (int j = 0; j < C.ns; ++j) acc.feed(pick(y, C.sbase + stride * j));
+    return acc.finish();
 }
 
-// row_sum: the k entries viewed as (k/4, 4) -> stream q holds entries 4r+q.  Its first cq rows
-// are S_t copies and the rest are stale entries, so each stream is itself a "c copies then a few
-// others" multi_row_sum (memoised); leftovers (k % 4) go into stream 0, then s0 + s1 + s2 + s3.
-__device__ __forceinline__ float row_sum_rep(float x, const float (&y)[MAX_STALE], int c, int k) {
-    const int sz = k / 4;
+// ATen row_sum (the last numel % 32 elements of a tensor): the k rows as (k/4, 4), stream q =
+// rows 4r + q summed by multi_row_sum, leftover rows (k % 4) added to stream 0, then
+// s0 + s1 + s2 + s3.
+__device__ __forceinline__ float row_sum_regs(const AggArgs& A, float x,
+                                              const float (&y)[MAX_STALE]) {
     float ps[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        int cq = (c - q + 3) / 4;                 // rows r with 4r + q < c
-        cq = cq < 0 ? 0 : (cq > sz ? sz : cq);
-        float z[MAX_STALE];
-#pragma unroll
-        for (int j = 0; j < MAX_STALE; ++j) {
-            const int i = 4 * (cq + j) + q;      // entry index (>= c when cq + j < sz)
-            z[j] = (cq + j < sz) ? entry(x, y, c, i) : 0.f;
-        }
-        ps[q] = multi_row_sum_rep(x, z, cq, sz);
-    }
-    for (int i = sz * 4; i < k; ++i) ps[0] += entry(x, y, c, i);
+    for (int q = 0; q < 4; ++q) ps[q] = multi_row_sum_strided(x, y, A.rs[q], 4);
+    for (int i = (A.k / 4) * 4; i < A.k; ++i) ps[0] += (i < A.c) ? x : pick(y, i - A.c);
     ps[0] += ps[1];
     ps[0] += ps[2];
     ps[0] += ps[3];
@@ -139,76 +180,113 @@ __device__ __forceinline__ float sqrt_rn(float x) {
     return (xs == 0.f || xs == __builtin_inff() || xs != xs) ? x : s;
 }
 
-__device__ __forceinline__ void adam_elem(const AggArgs& A, float g, float& p, float& m, float& v) {
+// Correctly rounded a / b for a launch-constant divisor b with rb = RN(1/b) (Markstein: q0
+// within 1 ulp, exact residual by fma, one correction).  Zero, tiny (near-subnormal) and
+// non-finite quotients take the IEEE division so signs and subnormals stay exact.
+__device__ __forceinline__ float div_const(float a, float b, float rb) {
+    const float q0 = a * rb;
+    const float r = __fmaf_rn(-q0, b, a);
+    const float q = __fmaf_rn(r, rb, q0);
+    const float aq = fabsf(q0);
+    return (aq >= 0x1p-124f && aq <= 0x1p+124f) ? q : __fdiv_rn(a, b);
+}
+
+__device__ __forceinline__ void adam_elem(const AggArgs& A, float s, float& p, float& m, float& v) {
+    const float g = div_const(s, A.fk, A.rk);               // rule(): mean = sum / k
     const float mi = __fmaf_rn(A.w1, g - m, m);
     float vi = v * A.b2;
     vi = __fmaf_rn(A.w2 * g, g, vi);
-    const float den = __fdiv_rn(sqrt_rn(vi), A.bc2s) + A.eps;
+    const float den = div_const(sqrt_rn(vi), A.bc2s, A.rbc2s) + A.eps;
     p = p + __fdiv_rn(A.neg_ss * mi, den);
     m = mi;
     v = vi;
 }
 
-__device__ __forceinline__ void do_elem(const AggArgs& A, long e, bool tail) {
-    const int k = A.c + A.ns;
-    float y[MAX_STALE];
-#pragma unroll
-    for (int q = 0; q < MAX_STALE; ++q)
-        y[q] = (q < A.ns && A.stale[q]) ? A.stale[q][e] : 0.f;
-    const float x = A.S[e];
-    const float s = tail ? row_sum_rep(x, y, A.c, k) : multi_row_sum_rep(x, y, A.c, k);
-    const float g = __fdiv_rn(s, (float)k);
-    float p = A.p[e], m = A.m[e], v = A.v[e];
-    adam_elem(A, g, p, m, v);
-    A.p[e] = p;
-    A.m[e] = m;
-    A.v[e] = v;
-}
-
 __device__ __forceinline__ bool in_tail(const AggArgs& A, long e) {
-    for (int t = 0; t < A.ntail; ++t)
-        if (e >= A.tail_lo[t] && e < A.tail_hi[t]) return true;
-    return false;
+    bool r = false;
+#pragma unroll
+    for (int t = 0; t < MAX_TAILS; ++t)
+        r |= (t < A.ntail) && e >= A.tail_lo[t] && e < A.tail_hi[t];
+    return r;
 }
 
-// one thread = 4 consecutive elements; blocks that touch no tail range take the float4 path
-__global__ void __launch_bounds__(256) k_aggregate_adam(AggArgs A) {
-    const long e0 = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
-    const long blo = (long)blockIdx.x * 1024;
+__device__ __forceinline__ bool block_touch(const AggArgs& A, long blo) {
     const long bhi = blo + 1024;
-    bool touch = bhi > A.P;
-    for (int t = 0; t < A.ntail; ++t) touch |= (A.tail_lo[t] < bhi && A.tail_hi[t] > blo);
-    if (e0 >= A.P) return;
-    if (!touch) {
-        const int k = A.c + A.ns;
-        const f32x4 xs = *reinterpret_cast<const f32x4*>(A.S + e0);
-        f32x4 ys[MAX_STALE];
+    bool touch = blo < A.lo || bhi > A.hi;
+#pragma unroll
+    for (int t = 0; t < MAX_TAILS; ++t)
+        touch |= (t < A.ntail) && A.tail_lo[t] < bhi && A.tail_hi[t] > blo;
+    return touch;
+}
+
+// One launch per <= MAX_TAILS tensor tails.  Blocks [0, nedge) are the pieces of the edge blocks
+// the host listed (launch edges, tail ranges): one element per thread, row_sum order on tail
+// elements; they start first and overlap the stream.  The other blocks are the streaming path, one thread per
+// aligned float4 group; a streaming block that is also an edge block returns at once.
+// LP: 4 = the level step of every k < 2^20, 0 = read at run time.  NSR: stale entries held in
+// registers by the streaming path (1 covers the reference's single slow worker).
+template <int LP, int NSR>
+__global__ void __launch_bounds__(256) k_aggregate_adam(AggArgs A) {
+    if ((int)blockIdx.x < A.nedge) {
+        // edge piece: 256 elements, one per thread, every load issued before the arithmetic
+        const long e = A.edge_lo[blockIdx.x] + threadIdx.x;
+        if (e < A.lo || e >= A.hi) return;
+        float y[MAX_STALE];
 #pragma unroll
         for (int q = 0; q < MAX_STALE; ++q)
-            ys[q] = (q < A.ns && A.stale[q]) ? *reinterpret_cast<const f32x4*>(A.stale[q] + e0)
-                                             : f32x4{0.f, 0.f, 0.f, 0.f};
-        f32x4 p = *reinterpret_cast<const f32x4*>(A.p + e0);
-        f32x4 m = *reinterpret_cast<const f32x4*>(A.m + e0);
-        f32x4 v = *reinterpret_cast<const f32x4*>(A.v + e0);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            float y[MAX_STALE];
-#pragma unroll
-            for (int q = 0; q < MAX_STALE; ++q) y[q] = ys[q][u];
-            const float s = multi_row_sum_rep(xs[u], y, A.c, k);
-            const float g = __fdiv_rn(s, (float)k);
-            float pp = p[u], mm = m[u], vv = v[u];
-            adam_elem(A, g, pp, mm, vv);
-            p[u] = pp;
-            m[u] = mm;
-            v[u] = vv;
-        }
-        *reinterpret_cast<f32x4*>(A.p + e0) = p;
-        *reinterpret_cast<f32x4*>(A.m + e0) = m;
-        *reinterpret_cast<f32x4*>(A.v + e0) = v;
-    } else {
-        for (long e = e0; e < e0 + 4 && e < A.P; ++e) do_elem(A, e, in_tail(A, e));
+            y[q] = (q < A.main.ns && A.stale[q]) ? A.stale[q][e] : 0.f;
+        const float x = A.S[e];
+        float p = A.p[e], m = A.m[e], v = A.v[e];
+        const float s = in_tail(A, e) ? row_sum_regs(A, x, y) : multi_row_sum_strided(x, y, A.main, 1);
+        adam_elem(A, s, p, m, v);
+        A.p[e] = p;
+        A.m[e] = m;
+        A.v[e] = v;
+        return;
     }
+    const long blo = 4 * (A.g0 + (long)(blockIdx.x - A.nedge) * 256);
+    if (block_touch(A, blo)) return;
+    const long e0 = blo + 4 * threadIdx.x;
+    const f32x4 xs = *reinterpret_cast<const f32x4*>(A.S + e0);
+    f32x4 ys[NSR];
+#pragma unroll
+    for (int q = 0; q < NSR; ++q)
+        ys[q] = (q < A.main.ns && A.stale[q]) ? *reinterpret_cast<const f32x4*>(A.stale[q] + e0)
+                                              : f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 p = *reinterpret_cast<const f32x4*>(A.p + e0);
+    f32x4 m = *reinterpret_cast<const f32x4*>(A.m + e0);
+    f32x4 v = *reinterpret_cast<const f32x4*>(A.v + e0);
+    const f32x4 sum = multi_row_sum_regs4<LP, NSR>(xs, ys, A.main);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        float pp = p[u], mm = m[u], vv = v[u];
+        adam_elem(A, sum[u], pp, mm, vv);
+        p[u] = pp;
+        m[u] = mm;
+        v[u] = vv;
+    }
+    *reinterpret_cast<f32x4*>(A.p + e0) = p;
+    *reinterpret_cast<f32x4*>(A.m + e0) = m;
+    *reinterpret_cast<f32x4*>(A.v + e0) = v;
+}
+
+// host: memo constants of a multi_row_sum over k rows, the first c of them copies of x
+static Casc make_casc(int c, int k, int sbase) {
+    Casc C{};
+    int lp = 0;
+    while ((1L << lp) < k) ++lp;     // ceil_log2(k)
+    lp /= 4;
+    if (lp < 4) lp = 4;
+    C.c = c;
+    C.ns = k - c;
+    C.lp = lp;
+    C.nb = k >> lp;
+    C.nbp = (c >> lp) < C.nb ? (c >> lp) : C.nb;
+    C.q1 = C.nbp & ((1 << lp) - 1);
+    C.q2 = (C.nbp >> lp) & ((1 << lp) - 1);
+    C.q3 = C.nbp >> (2 * lp);
+    C.sbase = sbase;
+    return C;
 }
 
 }  // namespace flsim
@@ -223,17 +301,17 @@ int flsim_aggregate_adam(const float* S, int c, const float* const* stale, int n
                          float* p, float* m, float* v, long P, const long* tensor_sizes,
                          int n_tensors, long step, double lr, double beta1, double beta2,
                          double eps, hipStream_t stream) {
-    FLSIM_REQUIRE(S && p && m && v, "null pointer");
+    FLSIM_REQUIRE(S && p && m && v && tensor_sizes, "null pointer");
     FLSIM_REQUIRE(c >= 0 && n_stale >= 0 && n_stale <= MAX_STALE, "bad entry counts c=%d ns=%d", c,
                   n_stale);
     FLSIM_REQUIRE(c + n_stale > 0, "empty weight_ups (reference: IndexError in rule, main.py:25)");
+    FLSIM_REQUIRE(c + n_stale < (1 << 24), "k = %d entries: beyond exact fp32 integers", c + n_stale);
     FLSIM_REQUIRE(step >= 1, "step must be >= 1");
+    FLSIM_REQUIRE(P > 0 && P < (1L << 31), "P = %ld out of range", P);
     const uintptr_t al = (uintptr_t)S | (uintptr_t)p | (uintptr_t)m | (uintptr_t)v;
     FLSIM_REQUIRE((al & 15) == 0, "S/p/m/v must be 16-byte aligned");
     AggArgs A{};
     A.S = S;
-    A.c = c;
-    A.ns = n_stale;
     for (int q = 0; q < n_stale; ++q) {
         A.stale[q] = stale ? stale[q] : nullptr;
         FLSIM_REQUIRE(((uintptr_t)A.stale[q] & 15) == 0, "stale entries must be 16-byte aligned");
@@ -241,34 +319,105 @@ int flsim_aggregate_adam(const float* S, int c, const float* const* stale, int n
     A.p = p;
     A.m = m;
     A.v = v;
-    A.P = P;
-    long off = 0;
-    int nt = 0;
-    for (int t = 0; t < n_tensors; ++t) {
-        const long n = tensor_sizes[t];
-        const long body = (n / 32) * 32;
-        if (body < n) {
-            FLSIM_REQUIRE(nt < MAX_TAILS, "too many tensors");
-            A.tail_lo[nt] = off + body;
-            A.tail_hi[nt] = off + n;
-            nt++;
-        }
-        off += n;
+    const int k = c + n_stale;
+    A.c = c;
+    A.k = k;
+    A.main = make_casc(c, k, 0);
+    const int sz = k / 4;
+    for (int q = 0; q < 4; ++q) {
+        int cq = (c - q + 3) / 4;                 // rows r with 4r + q < c
+        cq = cq < 0 ? 0 : (cq > sz ? sz : cq);
+        A.rs[q] = make_casc(cq, sz, 4 * cq + q - c);
     }
-    FLSIM_REQUIRE(off == P, "tensor sizes sum to %ld, P = %ld", off, P);
-    A.ntail = nt;
+    A.fk = (float)k;
+    {
+        volatile float one = 1.f, fk = (float)k;   // RN(1/k) in fp32, not via double
+        A.rk = one / fk;
+    }
     const double bc1 = 1.0 - pow(beta1, (double)step);
     const double bc2 = 1.0 - pow(beta2, (double)step);
     A.w1 = (float)(1.0 - beta1);
     A.b2 = (float)beta2;
     A.w2 = (float)(1.0 - beta2);
     A.bc2s = (float)sqrt(bc2);
+    {
+        volatile float one = 1.f, b = A.bc2s;
+        A.rbc2s = one / b;
+    }
     A.eps = (float)eps;
     A.neg_ss = (float)(-(lr / bc1));
-    const long threads = (P + 3) / 4;
-    hipLaunchKernelGGL(k_aggregate_adam, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream,
-                       A);
-    FLSIM_LAUNCH_CHECK();
+    // tail ranges (last numel % 32 elements of each tensor), split into launches of <= MAX_TAILS
+    long off = 0;
+    for (int t = 0; t < n_tensors; ++t) {
+        FLSIM_REQUIRE(tensor_sizes[t] > 0, "tensor %d has size %ld", t, tensor_sizes[t]);
+        off += tensor_sizes[t];
+    }
+    FLSIM_REQUIRE(off == P, "tensor sizes sum to %ld, P = %ld", off, P);
+    off = 0;
+    long lo = 0;
+    int t = 0;
+    while (lo < P) {
+        A.ntail = 0;
+        long hi = lo;
+        while (t < n_tensors) {
+            const long n = tensor_sizes[t];
+            const bool tail = (n % 32) != 0;
+            if (tail && A.ntail == MAX_TAILS) break;
+            if (tail) {
+                A.tail_lo[A.ntail] = (int)(off + (n / 32) * 32);
+                A.tail_hi[A.ntail] = (int)(off + n);
+                A.ntail++;
+            }
+            off += n;
+            hi = off;
+            ++t;
+        }
+        A.lo = lo;
+        A.hi = hi;
+        A.g0 = lo / 4;
+        const long groups = (hi + 3) / 4 - A.g0;
+        const long nblk = (groups + 255) / 256;
+        // edge blocks: the first and last block when they cross the launch range, and every
+        // block holding a tail range (host copy of block_touch)
+        A.nedge = 0;
+        auto add_block = [&](long b) {
+            const long blo = 4 * (A.g0 + b * 256);
+            for (int j = 0; j < A.nedge; j += 4)
+                if (A.edge_lo[j] == blo) return;
+            for (int j = 0; j < 4; ++j) A.edge_lo[A.nedge++] = blo + 256 * j;
+        };
+        for (long b : {0L, nblk - 1}) {
+            const long blo = 4 * (A.g0 + b * 256);
+            if (blo < A.lo || blo + 1024 > A.hi) add_block(b);
+        }
+        for (int j = 0; j < A.ntail; ++j) {
+            const long b0 = (A.tail_lo[j] / 4 - A.g0) / 256;
+            const long b1 = ((A.tail_hi[j] - 1) / 4 - A.g0) / 256;
+            for (long b = b0; b <= b1; ++b) add_block(b);
+        }
+        const dim3 grid((unsigned)(nblk + A.nedge));
+        // algorithmic HBM bytes: read S_t + the distinct stale entries + p, m, v; write p, m, v
+        int distinct = 0;
+        for (int q = 0; q < n_stale; ++q) {
+            bool seen = A.stale[q] == nullptr;
+            for (int r = 0; r < q && !seen; ++r) seen = A.stale[r] == A.stale[q];
+            distinct += !seen;
+        }
+        const double bytes = 4.0 * (double)(hi - lo) * (7 + distinct);
+        const int slot = probe_begin(stream);
+        const bool lp4 = A.main.lp == 4, ns1 = n_stale <= 1;
+        if (lp4 && ns1)
+            hipLaunchKernelGGL((k_aggregate_adam<4, 1>), grid, dim3(256), 0, stream, A);
+        else if (lp4)
+            hipLaunchKernelGGL((k_aggregate_adam<4, MAX_STALE>), grid, dim3(256), 0, stream, A);
+        else if (ns1)
+            hipLaunchKernelGGL((k_aggregate_adam<0, 1>), grid, dim3(256), 0, stream, A);
+        else
+            hipLaunchKernelGGL((k_aggregate_adam<0, MAX_STALE>), grid, dim3(256), 0, stream, A);
+        FLSIM_LAUNCH_CHECK();
+        if (probe_end(slot, stream, K_AGG, bytes)) return 2;
+        lo = hi;
+    }
     return 0;
 }
 

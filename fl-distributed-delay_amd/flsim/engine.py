@@ -92,13 +92,19 @@ class PN1Engine:
     def aggregate_adam(self, S, c, stale, theta, m, v, step, lr=1e-3, betas=(0.9, 0.999),
                        eps=1e-8):
         """stale: list of device tensors (or None = zero entry)."""
-        ns = len(stale)
-        arr = (ctypes.c_void_p * max(1, ns))(*[(t.data_ptr() if t is not None else None)
-                                               for t in stale])
-        check(lib().flsim_aggregate_adam(
-            ptr(S), int(c), arr, ns, ptr(theta), ptr(m), ptr(v), self.P, self.sizes,
-            len(PN1_SIZES), int(step), float(lr), float(betas[0]), float(betas[1]), float(eps),
-            stream_ptr()))
+        aggregate_adam(S, c, stale, theta, m, v, step, PN1_SIZES, lr, betas, eps)
+
+
+def aggregate_adam(S, c, stale, theta, m, v, step, sizes, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
+    """Fused rule() + Adam (main.py:23-25 + agents.py:9-21) over a flat parameter vector whose
+    tensors have numel `sizes` (named_parameters order).  stale: device tensors or None (zeros)."""
+    ns = len(stale)
+    arr = (ctypes.c_void_p * max(1, ns))(*[(t.data_ptr() if t is not None else None)
+                                           for t in stale])
+    csz = (ctypes.c_long * len(sizes))(*[int(n) for n in sizes])
+    check(lib().flsim_aggregate_adam(
+        ptr(S), int(c), arr, ns, ptr(theta), ptr(m), ptr(v), sum(int(n) for n in sizes), csz, len(sizes),
+        int(step), float(lr), float(betas[0]), float(betas[1]), float(eps), stream_ptr()))
 
 
 def worker_table(recs, device):

@@ -83,7 +83,6 @@ class FLSimulation:
         self.free_slots = []
         self.trace = []
         self.loss_log = []        # per epoch: float (synced) or (device tensor, fast mask)
-        self.agg_timing = None    # list -> (start event, end event, algorithmic bytes) per step
 
     # ---------------------------------------------------------------------------------------------
     def _slot(self):
@@ -161,17 +160,8 @@ class FLSimulation:
             else:
                 stale.append(None)
         self.step += 1
-        if self.agg_timing is not None:
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e0.record()
         eng.aggregate_adam(S, plan.c_t, stale, self.theta, self.m, self.v, self.step, self.lr,
                            self.betas, self.eps)
-        if self.agg_timing is not None:
-            e1.record()
-            n_stale_arrays = len({id(x) for x in stale if x is not None})
-            # read S_t + distinct stale slots + p, m, v; write p, m, v  
-            self.agg_timing.append((e0, e1, 4 * self.P * (1 + n_stale_arrays + 3 + 3)))
         for (_, src) in plan.stale:
             if self.semantics == "reference":
                 entry = self.stale_store[src]

@@ -66,6 +66,45 @@ def test_aggregate_adam_bit_exact(c, ns):
     assert bad == {"p": 0, "m": 0, "v": 0}, bad
 
 
+@pytest.mark.parametrize("c,ns,sizes", [
+    (4095, 0, [1000, 4096, 33, 7]),                       # k = 4095: three level-1 groups
+    (16383, 1, [2048, 31, 4000]),                         # 16k workers (configs[3])
+    (6, 3, [5, 37, 64, 1, 96, 100, 33, 2, 3, 70, 9, 11]), # > 8 tails: split launches
+])
+def test_aggregate_adam_layouts_and_edges(c, ns, sizes):
+    """Large k, odd tensor layouts (many row_sum tails, unaligned tensor starts) and the value
+    edge cases of the division paths: +-0, subnormal and huge gradients."""
+    from flsim.engine import aggregate_adam
+    from oracle import oracle as O
+    P = sum(sizes)
+    rs = np.random.RandomState(c + ns)
+    S = (rs.standard_normal(P) * 1e-2).astype(np.float32)
+    S[::17] = 0.0
+    S[1::17] = -0.0
+    S[2::17] = np.float32(3e-39) * rs.choice([-1, 1], len(S[2::17]))
+    S[3::17] = np.float32(1e30)
+    stale = [(rs.standard_normal(P) * 1e-2).astype(np.float32) for _ in range(ns)]
+    p = rs.standard_normal(P).astype(np.float32)
+    m = (rs.standard_normal(P) * 1e-3).astype(np.float32)
+    v = (rs.rand(P) * 1e-5).astype(np.float32)
+    dS = torch.from_numpy(S).to(DEV)
+    dst = [torch.from_numpy(s).to(DEV) for s in stale]
+    dp, dm, dv = (torch.from_numpy(a.copy()).to(DEV) for a in (p, m, v))
+    aggregate_adam(dS, c, dst, dp, dm, dv, 2, sizes)
+    torch.cuda.synchronize()
+    g = np.empty_like(S)
+    off = 0
+    for n in sizes:
+        g[off:off + n] = O.cascade_mean([S[off:off + n]] * c + [s[off:off + n] for s in stale])
+        off += n
+    O.adam_step(p, m, v, g, 2)
+    bad = {}
+    for name, a, b in (("p", dp, p), ("m", dm, m), ("v", dv, v)):
+        got = a.cpu().numpy()
+        bad[name] = int((got.view(np.uint32) != b.view(np.uint32)).sum())
+    assert bad == {"p": 0, "m": 0, "v": 0}, bad
+
+
 def test_aggregate_adam_torch1_zero_stale():
     from flsim.engine import PN1Engine
     eng = PN1Engine(DEV, chunk_workers=1)

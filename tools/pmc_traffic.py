@@ -1,0 +1,72 @@
+"""HBM traffic per launch from the rocprofv3 PMC passes of tools/gpu_profile.sh.
+
+  python tools/pmc_traffic.py <profile dir> [out.json ...]
+
+Reads <dir>/pmc_FETCH_SIZE/run_counter_collection.csv and <dir>/pmc_WRITE_SIZE/...csv, maps the
+template kernel names to the probe names bench.py reports, and writes
+{kernel: {"bytes_per_launch": B, "fetch": F, "write": W, "launches": n, "source": ...}}.
+Units and corrections follow MI355X_MICROARCH.md (HBM section): FETCH_SIZE / WRITE_SIZE are in
+KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide streaming read, so it is doubled.
+"""
+import csv
+import json
+import os
+import re
+import sys
+
+FWD = {(32, 32, 4): 1, (34, 34, 48): 2, (18, 18, 48): 3, (20, 20, 96): 4, (11, 11, 96): 5,
+       (13, 13, 192): 6}
+DGRAD = {(36, 36, 48): 2, (20, 20, 96): 3, (22, 22, 96): 4, (13, 13, 192): 5, (15, 15, 192): 6}
+
+
+def probe_name(kname):
+    if "k_aggregate_adam" in kname:
+        return "aggregate_adam"
+    m = re.search(r"Im2colKM<(\d+), (\d+), (\d+),", kname)
+    if m:
+        return f"conv{FWD[tuple(map(int, m.groups()))]}_wgrad"
+    m = re.search(r"Im2colKC<(\d+), (\d+), (\d+), (\d+),", kname)
+    if m:
+        ih, iw, ci, pad = map(int, m.groups())
+        if pad == 2:
+            return f"conv{FWD[(ih, iw, ci)]}_fwd"
+        return f"conv{DGRAD[(ih, iw, ci)]}_dgrad"
+    return None
+
+
+def read(path, counter):
+    out = {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if r["Counter_Name"] != counter:
+                continue
+            name = probe_name(r["Kernel_Name"])
+            if name is None:
+                continue
+            out.setdefault(name, []).append(float(r["Counter_Value"]))
+    return out
+
+
+def main():
+    d = sys.argv[1]
+    outs = sys.argv[2:] or [os.path.join(d, "traffic.json")]
+    fetch = read(os.path.join(d, "pmc_FETCH_SIZE", "run_counter_collection.csv"), "FETCH_SIZE")
+    write = read(os.path.join(d, "pmc_WRITE_SIZE", "run_counter_collection.csv"), "WRITE_SIZE")
+    res = {}
+    for k in sorted(set(fetch) & set(write)):
+        f = 2 * 1024 * sum(fetch[k]) / len(fetch[k])
+        w = 1024 * sum(write[k]) / len(write[k])
+        res[k] = dict(bytes_per_launch=int(f + w), fetch=int(f), write=int(w),
+                      launches=len(fetch[k]),
+                      source=f"rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE, "
+                             f"{os.path.basename(os.path.normpath(d))}")
+    for o in outs:
+        os.makedirs(os.path.dirname(os.path.abspath(o)), exist_ok=True)
+        with open(o, "w") as fh:
+            json.dump(res, fh, indent=1, sort_keys=True)
+    for k, v in res.items():
+        print(f"{k:16s} {v['bytes_per_launch'] / 1e6:10.2f} MB/launch  ({v['launches']} launches)")
+
+
+if __name__ == "__main__":
+    main()
