@@ -328,11 +328,11 @@ static int launch_gemm(const AL& al, const BL& bl, const EPI& epi, int M, int N,
     const int per = (ksteps + Z - 1) / Z;
     const int tm = ceil_div(M, BM), tn = ceil_div(N, BN);
     dim3 grid(tm * tn * Z);
-    const int slot = probe_begin(st);
-    hipLaunchKernelGGL((gemm_kernel<FM, FN, WM, WN, AL, BL, EPI>), grid, dim3(64 * WM * WN), 0, st,
-                       al, bl, epi, ksteps, per, tm, tn);
+    const ProbeSlot ps = probe_begin();
+    hipExtLaunchKernelGGL((gemm_kernel<FM, FN, WM, WN, AL, BL, EPI>), grid, dim3(64 * WM * WN), 0,
+                          st, ps.start, ps.stop, 0, al, bl, epi, ksteps, per, tm, tn);
     FLSIM_LAUNCH_CHECK();
-    return probe_end(slot, st, kid, alg_flops);
+    return probe_end(ps, kid, alg_flops);
 }
 
 // forward conv (also the data-gradient conv): out[m][n] for m < S*OH*OW, n < N
@@ -384,10 +384,11 @@ struct ConvGeo {
     int KP;              // packed forward K (9*CIP rounded to 16)
     int ZW;              // wgrad split
 };
-// ZW (pixel splits of the weight gradient) sized so each wgrad launch has ~3-6k blocks: several
-// rounds of resident blocks on 256 CUs (no half-empty last round, enough waves per SIMD).
+// ZW (pixel splits of the weight gradient) sized so each wgrad launch has thousands of blocks:
+// several rounds of resident blocks on 256 CUs.  Tile shapes per layer were picked with
+// tools/lab/gemm_lab.hip on MI355X (4-wave wgrad tiles: a 6-wave block loads two SIMDs twice).
 static const ConvGeo GEO[6] = {
-    {3, 4, 48, 32, 48, 4096},    {48, 48, 48, 34, 432, 2048},   {48, 48, 96, 18, 432, 1024},
+    {3, 4, 48, 32, 48, 8192},    {48, 48, 48, 34, 432, 2048},   {48, 48, 96, 18, 432, 1024},
     {96, 96, 96, 20, 864, 512},  {96, 96, 192, 11, 864, 256},  {192, 192, 192, 13, 1728, 128},
 };
 static const long P_OFF[18] = {0,       1296,    1344,    22080,   22128,   63600,
@@ -496,9 +497,9 @@ static int pack_weights(const GradState& g, const float* theta, hipStream_t st) 
 static int forward(const GradState& g, const WS& w, const float* theta, int S,
                    const WorkerRec* workers, uint64_t seed, int dropout, hipStream_t st) {
     // conv1, conv2 (+ReLU)  models.py:29-30
-    RC((conv_like<32, 32, 4, 2, 4, 3, 4, 1>(w.x0, S, g.wf[0], 48, 48,
+    RC((conv_like<32, 32, 4, 2, 2, 3, 4, 1>(w.x0, S, g.wf[0], 48, 48,
         EpiBiasRelu{w.a1, theta + P_OFF[1], S * 34 * 34, 48}, st, K_FWD1, 27)));
-    RC((conv_like<34, 34, 48, 2, 4, 3, 4, 1>(w.a1, S, g.wf[1], 48, 432,
+    RC((conv_like<34, 34, 48, 2, 2, 3, 8, 1>(w.a1, S, g.wf[1], 48, 432,
         EpiBiasRelu{w.a2, theta + P_OFF[3], S * 36 * 36, 48}, st, K_FWD2, 432)));
     {   // pool1 + dropout1  models.py:31-32
         const long tot = (long)S * 18 * 18 * 48;
@@ -507,9 +508,9 @@ static int forward(const GradState& g, const WS& w, const float* theta, int S,
                            dropout, tot);
         FLSIM_LAUNCH_CHECK();
     }
-    RC((conv_like<18, 18, 48, 2, 4, 3, 2, 2>(w.d1, S, g.wf[2], 96, 432,
+    RC((conv_like<18, 18, 48, 2, 4, 3, 4, 2>(w.d1, S, g.wf[2], 96, 432,
         EpiBiasRelu{w.a3, theta + P_OFF[5], S * 20 * 20, 96}, st, K_FWD3, 432)));
-    RC((conv_like<20, 20, 96, 2, 4, 3, 2, 2>(w.a3, S, g.wf[3], 96, 864,
+    RC((conv_like<20, 20, 96, 2, 4, 3, 4, 2>(w.a3, S, g.wf[3], 96, 864,
         EpiBiasRelu{w.a4, theta + P_OFF[7], S * 22 * 22, 96}, st, K_FWD4, 864)));
     {
         const long tot = (long)S * 11 * 11 * 96;
@@ -518,9 +519,9 @@ static int forward(const GradState& g, const WS& w, const float* theta, int S,
                            dropout, tot);
         FLSIM_LAUNCH_CHECK();
     }
-    RC((conv_like<11, 11, 96, 2, 4, 3, 2, 2>(w.d2, S, g.wf[4], 192, 864,
+    RC((conv_like<11, 11, 96, 2, 2, 6, 4, 2>(w.d2, S, g.wf[4], 192, 864,
         EpiBiasRelu{w.a5, theta + P_OFF[9], S * 13 * 13, 192}, st, K_FWD5, 864)));
-    RC((conv_like<13, 13, 192, 2, 4, 3, 2, 2>(w.a5, S, g.wf[5], 192, 1728,
+    RC((conv_like<13, 13, 192, 2, 2, 6, 4, 2>(w.a5, S, g.wf[5], 192, 1728,
         EpiBiasRelu{w.a6, theta + P_OFF[11], S * 15 * 15, 192}, st, K_FWD6, 1728)));
     {
         const long tot = (long)S * 7 * 7 * 192;
@@ -609,13 +610,13 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     }
     float* dz6 = w.a6;
     // ---- conv6: wgrad (input a5), bias, dgrad -> dz5 = . * (a5 > 0) into gx ----
-    RC((conv_wgrad<13, 13, 192, 3, 3, 2, 3>(dz6, w.a5, S, 192, 1728, g.sw[5], g.sb[5], GEO[5].ZW, st, K_WG6, 1728)));
-    RC((conv_like<15, 15, 192, 0, 4, 3, 2, 2>(dz6, S, g.wd[5], 192, 1728,
+    RC((conv_wgrad<13, 13, 192, 6, 3, 2, 2>(dz6, w.a5, S, 192, 1728, g.sw[5], g.sb[5], GEO[5].ZW, st, K_WG6, 1728)));
+    RC((conv_like<15, 15, 192, 0, 2, 6, 4, 2>(dz6, S, g.wd[5], 192, 1728,
         EpiMask<true>{w.gx, w.a5, S * 13 * 13, 192}, st, K_DG6, 1728)));
     float* dz5 = w.gx;
     // ---- conv5: wgrad (input d2), bias, dgrad -> grad wrt d2 (dropout site 2) into gy ----
-    RC((conv_wgrad<11, 11, 96, 3, 3, 2, 3>(dz5, w.d2, S, 192, 864, g.sw[4], g.sb[4], GEO[4].ZW, st, K_WG5, 864)));
-    RC((conv_like<13, 13, 192, 0, 4, 3, 2, 2>(dz5, S, g.wd[4], 96, 1728,
+    RC((conv_wgrad<11, 11, 96, 6, 3, 2, 2>(dz5, w.d2, S, 192, 864, g.sw[4], g.sb[4], GEO[4].ZW, st, K_WG5, 864)));
+    RC((conv_like<13, 13, 192, 0, 4, 3, 4, 2>(dz5, S, g.wd[4], 96, 1728,
         EpiDropMask{w.gy, w.d2, s25, S * 11 * 11, 96}, st, K_DG5, 1728)));
     {
         const long tot = (long)S * 22 * 22 * 96;
@@ -625,13 +626,13 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     }
     float* dz4 = w.a4;
     // ---- conv4: wgrad (input a3), bias, dgrad -> dz3 = . * (a3 > 0) into gx ----
-    RC((conv_wgrad<20, 20, 96, 3, 3, 2, 3>(dz4, w.a3, S, 96, 864, g.sw[3], g.sb[3], GEO[3].ZW, st, K_WG4, 864)));
-    RC((conv_like<22, 22, 96, 0, 4, 3, 2, 2>(dz4, S, g.wd[3], 96, 864,
+    RC((conv_wgrad<20, 20, 96, 3, 3, 2, 2>(dz4, w.a3, S, 96, 864, g.sw[3], g.sb[3], GEO[3].ZW, st, K_WG4, 864)));
+    RC((conv_like<22, 22, 96, 0, 4, 3, 4, 2>(dz4, S, g.wd[3], 96, 864,
         EpiMask<true>{w.gx, w.a3, S * 20 * 20, 96}, st, K_DG4, 864)));
     float* dz3 = w.gx;
     // ---- conv3: wgrad (input d1), bias, dgrad -> grad wrt d1 (site 1) into gy ----
-    RC((conv_wgrad<18, 18, 48, 3, 3, 2, 3>(dz3, w.d1, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW, st, K_WG3, 432)));
-    RC((conv_like<20, 20, 96, 0, 4, 3, 4, 1>(dz3, S, g.wd[2], 48, 864,
+    RC((conv_wgrad<18, 18, 48, 3, 3, 2, 2>(dz3, w.d1, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW, st, K_WG3, 432)));
+    RC((conv_like<20, 20, 96, 0, 2, 3, 8, 1>(dz3, S, g.wd[2], 48, 864,
         EpiDropMask{w.gy, w.d1, s25, S * 18 * 18, 48}, st, K_DG3, 864)));
     {
         const long tot = (long)S * 36 * 36 * 48;
@@ -642,7 +643,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     float* dz2 = w.a2;
     // ---- conv2: wgrad (input a1), bias, dgrad -> dz1 = . * (a1 > 0) into gx ----
     RC((conv_wgrad<34, 34, 48, 3, 3, 1, 3>(dz2, w.a1, S, 48, 432, g.sw[1], g.sb[1], GEO[1].ZW, st, K_WG2, 432)));
-    RC((conv_like<36, 36, 48, 0, 4, 3, 4, 1>(dz2, S, g.wd[1], 48, 432,
+    RC((conv_like<36, 36, 48, 0, 2, 3, 8, 1>(dz2, S, g.wd[1], 48, 432,
         EpiMask<true>{w.gx, w.a1, S * 34 * 34, 48}, st, K_DG2, 432)));
     float* dz1 = w.gx;
     // ---- conv1: wgrad (input x0), bias ----

@@ -20,18 +20,17 @@ struct Probe {
 };
 static Probe g_probe;
 
-int probe_begin(hipStream_t st) {
-    if (!g_probe.on || g_probe.used >= g_probe.cap) return -1;
-    if (hipEventRecord(g_probe.ev[2 * g_probe.used], st) != hipSuccess) return -1;
-    return g_probe.used;
+ProbeSlot probe_begin() {
+    if (!g_probe.on || g_probe.used >= g_probe.cap) return ProbeSlot{-1, nullptr, nullptr};
+    const int u = g_probe.used;
+    return ProbeSlot{u, g_probe.ev[2 * u], g_probe.ev[2 * u + 1]};
 }
 
-int probe_end(int slot, hipStream_t st, int kid, double work) {
-    if (slot < 0) return 0;
-    FLSIM_CHECK_HIP(hipEventRecord(g_probe.ev[2 * slot + 1], st));
-    g_probe.kid[slot] = kid;
-    g_probe.work[slot] = work;
-    g_probe.used = slot + 1;
+int probe_end(const ProbeSlot& ps, int kid, double work) {
+    if (ps.slot < 0) return 0;
+    g_probe.kid[ps.slot] = kid;
+    g_probe.work[ps.slot] = work;
+    g_probe.used = ps.slot + 1;
     return 0;
 }
 

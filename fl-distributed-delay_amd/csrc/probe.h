@@ -2,6 +2,8 @@
 // after selected launches (the worker-batched GEMMs and the fused aggregation), tagged with the
 // launch's kernel id and its algorithmic work (FLOPs for the GEMMs, HBM bytes for aggregation).
 #pragma once
+#include <hip/hip_ext.h>
+
 #include "common.h"
 
 namespace flsim {
@@ -13,9 +15,15 @@ enum KernelId {
     K_L1W, K_L1D, K_L2W, K_L2D, K_AGG, K_COUNT
 };
 
-// slot for the launch that follows, or -1 when the probe is off or full
-int probe_begin(hipStream_t st);
-// records the stop event; returns a C-ABI status
-int probe_end(int slot, hipStream_t st, int kid, double work);
+// Event pair for the launch that follows (nullptr events when the probe is off or full).  The
+// launch passes them to hipExtLaunchKernelGGL, which stamps them in the kernel's own dispatch
+// packet: the measured interval is the kernel, without separate marker packets.
+struct ProbeSlot {
+    int slot;
+    hipEvent_t start, stop;
+};
+ProbeSlot probe_begin();
+// registers the launch (kernel id, algorithmic work); returns a C-ABI status
+int probe_end(const ProbeSlot& ps, int kid, double work);
 
 }  // namespace flsim

@@ -404,18 +404,13 @@ int flsim_aggregate_adam(const float* S, int c, const float* const* stale, int n
             distinct += !seen;
         }
         const double bytes = 4.0 * (double)(hi - lo) * (7 + distinct);
-        const int slot = probe_begin(stream);
+        const ProbeSlot ps = probe_begin();
         const bool lp4 = A.main.lp == 4, ns1 = n_stale <= 1;
-        if (lp4 && ns1)
-            hipLaunchKernelGGL((k_aggregate_adam<4, 1>), grid, dim3(256), 0, stream, A);
-        else if (lp4)
-            hipLaunchKernelGGL((k_aggregate_adam<4, MAX_STALE>), grid, dim3(256), 0, stream, A);
-        else if (ns1)
-            hipLaunchKernelGGL((k_aggregate_adam<0, 1>), grid, dim3(256), 0, stream, A);
-        else
-            hipLaunchKernelGGL((k_aggregate_adam<0, MAX_STALE>), grid, dim3(256), 0, stream, A);
+        auto kern = lp4 ? (ns1 ? k_aggregate_adam<4, 1> : k_aggregate_adam<4, MAX_STALE>)
+                        : (ns1 ? k_aggregate_adam<0, 1> : k_aggregate_adam<0, MAX_STALE>);
+        hipExtLaunchKernelGGL(kern, grid, dim3(256), 0, stream, ps.start, ps.stop, 0, A);
         FLSIM_LAUNCH_CHECK();
-        if (probe_end(slot, stream, K_AGG, bytes)) return 2;
+        if (probe_end(ps, K_AGG, bytes)) return 2;
         lo = hi;
     }
     return 0;
