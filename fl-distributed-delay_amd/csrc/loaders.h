@@ -1,6 +1,7 @@
 // Operand loaders and epilogues for gemm_kernel (gemm_core.h).
 #pragma once
 #include "gemm_core.h"
+#include "pn1.h"
 
 namespace flsim {
 
@@ -13,12 +14,17 @@ __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 // k = (kh*3 + kw) * CI + ci (CI >= 16 and a multiple of 16, or CI == 4 for the padded input).
 // Input X is NHWC.  Output spatial OH = IH + 2*PAD - 2.
 // ---------------------------------------------------------------------------------------------
-template <int IH, int IW, int CI, int PAD, int TR, int NT>
+// WIN = true: output rows in max-pool window order, m = ((n * PH + ph) * PW + pw) * 4 + 2 dy + dx
+// with (oh, ow) = (2 ph + dy, 2 pw + dx); the floor-mode border rows/columns a 2x2 pool drops
+// are not computed at all (PerformantNet1 discards them: models.py:31,35,39).
+template <int IH, int IW, int CI, int PAD, int TR, int NT, bool WIN = false>
 struct Im2colKC {
     static constexpr int ROWS = TR;
     static constexpr bool KC = true;
     static constexpr int OH = IH + 2 * PAD - 2;
     static constexpr int OW = IW + 2 * PAD - 2;
+    static constexpr int PH = OH / 2, PW = OW / 2;
+    static constexpr int ROWS_PER_IMG = WIN ? 4 * PH * PW : OH * OW;
     static constexpr int TOTAL = ROWS * 4;
     static constexpr int UNITS = (TOTAL + NT - 1) / NT;
     static_assert(NT % 4 == 0, "");
@@ -40,10 +46,17 @@ struct Im2colKC {
             row[j] = (short)r;
             const int m = m0 + r;
             if (u < TOTAL && m < M) {
-                const int nimg = m / (OH * OW);
-                const int rem = m - nimg * (OH * OW);
-                oh[j] = (short)(rem / OW);
-                ow[j] = (short)(rem - (rem / OW) * OW);
+                const int nimg = m / ROWS_PER_IMG;
+                const int rem = m - nimg * ROWS_PER_IMG;
+                if constexpr (WIN) {
+                    const int q = rem >> 2;
+                    const int ph = q / PW;
+                    oh[j] = (short)(2 * ph + ((rem >> 1) & 1));
+                    ow[j] = (short)(2 * (q - ph * PW) + (rem & 1));
+                } else {
+                    oh[j] = (short)(rem / OW);
+                    ow[j] = (short)(rem - (rem / OW) * OW);
+                }
                 base[j] = nimg * (IH * IW * CI);
             } else {
                 base[j] = -1;
@@ -225,6 +238,53 @@ struct EpiBiasRelu {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
             if (m + r < M) Y[(long)(m + r) * N + n] = fmaxf(v[r] + b, 0.f);
+    }
+};
+
+// conv forward + bias + ReLU + 2x2 max-pool + dropout (models.py:30-32 / 34-36 / 38-40), rows in
+// pool-window order (Im2colKC<..., WIN>): a lane's 4 accumulator rows are one pooling window of
+// one channel.  Writes the pooled, dropped output d (NHWC, or torch flatten order for NCHW_OUT)
+// and the argmax (first max in row-major window order, as torch CPU) for the backward pass.
+template <int PH, int PW, int C, bool NCHW_OUT>
+struct EpiPoolDrop {
+    static constexpr bool ASUM = false;
+    float* d;
+    uint8_t* idx;
+    const float* bias;
+    const WorkerRec* workers;
+    uint64_t seed;
+    uint32_t site, thr;
+    float scale;
+    int dropout;
+    int M;
+    __device__ void apply4(int m, int n, int z, f32x4 v) const {
+        if (n >= C || m >= M) return;
+        const float b = bias[n];
+        float mv = fmaxf(v[0] + b, 0.f);
+        int mi = 0;
+#pragma unroll
+        for (int r = 1; r < 4; ++r) {
+            const float x = fmaxf(v[r] + b, 0.f);
+            if (x > mv) { mv = x; mi = r; }
+        }
+        const int q = m >> 2;                       // pooled pixel (s, ph, pw)
+        const int pw = q % PW;
+        const int ph = (q / PW) % PH;
+        const int s = q / (PW * PH);
+        const int w = s / SAMPLES_PER_WORKER;
+        const int nl = s - w * SAMPLES_PER_WORKER;
+        float out = mv;
+        if (dropout) {
+            const WorkerRec wr = workers[w];
+            const uint32_t en = (uint32_t)(((nl * C + n) * PH + ph) * PW + pw);
+            out = philox_word(seed, wr.t, wr.i, site, en) >= thr ? mv * scale : 0.f;
+        }
+        const long e = (long)q * C + n;
+        idx[e] = (uint8_t)mi;
+        if (NCHW_OUT)
+            d[(long)s * (C * PH * PW) + (n * PH + ph) * PW + pw] = out;
+        else
+            d[e] = out;
     }
 };
 

@@ -79,70 +79,60 @@ k_load_input(const float* __restrict__ x, const int64_t* __restrict__ yin, float
 }
 
 // =============================================================================================
-// max_pool2d(2,2) (floor mode; first max in row-major window order wins, like torch CPU) fused
-// with dropout (models.py:31-32 / 35-36 / 39-40).  in: a [S][H][W][C] -> out d, idx (0..3).
-// NCHW_OUT writes d in torch flatten order [S][C*PH*PW] (models.py:41 view(bs,-1)).
+// gradient through dropout + max_pool2d: dz[n][h][w][c] = gy[n][h/2][w/2][c] at the window's
+// argmax, 0 elsewhere and on the floor-mode border (models.py:31,35,39 backward).  One thread
+// per (window, 4 channels): one gy float4 (or 4 NCHW scalars), one idx word, four float4 stores.
+// gy is already masked / scaled by the consumer's epilogue.
 // =============================================================================================
-template <int H, int W, int C, bool NCHW_OUT>
+template <int H, int W, int C, bool NCHW_G>
 __global__ void __launch_bounds__(256)
-k_pool_drop_fwd(const float* __restrict__ a, float* __restrict__ d, uint8_t* __restrict__ idx,
-                const WorkerRec* __restrict__ workers, uint64_t seed, uint32_t site,
-                uint32_t thr, float scale, int dropout, long total) {
+k_pool_scatter(const float* __restrict__ gy, const uint8_t* __restrict__ idx,
+               float* __restrict__ dz, long total) {
     constexpr int PH = H / 2, PW = W / 2;
-    const long e = (long)blockIdx.x * 256 + threadIdx.x;  // NHWC index of pooled element
-    if (e >= total) return;
-    const int c = (int)(e % C);
-    const long pix = e / C;
-    const int pw = (int)(pix % PW);
-    const int ph = (int)((pix / PW) % PH);
-    const int s = (int)(pix / (PW * PH));
-    const float* base = a + (((long)s * H + 2 * ph) * W + 2 * pw) * C + c;
-    const float v0 = base[0], v1 = base[C], v2 = base[(long)W * C], v3 = base[(long)W * C + C];
-    float mv = v0;
-    int mi = 0;
-    if (v1 > mv) { mv = v1; mi = 1; }
-    if (v2 > mv) { mv = v2; mi = 2; }
-    if (v3 > mv) { mv = v3; mi = 3; }
-    const int w = s / SAMPLES_PER_WORKER;
-    const int nl = s - w * SAMPLES_PER_WORKER;
-    const uint32_t en = (uint32_t)(((nl * C + c) * PH + ph) * PW + pw);   // NCHW within worker
-    float out = mv;
-    if (dropout) {
-        const WorkerRec wr = workers[w];
-        out = philox_word(seed, wr.t, wr.i, site, en) >= thr ? mv * scale : 0.f;
-    }
-    idx[e] = (uint8_t)mi;
-    if (NCHW_OUT)
-        d[(long)s * (C * PH * PW) + (c * PH + ph) * PW + pw] = out;
-    else
-        d[e] = out;
-}
-
-// gradient through dropout + maxpool: thread per input element of the pool (NHWC [S][H][W][C]).
-// gd = gradient wrt the dropout output (layout of d), already multiplied by the dropout scale
-// and masked with (d > 0) by the producing epilogue.  Non-argmax positions (and the floor-mode
-// border) get 0.
-template <int H, int W, int C, bool NCHW_IN>
-__global__ void __launch_bounds__(256)
-k_pool_bwd(const float* __restrict__ gd, const uint8_t* __restrict__ idx, float* __restrict__ dz,
-           long total) {
-    constexpr int PH = H / 2, PW = W / 2;
+    constexpr int CH = (H + 1) / 2, CW = (W + 1) / 2;   // cells incl. the border
+    constexpr int C4 = C / 4;
     const long e = (long)blockIdx.x * 256 + threadIdx.x;
     if (e >= total) return;
-    const int c = (int)(e % C);
-    const long pix = e / C;
-    const int w = (int)(pix % W);
-    const int h = (int)((pix / W) % H);
-    const int s = (int)(pix / (W * H));
-    const int ph = h >> 1, pw = w >> 1;
-    float v = 0.f;
-    if (ph < PH && pw < PW) {
-        const long pe = (((long)s * PH + ph) * PW + pw) * C + c;
-        if (idx[pe] == (uint8_t)(((h & 1) << 1) | (w & 1))) {
-            v = NCHW_IN ? gd[(long)s * (C * PH * PW) + (c * PH + ph) * PW + pw] : gd[pe];
+    const int c = 4 * (int)(e % C4);
+    const long cell = e / C4;
+    const int cw = (int)(cell % CW);
+    const int ch = (int)((cell / CW) % CH);
+    const int n = (int)(cell / (CW * CH));
+    f32x4 g = f32x4{0.f, 0.f, 0.f, 0.f};
+    uint32_t id = 0xffffffffu;
+    if (ch < PH && cw < PW) {
+        const long pe = (((long)n * PH + ch) * PW + cw) * C + c;
+        id = *reinterpret_cast<const uint32_t*>(idx + pe);
+        if constexpr (NCHW_G) {
+            const float* b = gy + (long)n * (C * PH * PW) + (long)c * (PH * PW) + ch * PW + cw;
+            g.x = b[0];
+            g.y = b[PH * PW];
+            g.z = b[2 * PH * PW];
+            g.w = b[3 * PH * PW];
+        } else {
+            g = *reinterpret_cast<const f32x4*>(gy + pe);
         }
     }
-    dz[e] = v;
+#pragma unroll
+    for (int pos = 0; pos < 4; ++pos) {
+        const int h = 2 * ch + (pos >> 1), w = 2 * cw + (pos & 1);
+        if (h >= H || w >= W) continue;
+        f32x4 v;
+        v.x = ((id & 0xff) == (uint32_t)pos) ? g.x : 0.f;
+        v.y = (((id >> 8) & 0xff) == (uint32_t)pos) ? g.y : 0.f;
+        v.z = (((id >> 16) & 0xff) == (uint32_t)pos) ? g.z : 0.f;
+        v.w = ((id >> 24) == (uint32_t)pos) ? g.w : 0.f;
+        *reinterpret_cast<f32x4*>(dz + (((long)n * H + h) * W + w) * C + c) = v;
+    }
+}
+
+template <int H, int W, int C, bool NCHW_G>
+static int pool_scatter(const float* gy, const uint8_t* idx, float* dz, int S, hipStream_t st) {
+    const long total = (long)S * ((H + 1) / 2) * ((W + 1) / 2) * (C / 4);
+    hipLaunchKernelGGL((k_pool_scatter<H, W, C, NCHW_G>), dim3(ceil_div(total, 256)), dim3(256), 0,
+                       st, gy, idx, dz, total);
+    FLSIM_LAUNCH_CHECK();
+    return 0;
 }
 
 // =============================================================================================
@@ -376,6 +366,28 @@ static int conv_wgrad(const float* dz, const float* X, int S, int CO, int KP, fl
                                        2.0 * M * CO * kreal);
 }
 
+// forward conv fused with bias + ReLU + 2x2 max-pool + dropout: GEMM rows in pool-window order
+template <int IH, int IW, int CI, int CO, int FM, int FN, int WM, int WN, bool NCHW_OUT>
+static int conv_pool_fwd(const float* X, int S, const float* Wpk, int KP, float* d, uint8_t* idx,
+                         const float* bias, const WorkerRec* workers, uint64_t seed, uint32_t site,
+                         int dropout, hipStream_t st, int kid, int kreal) {
+    constexpr int NT = 64 * WM * WN;
+    constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
+    using AL = Im2colKC<IH, IW, CI, 2, BM, NT, true>;
+    using BL = RowsKC<BN, NT>;
+    AL al;
+    al.X = X;
+    al.M = S * AL::ROWS_PER_IMG;
+    BL bl;
+    bl.P = Wpk;
+    bl.ld = KP;
+    bl.NR = CO;
+    EpiPoolDrop<AL::PH, AL::PW, CO, NCHW_OUT> epi{d, idx, bias, workers, seed, site, THR_P25,
+                                                  SCALE_P25, dropout, al.M};
+    return launch_gemm<FM, FN, WM, WN>(al, bl, epi, al.M, CO, KP / GK, 1, st, kid,
+                                       2.0 * al.M * CO * kreal);
+}
+
 // =============================================================================================
 // Net plan
 // =============================================================================================
@@ -499,37 +511,21 @@ static int forward(const GradState& g, const WS& w, const float* theta, int S,
     // conv1, conv2 (+ReLU)  models.py:29-30
     RC((conv_like<32, 32, 4, 2, 2, 3, 4, 1>(w.x0, S, g.wf[0], 48, 48,
         EpiBiasRelu{w.a1, theta + P_OFF[1], S * 34 * 34, 48}, st, K_FWD1, 27)));
-    RC((conv_like<34, 34, 48, 2, 2, 3, 8, 1>(w.a1, S, g.wf[1], 48, 432,
-        EpiBiasRelu{w.a2, theta + P_OFF[3], S * 36 * 36, 48}, st, K_FWD2, 432)));
-    {   // pool1 + dropout1  models.py:31-32
-        const long tot = (long)S * 18 * 18 * 48;
-        hipLaunchKernelGGL((k_pool_drop_fwd<36, 36, 48, false>), dim3(ceil_div(tot, 256)), dim3(256),
-                           0, st, w.a2, w.d1, w.i1, workers, seed, SITE_DROP1, THR_P25, SCALE_P25,
-                           dropout, tot);
-        FLSIM_LAUNCH_CHECK();
-    }
+    // conv2 + ReLU + pool1 + dropout1 (models.py:30-32), one fused launch
+    RC((conv_pool_fwd<34, 34, 48, 48, 2, 3, 8, 1, false>(w.a1, S, g.wf[1], 432, w.d1, w.i1,
+        theta + P_OFF[3], workers, seed, SITE_DROP1, dropout, st, K_FWD2, 432)));
     RC((conv_like<18, 18, 48, 2, 4, 3, 4, 2>(w.d1, S, g.wf[2], 96, 432,
         EpiBiasRelu{w.a3, theta + P_OFF[5], S * 20 * 20, 96}, st, K_FWD3, 432)));
-    RC((conv_like<20, 20, 96, 2, 4, 3, 4, 2>(w.a3, S, g.wf[3], 96, 864,
-        EpiBiasRelu{w.a4, theta + P_OFF[7], S * 22 * 22, 96}, st, K_FWD4, 864)));
-    {
-        const long tot = (long)S * 11 * 11 * 96;
-        hipLaunchKernelGGL((k_pool_drop_fwd<22, 22, 96, false>), dim3(ceil_div(tot, 256)), dim3(256),
-                           0, st, w.a4, w.d2, w.i2, workers, seed, SITE_DROP2, THR_P25, SCALE_P25,
-                           dropout, tot);
-        FLSIM_LAUNCH_CHECK();
-    }
+    // conv4 + ReLU + pool2 + dropout1 (models.py:34-36)
+    RC((conv_pool_fwd<20, 20, 96, 96, 4, 3, 4, 2, false>(w.a3, S, g.wf[3], 864, w.d2, w.i2,
+        theta + P_OFF[7], workers, seed, SITE_DROP2, dropout, st, K_FWD4, 864)));
     RC((conv_like<11, 11, 96, 2, 2, 6, 4, 2>(w.d2, S, g.wf[4], 192, 864,
         EpiBiasRelu{w.a5, theta + P_OFF[9], S * 13 * 13, 192}, st, K_FWD5, 864)));
-    RC((conv_like<13, 13, 192, 2, 2, 6, 4, 2>(w.a5, S, g.wf[5], 192, 1728,
-        EpiBiasRelu{w.a6, theta + P_OFF[11], S * 15 * 15, 192}, st, K_FWD6, 1728)));
-    {
-        const long tot = (long)S * 7 * 7 * 192;
-        hipLaunchKernelGGL((k_pool_drop_fwd<15, 15, 192, true>), dim3(ceil_div(tot, 256)), dim3(256),
-                           0, st, w.a6, w.d3, w.i3, workers, seed, SITE_DROP3, THR_P25, SCALE_P25,
-                           dropout, tot);
-        FLSIM_LAUNCH_CHECK();
-    }
+    // conv6 + ReLU + pool3 + dropout1 (models.py:38-40), written in torch's flatten order
+    // (models.py:41) so linear1 keeps the torch weight layout; the floor-mode border row/column
+    // of the 15x15 output (dropped by the pool) is never computed
+    RC((conv_pool_fwd<13, 13, 192, 192, 2, 6, 4, 2, true>(w.a5, S, g.wf[5], 1728, w.d3, w.i3,
+        theta + P_OFF[11], workers, seed, SITE_DROP3, dropout, st, K_FWD6, 1728)));
     // linear1 + relu + dropout2 (models.py:41-43), split-K partials then finish
     {
         constexpr int NT = 256;
@@ -601,13 +597,8 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
         EpiDropMask de{w.gy, w.d3, s25, S, 9408};
         RC((launch_gemm<4, 4, 2, 2>(dl, wl, de, S, 9408, 512 / GK, 1, st, K_L1D, 2.0 * S * 512 * 9408)));
     }
-    // ---- pool3 backward -> dz6 (a6 buffer) ----
-    {
-        const long tot = (long)S * 15 * 15 * 192;
-        hipLaunchKernelGGL((k_pool_bwd<15, 15, 192, true>), dim3(ceil_div(tot, 256)), dim3(256), 0, st,
-                           w.gy, w.i3, w.a6, tot);
-        FLSIM_LAUNCH_CHECK();
-    }
+    // ---- pool3 backward -> dz6 (a6 buffer: conv6 fwd no longer writes it) ----
+    RC((pool_scatter<15, 15, 192, true>(w.gy, w.i3, w.a6, S, st)));
     float* dz6 = w.a6;
     // ---- conv6: wgrad (input a5), bias, dgrad -> dz5 = . * (a5 > 0) into gx ----
     RC((conv_wgrad<13, 13, 192, 6, 3, 2, 2>(dz6, w.a5, S, 192, 1728, g.sw[5], g.sb[5], GEO[5].ZW, st, K_WG6, 1728)));
@@ -618,12 +609,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC((conv_wgrad<11, 11, 96, 6, 3, 2, 2>(dz5, w.d2, S, 192, 864, g.sw[4], g.sb[4], GEO[4].ZW, st, K_WG5, 864)));
     RC((conv_like<13, 13, 192, 0, 4, 3, 4, 2>(dz5, S, g.wd[4], 96, 1728,
         EpiDropMask{w.gy, w.d2, s25, S * 11 * 11, 96}, st, K_DG5, 1728)));
-    {
-        const long tot = (long)S * 22 * 22 * 96;
-        hipLaunchKernelGGL((k_pool_bwd<22, 22, 96, false>), dim3(ceil_div(tot, 256)), dim3(256), 0, st,
-                           w.gy, w.i2, w.a4, tot);
-        FLSIM_LAUNCH_CHECK();
-    }
+    RC((pool_scatter<22, 22, 96, false>(w.gy, w.i2, w.a4, S, st)));
     float* dz4 = w.a4;
     // ---- conv4: wgrad (input a3), bias, dgrad -> dz3 = . * (a3 > 0) into gx ----
     RC((conv_wgrad<20, 20, 96, 3, 3, 2, 2>(dz4, w.a3, S, 96, 864, g.sw[3], g.sb[3], GEO[3].ZW, st, K_WG4, 864)));
@@ -634,12 +620,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC((conv_wgrad<18, 18, 48, 3, 3, 2, 2>(dz3, w.d1, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW, st, K_WG3, 432)));
     RC((conv_like<20, 20, 96, 0, 2, 3, 8, 1>(dz3, S, g.wd[2], 48, 864,
         EpiDropMask{w.gy, w.d1, s25, S * 18 * 18, 48}, st, K_DG3, 864)));
-    {
-        const long tot = (long)S * 36 * 36 * 48;
-        hipLaunchKernelGGL((k_pool_bwd<36, 36, 48, false>), dim3(ceil_div(tot, 256)), dim3(256), 0, st,
-                           w.gy, w.i1, w.a2, tot);
-        FLSIM_LAUNCH_CHECK();
-    }
+    RC((pool_scatter<36, 36, 48, false>(w.gy, w.i1, w.a2, S, st)));
     float* dz2 = w.a2;
     // ---- conv2: wgrad (input a1), bias, dgrad -> dz1 = . * (a1 > 0) into gx ----
     RC((conv_wgrad<34, 34, 48, 3, 3, 1, 3>(dz2, w.a1, S, 48, 432, g.sw[1], g.sb[1], GEO[1].ZW, st, K_WG2, 432)));

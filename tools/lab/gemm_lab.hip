@@ -8,7 +8,7 @@
 #include <algorithm>
 #include <vector>
 
-#include "loaders.h"
+#include "gemm_variants.h"
 
 using namespace flsim;
 
@@ -91,6 +91,72 @@ static void conv_wgrad(const char* tag, const float* dz, const float* X, float* 
     time_gemm<FM, FN, WM, WN>(tag, al, bl, epi, CO, KP, ceil_div(M, GK), Z, 2.0 * M * CO * kreal);
 }
 
+
+template <int FM, int FN, int WM, int WN, int KSUB, int PRIO, int MINW, class AL, class BL, class EPI>
+static double time_gemm_v(const char* tag, const AL& al, const BL& bl, const EPI& epi, int M, int N,
+                          int ksteps, int Z, double flops) {
+    constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
+    const int per = (ksteps + Z - 1) / Z;
+    const int tm = ceil_div(M, BM), tn = ceil_div(N, BN);
+    dim3 grid(tm * tn * Z);
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    auto k = gemm_kernel_v<FM, FN, WM, WN, KSUB, PRIO, MINW, AL, BL, EPI>;
+    for (int i = 0; i < 2; ++i) hipLaunchKernelGGL(k, grid, dim3(64 * WM * WN), 0, 0, al, bl, epi, ksteps, per, tm, tn);
+    CK(hipDeviceSynchronize());
+    const int iters = 5;
+    CK(hipEventRecord(e0, 0));
+    for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(k, grid, dim3(64 * WM * WN), 0, 0, al, bl, epi, ksteps, per, tm, tn);
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    ms /= iters;
+    printf("%-34s FM%d FN%d W%dx%d KSUB%d PRIO%d MINW%d tile %3dx%3d grid %7d  %8.3f ms  %6.1f TF/s\n", tag, FM, FN,
+           WM, WN, KSUB, PRIO, MINW, BM, BN, grid.x, ms, flops / (ms * 1e-3) / 1e12);
+    fflush(stdout);
+    return ms;
+}
+
+template <int IH, int CI, int PAD, int FM, int FN, int WM, int WN, int KSUB, int PRIO, int MINW>
+static void conv_fwd_v(const char* tag, const float* X, const float* W, const float* b, float* Y,
+                       int S, int CO, int kreal) {
+    constexpr int NT = 64 * WM * WN, BM = 16 * FM * WM, BN = 16 * FN * WN;
+    using AL = Im2colKC<IH, IH, CI, PAD, BM, NT>;
+    using BL = RowsKC<BN, NT>;
+    AL al;
+    al.X = X;
+    al.M = S * AL::OH * AL::OW;
+    BL bl;
+    bl.P = W;
+    const int KP = (9 * CI + 15) / 16 * 16;
+    bl.ld = KP;
+    bl.NR = CO;
+    EpiBiasRelu epi{Y, b, al.M, CO};
+    time_gemm_v<FM, FN, WM, WN, KSUB, PRIO, MINW>(tag, al, bl, epi, al.M, CO, KP / GK, 1, 2.0 * al.M * CO * kreal);
+}
+
+template <int IH, int CI, int FM, int FN, int WM, int WN, int KSUB, int PRIO, int MINW>
+static void conv_wgrad_v(const char* tag, const float* dz, const float* X, float* slab, float* bslab,
+                         int S, int CO, int Z, int kreal) {
+    constexpr int NT = 64 * WM * WN, BM = 16 * FM * WM, BN = 16 * FN * WN;
+    using AL = RowsKM<BM, NT>;
+    using BL = Im2colKM<IH, IH, CI, 2, BN, NT>;
+    const int M = S * BL::OH * BL::OW;
+    const int KP = (9 * CI + 15) / 16 * 16;
+    AL al;
+    al.P = dz;
+    al.ld = CO;
+    al.NK = M;
+    al.NC = CO;
+    BL bl;
+    bl.X = X;
+    bl.M = M;
+    EpiSlabAcc epi{slab, CO, KP, (long)CO * KP, bslab};
+    time_gemm_v<FM, FN, WM, WN, KSUB, PRIO, MINW>(tag, al, bl, epi, CO, KP, ceil_div(M, GK), Z, 2.0 * M * CO * kreal);
+}
+
 int main(int argc, char** argv) {
     const int S = 4096;
     const size_t big = (size_t)S * 36 * 36 * 48;   // largest activation
@@ -104,53 +170,29 @@ int main(int argc, char** argv) {
     auto want = [&](const char* t) { return !*only || strstr(t, only); };
 #define F(tag, IH, CI, PAD, CO, K, FM, FN, WM, WN) \
     if (want(tag)) conv_fwd<IH, CI, PAD, FM, FN, WM, WN>(tag, X, W, b, Y, S, CO, K);
+#define FV(tag, IH, CI, PAD, CO, K, FM, FN, WM, WN, KS, PR, MW) \
+    if (want(tag)) conv_fwd_v<IH, CI, PAD, FM, FN, WM, WN, KS, PR, MW>(tag, X, W, b, Y, S, CO, K);
 #define G(tag, IH, CI, CO, Z, K, FM, FN, WM, WN) \
     if (want(tag)) conv_wgrad<IH, CI, FM, FN, WM, WN>(tag, Y, X, slab, bsl, S, CO, Z, K);
-    // forward (PAD 2) and data-gradient (PAD 0) convolutions
-    F("fwd6 base", 13, 192, 2, 192, 1728, 4, 3, 2, 2)
-    F("fwd6 128x192 8w", 13, 192, 2, 192, 1728, 2, 6, 4, 2)
-    F("fwd5 base", 11, 96, 2, 192, 864, 4, 3, 2, 2)
-    F("fwd5 128x192 8w", 11, 96, 2, 192, 864, 2, 6, 4, 2)
-    F("fwd3 base", 18, 48, 2, 96, 432, 4, 3, 2, 2)
-    F("fwd3 256x96 8w", 18, 48, 2, 96, 432, 4, 3, 4, 2)
-    F("fwd3 128x96 8w", 18, 48, 2, 96, 432, 2, 3, 4, 2)
-    F("dg6 base", 15, 192, 0, 192, 1728, 4, 3, 2, 2)
-    F("dg6 128x192 8w", 15, 192, 0, 192, 1728, 2, 6, 4, 2)
-    F("dg5 base", 13, 192, 0, 96, 1728, 4, 3, 2, 2)
-    F("dg5 256x96 8w", 13, 192, 0, 96, 1728, 4, 3, 4, 2)
-    F("dg4 base", 22, 96, 0, 96, 864, 4, 3, 2, 2)
-    F("dg4 256x96 8w", 22, 96, 0, 96, 864, 4, 3, 4, 2)
-    F("dg3 base", 20, 96, 0, 48, 864, 4, 3, 4, 1)
-    F("dg3 256x48 8w", 20, 96, 0, 48, 864, 2, 3, 8, 1)
-    F("dg3 128x48", 20, 96, 0, 48, 864, 2, 3, 4, 1)
-    F("dg2 base", 36, 48, 0, 48, 432, 4, 3, 4, 1)
-    F("dg2 256x48 8w", 36, 48, 0, 48, 432, 2, 3, 8, 1)
-    F("dg2 128x48", 36, 48, 0, 48, 432, 2, 3, 4, 1)
-    F("fwd2 base", 34, 48, 2, 48, 432, 4, 3, 4, 1)
-    F("fwd2 256x48 8w", 34, 48, 2, 48, 432, 2, 3, 8, 1)
-    F("fwd1 base", 32, 4, 2, 48, 27, 4, 3, 4, 1)
-    F("fwd1 256x48 8w", 32, 4, 2, 48, 27, 2, 3, 8, 1)
-    F("fwd1 128x48", 32, 4, 2, 48, 27, 2, 3, 4, 1)
-    // weight gradients
-    G("wg6 base", 13, 192, 192, 128, 1728, 3, 3, 2, 3)
-    G("wg6 192x96 4w", 13, 192, 192, 128, 1728, 6, 3, 2, 2)
-    G("wg6 96x96 4w z256", 13, 192, 192, 256, 1728, 3, 3, 2, 2)
-    G("wg5 base", 11, 96, 192, 256, 864, 3, 3, 2, 3)
-    G("wg5 192x96 4w", 11, 96, 192, 256, 864, 6, 3, 2, 2)
-    G("wg5 96x96 4w", 11, 96, 192, 256, 864, 3, 3, 2, 2)
-    G("wg5 96x96 4w z512", 11, 96, 192, 512, 864, 3, 3, 2, 2)
-    G("wg4 96x96 4w z512", 20, 96, 96, 512, 864, 3, 3, 2, 2)
-    G("wg4 96x96 4w z1024", 20, 96, 96, 1024, 864, 3, 3, 2, 2)
-    G("wg3 base", 18, 48, 96, 1024, 432, 3, 3, 2, 3)
-    G("wg3 96x96 4w", 18, 48, 96, 1024, 432, 3, 3, 2, 2)
-    G("wg3 96x96 4w z2048", 18, 48, 96, 2048, 432, 3, 3, 2, 2)
-    G("wg3 96x48 2w z2048", 18, 48, 96, 2048, 432, 3, 3, 2, 1)
-    G("wg2 base", 34, 48, 48, 2048, 432, 3, 3, 1, 3)
-    G("wg2 48x96 2w", 34, 48, 48, 2048, 432, 3, 3, 1, 2)
-    G("wg2 48x192 4w", 34, 48, 48, 2048, 432, 3, 3, 1, 4)
-    G("wg2 48x48 1w z4096", 34, 48, 48, 4096, 432, 3, 3, 1, 1)
-    G("wg2 48x48 1w z8192", 34, 48, 48, 8192, 432, 3, 3, 1, 1)
-    G("wg1 base", 32, 4, 48, 4096, 27, 3, 3, 1, 1)
-    G("wg1 z8192", 32, 4, 48, 8192, 27, 3, 3, 1, 1)
+#define GV(tag, IH, CI, CO, Z, K, FM, FN, WM, WN, KS, PR, MW) \
+    if (want(tag)) conv_wgrad_v<IH, CI, FM, FN, WM, WN, KS, PR, MW>(tag, Y, X, slab, bsl, S, CO, Z, K);
+    F("fwd6 cur", 13, 192, 2, 192, 1728, 2, 6, 4, 2)
+    FV("fwd6 v1", 13, 192, 2, 192, 1728, 2, 6, 4, 2, 1, 0, 1)
+    FV("fwd6 ks2", 13, 192, 2, 192, 1728, 2, 6, 4, 2, 2, 0, 1)
+    FV("fwd6 prio", 13, 192, 2, 192, 1728, 2, 6, 4, 2, 1, 1, 1)
+    FV("fwd6 ks2 prio", 13, 192, 2, 192, 1728, 2, 6, 4, 2, 2, 1, 1)
+    FV("fwd6 minw2", 13, 192, 2, 192, 1728, 2, 6, 4, 2, 1, 0, 2)
+    FV("fwd6 ks2 minw2", 13, 192, 2, 192, 1728, 2, 6, 4, 2, 2, 0, 2)
+    FV("fwd6 4x3 ks2", 13, 192, 2, 192, 1728, 4, 3, 2, 2, 2, 0, 1)
+    FV("fwd6 4x6 ks2", 13, 192, 2, 192, 1728, 4, 6, 2, 2, 2, 0, 1)
+    FV("fwd6 4x6 ks1", 13, 192, 2, 192, 1728, 4, 6, 2, 2, 1, 0, 1)
+    F("fwd4 cur", 20, 96, 2, 96, 864, 4, 3, 4, 2)
+    FV("fwd4 ks2", 20, 96, 2, 96, 864, 4, 3, 4, 2, 2, 0, 1)
+    FV("fwd4 prio", 20, 96, 2, 96, 864, 4, 3, 4, 2, 1, 1, 1)
+    G("wg6 cur", 13, 192, 192, 128, 1728, 6, 3, 2, 2)
+    GV("wg6 ks2", 13, 192, 192, 128, 1728, 6, 3, 2, 2, 2, 0, 1)
+    GV("wg6 prio", 13, 192, 192, 128, 1728, 6, 3, 2, 2, 1, 1, 1)
+    GV("wg6 8w ks2", 13, 192, 192, 128, 1728, 3, 3, 4, 2, 2, 0, 1)
+    GV("wg6 6x6 ks1", 13, 192, 192, 128, 1728, 6, 6, 2, 1, 1, 0, 1)
     return 0;
 }
