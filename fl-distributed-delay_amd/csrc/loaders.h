@@ -27,13 +27,16 @@ struct Im2colKC {
     static constexpr int ROWS_PER_IMG = WIN ? 4 * PH * PW : OH * OW;
     static constexpr int TOTAL = ROWS * 4;
     static constexpr int UNITS = (TOTAL + NT - 1) / NT;
+    // CI % 16 == 0: a 16-deep k step lies inside one filter tap, so the tap and the channel base
+    // are block-uniform (scalar) and each unit needs one add and one mask test per step
+    static constexpr bool TAP_UNIFORM = CI % 16 == 0;
     static_assert(NT % 4 == 0, "");
     static_assert(CI == 4 || CI % 16 == 0, "");
 
     const float* X;
     int M;
-    int base[UNITS];
-    short oh[UNITS], ow[UNITS];
+    long base[UNITS];       // element offset of input pixel (oh - PAD, ow - PAD), channel 4q
+    short tapmask[UNITS];   // bit kh*3+kw set iff that tap of this output pixel is inside X
     short row[UNITS];
     int q;
 
@@ -45,39 +48,54 @@ struct Im2colKC {
             const int r = u >> 2;
             row[j] = (short)r;
             const int m = m0 + r;
+            base[j] = 0;
+            tapmask[j] = 0;
             if (u < TOTAL && m < M) {
                 const int nimg = m / ROWS_PER_IMG;
                 const int rem = m - nimg * ROWS_PER_IMG;
+                int oh, ow;
                 if constexpr (WIN) {
-                    const int q = rem >> 2;
-                    const int ph = q / PW;
-                    oh[j] = (short)(2 * ph + ((rem >> 1) & 1));
-                    ow[j] = (short)(2 * (q - ph * PW) + (rem & 1));
+                    const int qq = rem >> 2;
+                    const int ph = qq / PW;
+                    oh = 2 * ph + ((rem >> 1) & 1);
+                    ow = 2 * (qq - ph * PW) + (rem & 1);
                 } else {
-                    oh[j] = (short)(rem / OW);
-                    ow[j] = (short)(rem - (rem / OW) * OW);
+                    oh = rem / OW;
+                    ow = rem - oh * OW;
                 }
-                base[j] = nimg * (IH * IW * CI);
-            } else {
-                base[j] = -1;
-                oh[j] = 0;
-                ow[j] = 0;
+                base[j] = ((long)nimg * IH * IW + (long)(oh - PAD) * IW + (ow - PAD)) * CI + 4 * q;
+                int msk = 0;
+#pragma unroll
+                for (int t = 0; t < 9; ++t) {
+                    const int ih = oh + t / 3 - PAD, iw = ow + t % 3 - PAD;
+                    if ((unsigned)ih < (unsigned)IH && (unsigned)iw < (unsigned)IW) msk |= 1 << t;
+                }
+                tapmask[j] = (short)msk;
             }
         }
     }
     __device__ void load(int ks, f32x4 (&r)[UNITS]) const {
-        const int k = ks * GK + 4 * q;
-        const int khkw = k / CI;
-        const int ci = k - khkw * CI;
-        const int kh = khkw / 3;
-        const int kw = khkw - kh * 3;
+        if constexpr (TAP_UNIFORM) {
+            const int kk = ks * GK;                 // uniform
+            const int khkw = kk / CI;
+            const int ci0 = kk - khkw * CI;
+            const int kh = khkw / 3;
+            const long off = (long)(kh * IW + (khkw - 3 * kh)) * CI + ci0;
 #pragma unroll
-        for (int j = 0; j < UNITS; ++j) {
-            const int ih = oh[j] + kh - PAD;
-            const int iw = ow[j] + kw - PAD;
-            const bool ok = base[j] >= 0 && khkw < 9 && (unsigned)ih < (unsigned)IH &&
-                            (unsigned)iw < (unsigned)IW;
-            r[j] = ok ? ldg4(X + base[j] + (ih * IW + iw) * CI + ci) : zero4();
+            for (int j = 0; j < UNITS; ++j) {
+                const bool ok = khkw < 9 && ((tapmask[j] >> khkw) & 1);
+                r[j] = ok ? ldg4(X + base[j] + off) : zero4();
+            }
+        } else {
+            const int k = ks * GK + 4 * q;          // CI == 4: one tap per lane quad
+            const int khkw = k / CI;
+            const int kh = khkw / 3;
+            const long off = (long)(kh * IW + (khkw - 3 * kh)) * CI - 4 * q + (k - khkw * CI);
+#pragma unroll
+            for (int j = 0; j < UNITS; ++j) {
+                const bool ok = khkw < 9 && ((tapmask[j] >> khkw) & 1);
+                r[j] = ok ? ldg4(X + base[j] + off) : zero4();
+            }
         }
     }
     __device__ void store(float* lds, const f32x4 (&r)[UNITS]) const {

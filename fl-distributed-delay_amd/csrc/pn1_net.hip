@@ -287,25 +287,70 @@ __global__ void k_pack_dgrad(const float* __restrict__ W, float* __restrict__ Wd
 // =============================================================================================
 // epoch-end finalize: S_t (torch layout) = sum_z slab[z]  (fixed z order: deterministic)
 // =============================================================================================
-// conv weight: out[co][ci][kh][kw] = sum_z slab[z][co][khkw*CIP + ci]
-__global__ void k_fin_conv(const float* __restrict__ slab, int Z, int CO, int CI, int CIP, int KP,
-                           float* __restrict__ out) {
-    const int e = blockIdx.x * 256 + threadIdx.x;
-    if (e >= CO * CI * 9) return;
-    const int khkw = e % 9;
-    const int ci = (e / 9) % CI;
-    const int co = e / (9 * CI);
-    const long o = (long)co * KP + khkw * CIP + ci;
-    float acc = 0.f;
-    for (int z = 0; z < Z; ++z) acc += slab[(long)z * CO * KP + o];
-    out[e] = acc;
+// Block = `cols` element columns x `zl` z-lanes: lane tz sums slabs z = tz, tz + zl, ... (V
+// consecutive elements, one vector load per slab), then the zl partials are added in z-lane
+// order.  The order is fixed, so S_t is deterministic; every slab byte is read once, coalesced.
+// CO > 0 remaps the packed conv layout [co][khkw*CIP + ci] to torch's [co][ci][kh][kw].
+template <int V>
+__global__ void __launch_bounds__(256)
+k_fin_sum(const float* __restrict__ slab, int Z, long n, int zl, float* __restrict__ out, int CO,
+          int CI, int CIP, int KP) {
+    __shared__ float red[256 * V];
+    const int cols = 256 / zl;
+    const int tx = threadIdx.x % cols, tz = threadIdx.x / cols;
+    const long e0 = ((long)blockIdx.x * cols + tx) * V;
+    float acc[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) acc[v] = 0.f;
+    if (e0 < n) {
+        for (int z = tz; z < Z; z += zl) {
+            const float* p = slab + (long)z * n + e0;
+            if constexpr (V == 4) {
+                const f32x4 x = *reinterpret_cast<const f32x4*>(p);
+                acc[0] += x.x;
+                acc[1] += x.y;
+                acc[2] += x.z;
+                acc[3] += x.w;
+            } else {
+                acc[0] += p[0];
+            }
+        }
+    }
+#pragma unroll
+    for (int v = 0; v < V; ++v) red[threadIdx.x * V + v] = acc[v];
+    __syncthreads();
+    if (tz != 0 || e0 >= n) return;
+    for (int j = 1; j < zl; ++j)
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[v] += red[(j * cols + tx) * V + v];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        const long s = e0 + v;
+        if (CO > 0) {
+            const int co = (int)(s / KP);
+            const int k = (int)(s - (long)co * KP);
+            const int khkw = k / CIP, ci = k - (k / CIP) * CIP;
+            if (khkw < 9 && ci < CI) out[((long)co * CI + ci) * 9 + khkw] = acc[v];
+        } else {
+            out[s] = acc[v];
+        }
+    }
 }
-__global__ void k_fin_plain(const float* __restrict__ slab, int Z, long n, float* __restrict__ out) {
-    const long e = (long)blockIdx.x * 256 + threadIdx.x;
-    if (e >= n) return;
-    float acc = 0.f;
-    for (int z = 0; z < Z; ++z) acc += slab[(long)z * n + e];
-    out[e] = acc;
+
+static int fin_sum(const float* slab, int Z, long n, float* out, hipStream_t st, int CO = 0,
+                   int CI = 0, int CIP = 1, int KP = 1) {
+    int zl = 1;
+    while (zl < Z && zl < 16) zl *= 2;
+    const int cols = 256 / zl;
+    if (n % 4 == 0) {
+        hipLaunchKernelGGL(k_fin_sum<4>, dim3(ceil_div(n, 4L * cols)), dim3(256), 0, st, slab, Z, n,
+                           zl, out, CO, CI, CIP, KP);
+    } else {
+        hipLaunchKernelGGL(k_fin_sum<1>, dim3(ceil_div(n, (long)cols)), dim3(256), 0, st, slab, Z,
+                           n, zl, out, CO, CI, CIP, KP);
+    }
+    FLSIM_LAUNCH_CHECK();
+    return 0;
 }
 
 // =============================================================================================
@@ -732,23 +777,16 @@ int flsim_pn1_end_epoch(void* gradstate, float* grad_out, hipStream_t stream) {
     GradState g = gs_layout((float*)gradstate);
     for (int l = 0; l < 6; ++l) {
         const ConvGeo& c = GEO[l];
-        const long n = (long)c.CO * c.CI * 9;
-        hipLaunchKernelGGL(k_fin_conv, dim3(ceil_div(n, 256)), dim3(256), 0, stream, g.sw[l], c.ZW,
-                           c.CO, c.CI, c.CIP, c.KP, grad_out + P_OFF[2 * l]);
-        FLSIM_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_fin_plain, dim3(ceil_div(c.CO, 256)), dim3(256), 0, stream, g.sb[l], c.ZW,
-                           (long)c.CO, grad_out + P_OFF[2 * l + 1]);
-        FLSIM_LAUNCH_CHECK();
+        RC(fin_sum(g.sw[l], c.ZW, (long)c.CO * c.KP, grad_out + P_OFF[2 * l], stream, c.CO, c.CI,
+                   c.CIP, c.KP));
+        RC(fin_sum(g.sb[l], c.ZW, c.CO, grad_out + P_OFF[2 * l + 1], stream));
     }
-    struct { float* s; int z; long n; long off; } lin[6] = {
-        {g.l1w, ZL1W, 512L * 9408, P_OFF[12]}, {g.l1b, ZL1W, 512, P_OFF[13]},
-        {g.l2w, ZL2W, 256L * 512, P_OFF[14]},  {g.l2b, ZL2W, 256, P_OFF[15]},
-        {g.l3w, ZH, 2560, P_OFF[16]},          {g.l3b, ZH, 10, P_OFF[17]}};
-    for (auto& L : lin) {
-        hipLaunchKernelGGL(k_fin_plain, dim3(ceil_div(L.n, 256)), dim3(256), 0, stream, L.s, L.z, L.n,
-                           grad_out + L.off);
-        FLSIM_LAUNCH_CHECK();
-    }
+    RC(fin_sum(g.l1w, ZL1W, 512L * 9408, grad_out + P_OFF[12], stream));
+    RC(fin_sum(g.l1b, ZL1W, 512, grad_out + P_OFF[13], stream));
+    RC(fin_sum(g.l2w, ZL2W, 256L * 512, grad_out + P_OFF[14], stream));
+    RC(fin_sum(g.l2b, ZL2W, 256, grad_out + P_OFF[15], stream));
+    RC(fin_sum(g.l3w, ZH, 2560, grad_out + P_OFF[16], stream));
+    RC(fin_sum(g.l3b, ZH, 10, grad_out + P_OFF[17], stream));
     return 0;
 }
 

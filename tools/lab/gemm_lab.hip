@@ -92,7 +92,7 @@ static void conv_wgrad(const char* tag, const float* dz, const float* X, float* 
 }
 
 
-template <int FM, int FN, int WM, int WN, int KSUB, int PRIO, int MINW, class AL, class BL, class EPI>
+template <int FM, int FN, int WM, int WN, int KSUB, int PRIO, int MINW, int MODE = 0, class AL, class BL, class EPI>
 static double time_gemm_v(const char* tag, const AL& al, const BL& bl, const EPI& epi, int M, int N,
                           int ksteps, int Z, double flops) {
     constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
@@ -102,7 +102,7 @@ static double time_gemm_v(const char* tag, const AL& al, const BL& bl, const EPI
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    auto k = gemm_kernel_v<FM, FN, WM, WN, KSUB, PRIO, MINW, AL, BL, EPI>;
+    auto k = gemm_kernel_v<FM, FN, WM, WN, KSUB, PRIO, MINW, AL, BL, EPI, MODE>;
     for (int i = 0; i < 2; ++i) hipLaunchKernelGGL(k, grid, dim3(64 * WM * WN), 0, 0, al, bl, epi, ksteps, per, tm, tn);
     CK(hipDeviceSynchronize());
     const int iters = 5;
@@ -119,7 +119,7 @@ static double time_gemm_v(const char* tag, const AL& al, const BL& bl, const EPI
     return ms;
 }
 
-template <int IH, int CI, int PAD, int FM, int FN, int WM, int WN, int KSUB, int PRIO, int MINW>
+template <int IH, int CI, int PAD, int FM, int FN, int WM, int WN, int KSUB, int PRIO, int MINW, int MODE = 0>
 static void conv_fwd_v(const char* tag, const float* X, const float* W, const float* b, float* Y,
                        int S, int CO, int kreal) {
     constexpr int NT = 64 * WM * WN, BM = 16 * FM * WM, BN = 16 * FN * WN;
@@ -134,7 +134,7 @@ static void conv_fwd_v(const char* tag, const float* X, const float* W, const fl
     bl.ld = KP;
     bl.NR = CO;
     EpiBiasRelu epi{Y, b, al.M, CO};
-    time_gemm_v<FM, FN, WM, WN, KSUB, PRIO, MINW>(tag, al, bl, epi, al.M, CO, KP / GK, 1, 2.0 * al.M * CO * kreal);
+    time_gemm_v<FM, FN, WM, WN, KSUB, PRIO, MINW, MODE>(tag, al, bl, epi, al.M, CO, KP / GK, 1, 2.0 * al.M * CO * kreal);
 }
 
 template <int IH, int CI, int FM, int FN, int WM, int WN, int KSUB, int PRIO, int MINW>
@@ -176,23 +176,18 @@ int main(int argc, char** argv) {
     if (want(tag)) conv_wgrad<IH, CI, FM, FN, WM, WN>(tag, Y, X, slab, bsl, S, CO, Z, K);
 #define GV(tag, IH, CI, CO, Z, K, FM, FN, WM, WN, KS, PR, MW) \
     if (want(tag)) conv_wgrad_v<IH, CI, FM, FN, WM, WN, KS, PR, MW>(tag, Y, X, slab, bsl, S, CO, Z, K);
+#define FM_(tag, IH, CI, PAD, CO, K, FM, FN, WM, WN, MODE) \
+    if (want(tag)) conv_fwd_v<IH, CI, PAD, FM, FN, WM, WN, 1, 0, 1, MODE>(tag, X, W, b, Y, S, CO, K);
     F("fwd6 cur", 13, 192, 2, 192, 1728, 2, 6, 4, 2)
-    FV("fwd6 v1", 13, 192, 2, 192, 1728, 2, 6, 4, 2, 1, 0, 1)
-    FV("fwd6 ks2", 13, 192, 2, 192, 1728, 2, 6, 4, 2, 2, 0, 1)
-    FV("fwd6 prio", 13, 192, 2, 192, 1728, 2, 6, 4, 2, 1, 1, 1)
-    FV("fwd6 ks2 prio", 13, 192, 2, 192, 1728, 2, 6, 4, 2, 2, 1, 1)
-    FV("fwd6 minw2", 13, 192, 2, 192, 1728, 2, 6, 4, 2, 1, 0, 2)
-    FV("fwd6 ks2 minw2", 13, 192, 2, 192, 1728, 2, 6, 4, 2, 2, 0, 2)
-    FV("fwd6 4x3 ks2", 13, 192, 2, 192, 1728, 4, 3, 2, 2, 2, 0, 1)
-    FV("fwd6 4x6 ks2", 13, 192, 2, 192, 1728, 4, 6, 2, 2, 2, 0, 1)
-    FV("fwd6 4x6 ks1", 13, 192, 2, 192, 1728, 4, 6, 2, 2, 1, 0, 1)
+    F("fwd6 256x192 4x6 4x2", 13, 192, 2, 192, 1728, 4, 6, 4, 2)
+    FM_("fwd6 256x192 fixedload", 13, 192, 2, 192, 1728, 4, 6, 4, 2, 3)
+    FM_("fwd6 256x192 noload", 13, 192, 2, 192, 1728, 4, 6, 4, 2, 1)
+    F("fwd6 256x192 8x3 2x4", 13, 192, 2, 192, 1728, 8, 3, 2, 4)
+    F("fwd6 256x96 4x3 4x2", 13, 192, 2, 192, 1728, 4, 3, 4, 2)
+    F("fwd6 128x192 4x6 2x2", 13, 192, 2, 192, 1728, 4, 6, 2, 2)
+    F("fwd6 256x192 8x6 2x2", 13, 192, 2, 192, 1728, 8, 6, 2, 2)
     F("fwd4 cur", 20, 96, 2, 96, 864, 4, 3, 4, 2)
-    FV("fwd4 ks2", 20, 96, 2, 96, 864, 4, 3, 4, 2, 2, 0, 1)
-    FV("fwd4 prio", 20, 96, 2, 96, 864, 4, 3, 4, 2, 1, 1, 1)
-    G("wg6 cur", 13, 192, 192, 128, 1728, 6, 3, 2, 2)
-    GV("wg6 ks2", 13, 192, 192, 128, 1728, 6, 3, 2, 2, 2, 0, 1)
-    GV("wg6 prio", 13, 192, 192, 128, 1728, 6, 3, 2, 2, 1, 1, 1)
-    GV("wg6 8w ks2", 13, 192, 192, 128, 1728, 3, 3, 4, 2, 2, 0, 1)
-    GV("wg6 6x6 ks1", 13, 192, 192, 128, 1728, 6, 6, 2, 1, 1, 0, 1)
+    F("fwd4 256x96 8x3 2x2", 20, 96, 2, 96, 864, 8, 3, 2, 2)
+    F("fwd4 512x96 8x3 4x2", 20, 96, 2, 96, 864, 8, 3, 4, 2)
     return 0;
 }

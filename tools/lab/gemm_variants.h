@@ -7,7 +7,7 @@ namespace flsim {
 // KSUB 16-deep sub-steps per barrier (LDS stage = KSUB sub-tiles), PRIO: s_setprio 1 around the
 // MFMA block.
 template <int FM, int FN, int WAVES_M, int WAVES_N, int KSUB, int PRIO, int MINW, class AL,
-          class BL, class EPI>
+          class BL, class EPI, int MODE = 0>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, MINW)
 gemm_kernel_v(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, int tiles_m,
               int tiles_n) {
@@ -79,7 +79,8 @@ gemm_kernel_v(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, int
     int cur = 0;
     for (int ks = ks0; ks < ks1; ks += KSUB) {
         const bool more = ks + KSUB < ks1;
-        if (more) load_stage(ks + KSUB);
+        if (MODE == 0 && more) load_stage(ks + KSUB);
+        if (MODE == 3 && more) load_stage(ks0);
         if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int s = 0; s < KSUB; ++s) {
@@ -106,9 +107,9 @@ gemm_kernel_v(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, int
             }
         }
         if (PRIO) __builtin_amdgcn_s_setprio(0);
-        if (more) store_stage(lds + (cur ^ 1) * BUF, ks + KSUB);
-        __syncthreads();
-        cur ^= 1;
+        if ((MODE == 0 || MODE == 3) && more) store_stage(lds + (cur ^ 1) * BUF, ks + KSUB);
+        if (MODE != 2) __syncthreads();
+        if (MODE == 0 || MODE == 3) cur ^= 1;
     }
 
     if constexpr (EPI::ASUM) {
