@@ -60,6 +60,26 @@ k_fill_batch(const uint8_t* __restrict__ pool, const int32_t* __restrict__ label
     }
 }
 
+// evaluation batches (util.py:31-45 testloader, shuffle=False): sample s of the chunk is pool
+// image first + s (samples past n_images repeat the last image; their predictions are dropped)
+__global__ void __launch_bounds__(256)
+k_fill_seq(const uint8_t* __restrict__ pool, int first, int n_images, const float* __restrict__ lut,
+           float* __restrict__ x0, int32_t* __restrict__ y) {
+    const int s = blockIdx.x;
+    const int idx = first + (s < n_images ? s : n_images - 1);
+    if (threadIdx.x == 0) y[s] = 0;
+    const uint8_t* img = pool + (long)idx * 3072;
+    float* out = x0 + (long)s * 4096;
+    for (int p = threadIdx.x; p < 1024; p += 256) {
+        f32x4 v;
+        v.x = lut[img[p]];
+        v.y = lut[img[1024 + p]];
+        v.z = lut[img[2048 + p]];
+        v.w = 0.f;
+        *reinterpret_cast<f32x4*>(out + 4 * p) = v;
+    }
+}
+
 // explicit input (Worker.fwd_bkwd(inp, outp) facade): x NCHW fp32 [S][3][32][32], y int64
 __global__ void __launch_bounds__(256)
 k_load_input(const float* __restrict__ x, const int64_t* __restrict__ yin, float* __restrict__ x0,
@@ -167,7 +187,8 @@ k_linear_finish(const float* __restrict__ part, int Z, const float* __restrict__
 __global__ void __launch_bounds__(256)
 k_head(const float* __restrict__ e2, const float* __restrict__ W3, const float* __restrict__ b3,
        const int32_t* __restrict__ y, float* __restrict__ loss_s, float* __restrict__ dlog,
-       float* __restrict__ dh2, int S, int backward, float s50) {
+       float* __restrict__ dh2, int S, int backward, float s50,
+       int32_t* __restrict__ pred, int n_pred) {
     const int s = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (s >= S) return;
@@ -192,6 +213,12 @@ k_head(const float* __restrict__ e2, const float* __restrict__ W3, const float* 
 #pragma unroll
     for (int j = 0; j < 10; ++j) zy = (j == lab) ? z[j] : zy;
     if (lane == 0) loss_s[s] = (mx + logf(se)) - zy;
+    if (pred && lane == 0 && s < n_pred) {       // torch.max(outputs, 1): first max wins
+        int am = 0;
+#pragma unroll
+        for (int j = 1; j < 10; ++j) am = z[j] > z[am] ? j : am;
+        pred[s] = am;
+    }
     if (!backward) return;
     float g[10];
     const float inv = 1.f / se;
@@ -721,7 +748,7 @@ static int run_chunk(void* gradstate, const WS& w, const float* theta, const Wor
     RC(forward(g, w, theta, S, workers, seed, dropout, stream));
     hipLaunchKernelGGL(k_head, dim3(ceil_div(S, 4)), dim3(256), 0, stream, w.e2, theta + P_OFF[16],
                        theta + P_OFF[17], w.y, w.loss_s, w.dlog, w.dh2, S, backward_pass,
-                       dropout ? SCALE_P50 : 1.f);
+                       dropout ? SCALE_P50 : 1.f, (int32_t*)nullptr, 0);
     FLSIM_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_worker_loss, dim3(n_chunk_workers), dim3(128), 0, stream, w.loss_s,
                        worker_loss);
@@ -769,6 +796,34 @@ int flsim_pn1_fwd_bwd_input(void* gradstate, void* workspace, int max_samples, c
     FLSIM_LAUNCH_CHECK();
     return run_chunk(gradstate, w, theta, workers, n_samples / SAMPLES_PER_WORKER, seed, dropout,
                      backward_pass, worker_loss, stream);
+}
+
+// Evaluation (util.py:31-45 print_test_accuracy; main.py:190 central.model.eval(), so dropout is
+// off): forward of pool images [first, first + n_images) in chunks of max_samples, argmax of the
+// logits into pred[n_images].  Re-packs theta (the next begin_epoch packs again).
+int flsim_pn1_eval_pool(void* gradstate, void* workspace, int max_samples, const float* theta,
+                        const uint8_t* pool, int first, int n_images, const float* lut,
+                        int32_t* pred, hipStream_t stream) {
+    FLSIM_REQUIRE(gradstate && workspace && theta && pool && lut && pred, "null pointer");
+    FLSIM_REQUIRE(n_images > 0 && first >= 0, "bad image range");
+    FLSIM_REQUIRE(max_samples >= SAMPLES_PER_WORKER && max_samples % SAMPLES_PER_WORKER == 0,
+                  "max_samples must be a positive multiple of %d", SAMPLES_PER_WORKER);
+    GradState g = gs_layout((float*)gradstate);
+    WS w = ws_layout((char*)workspace, max_samples);
+    RC(pack_weights(g, theta, stream));
+    for (int c0 = 0; c0 < n_images; c0 += max_samples) {
+        const int n = n_images - c0 < max_samples ? n_images - c0 : max_samples;
+        const int S = ceil_div(n, SAMPLES_PER_WORKER) * SAMPLES_PER_WORKER;
+        hipLaunchKernelGGL(k_fill_seq, dim3(S), dim3(256), 0, stream, pool, first + c0, n, lut,
+                           w.x0, w.y);
+        FLSIM_LAUNCH_CHECK();
+        RC(forward(g, w, theta, S, nullptr, 0, 0, stream));
+        hipLaunchKernelGGL(k_head, dim3(ceil_div(S, 4)), dim3(256), 0, stream, w.e2,
+                           theta + P_OFF[16], theta + P_OFF[17], w.y, w.loss_s, w.dlog, w.dh2, S,
+                           0, 1.f, pred + c0, n);
+        FLSIM_LAUNCH_CHECK();
+    }
+    return 0;
 }
 
 // S_t (torch named_parameters layout, P floats) = sum of the epoch's slabs

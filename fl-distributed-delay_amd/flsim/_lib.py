@@ -18,6 +18,7 @@ EXPORTS = [
     "flsim_sched_state", "flsim_pn1_param_count", "flsim_pn1_gradstate_bytes",
     "flsim_pn1_workspace_bytes", "flsim_pn1_workspace_offset", "flsim_pn1_begin_epoch",
     "flsim_pn1_fwd_bwd_chunk", "flsim_pn1_fwd_bwd_input", "flsim_pn1_end_epoch",
+    "flsim_pn1_eval_pool",
     "flsim_aggregate_adam", "flsim_probe_enable", "flsim_probe_read", "flsim_probe_disable",
     "flsim_probe_kernel_count", "flsim_probe_kernel_name",
 ]
@@ -63,6 +64,8 @@ def lib():
         vp, vp, ctypes.c_int, vp, vp, vp, ctypes.c_int, vp, ctypes.c_uint64, ctypes.c_int,
         ctypes.c_int, vp, vp]
     L.flsim_pn1_end_epoch.argtypes = [vp, vp, vp]
+    L.flsim_pn1_eval_pool.argtypes = [vp, vp, ctypes.c_int, vp, vp, ctypes.c_int, ctypes.c_int,
+                                      vp, vp, vp]
     L.flsim_aggregate_adam.argtypes = [
         vp, ctypes.c_int, vp, ctypes.c_int, vp, vp, vp, ctypes.c_long, vp, ctypes.c_int,
         ctypes.c_long, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp]

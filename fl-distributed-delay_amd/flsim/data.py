@@ -17,15 +17,16 @@ import numpy as np
 import torch
 
 POOL_SIZE = 50000
+TEST_SIZE = 10000
 CLASSES_A = (0, 2, 3, 4, 5, 6, 7, 8)
 CLASSES_B = (1, 9)
 
 
-def make_pool(seed=0, size=POOL_SIZE):
+def make_pool(seed=0, size=POOL_SIZE, noise_seed=None):
     rs = np.random.RandomState(seed)
     proto = rs.randint(0, 256, size=(10, 3, 32, 32)).astype(np.int16)
     labels = (np.arange(size) % 10).astype(np.int64)
-    noise_rs = np.random.RandomState(seed + 1)
+    noise_rs = np.random.RandomState(seed + 1 if noise_seed is None else noise_seed)
     imgs = np.empty((size, 3, 32, 32), np.uint8)
     for s in range(0, size, 5000):
         e = min(size, s + 5000)
@@ -34,13 +35,40 @@ def make_pool(seed=0, size=POOL_SIZE):
     return imgs, labels
 
 
+def make_test_pool(seed=0, size=TEST_SIZE):
+    """The test split (main.py:72-73 CIFAR10(train=False), 10,000 images, 1,000 per class):
+    the training pool's class prototypes with an independent noise stream (seed + 2)."""
+    return make_pool(seed, size, noise_seed=seed + 2)
+
+
+def load_cifar10_bin(data_dir):
+    """Real CIFAR-10 from a local copy of the binary distribution (cifar-10-batches-bin:
+    data_batch_1..5.bin, test_batch.bin; records of 1 label byte + 3072 pixel bytes, R/G/B
+    planes of 32x32) -- the same NCHW u8 layout as the synthetic pool.  Returns
+    ((train_imgs, train_labels), (test_imgs, test_labels)).  No network access, no pickle."""
+    import os
+
+    def read(names):
+        raw = b"".join(open(os.path.join(data_dir, n), "rb").read() for n in names)
+        a = np.frombuffer(raw, np.uint8)
+        if a.size % 3073:
+            raise ValueError(f"{data_dir}: CIFAR-10 binary records are 3073 bytes")
+        a = a.reshape(-1, 3073)
+        return np.ascontiguousarray(a[:, 1:].reshape(-1, 3, 32, 32)), a[:, 0].astype(np.int64)
+
+    train = read([f"data_batch_{i}.bin" for i in range(1, 6)])
+    test = read(["test_batch.bin"])
+    return train, test
+
+
 def normalize_lut():
     u = np.arange(256, dtype=np.float32)
     return ((u / np.float32(255.0)) - np.float32(0.5)) / np.float32(0.5)
 
 
 class DevicePool:
-    """The pool, labels, class lists and normalisation table uploaded once to HBM."""
+    """The pool, labels, class lists and normalisation table uploaded once to HBM (the train
+    split; a test split uses the same class with pool=make_test_pool(seed))."""
 
     def __init__(self, device, seed=0, pool=None):
         imgs, labels = pool if pool is not None else make_pool(seed)

@@ -77,6 +77,16 @@ class PN1Engine:
             int(x.shape[0]), ptr(workers_dev), ctypes.c_uint64(seed), int(bool(dropout)),
             int(bool(backward)), ptr(loss_out), stream_ptr()))
 
+    def evaluate(self, theta, pool, first=0, n_images=None):
+        """Predictions (argmax of the logits, dropout off) for pool images [first, first + n):
+        util.print_test_accuracy's forward (util.py:31-45).  Returns a device int32 tensor."""
+        n = int(pool.imgs.shape[0]) - first if n_images is None else int(n_images)
+        pred = torch.empty(n, dtype=torch.int32, device=self.device)
+        check(lib().flsim_pn1_eval_pool(
+            ptr(self.gradstate), ptr(self.workspace), self.max_samples, ptr(theta), ptr(pool.imgs),
+            int(first), n, ptr(pool.lut), ptr(pred), stream_ptr()))
+        return pred
+
     def end_epoch(self, grad_out):
         check(lib().flsim_pn1_end_epoch(ptr(self.gradstate), ptr(grad_out), stream_ptr()))
 

@@ -19,8 +19,8 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from .data import DevicePool
-from .engine import PN1Engine, PN1_SIZES, padded, worker_table
+from .data import DevicePool, make_test_pool
+from .engine import PN1Engine, PN1_SHAPES, PN1_SIZES, padded, worker_table
 from .schedule import Schedule, reference_delays
 
 SEMANTICS = ("reference", "torch1")
@@ -39,7 +39,7 @@ class FLSimulation:
     def __init__(self, n_workers, delay=100, delays=None, throttle=False, lr=1e-3, seed=0,
                  semantics="reference", dropout=True, chunk_workers=32, device=None, theta0=None,
                  group=None, max_throttle=32, pool=None, betas=(0.9, 0.999), eps=1e-8,
-                 engine=None, device_pool=None):
+                 engine=None, device_pool=None, test_pool=None):
         if semantics not in SEMANTICS:
             raise NotImplementedError(f"semantics {semantics!r} (supported: {SEMANTICS})")
         self.n = int(n_workers)
@@ -83,6 +83,8 @@ class FLSimulation:
         self.free_slots = []
         self.trace = []
         self.loss_log = []        # per epoch: float (synced) or (device tensor, fast mask)
+        self._test_src = test_pool  # (imgs, labels) of the test split, or None = synthetic
+        self._test = None
 
     # ---------------------------------------------------------------------------------------------
     def _slot(self):
@@ -189,6 +191,88 @@ class FLSimulation:
                 out.append(e)
         self.loss_log = list(out)
         return out
+
+    # ---------------------------------------------------------------------------------------------
+    def evaluate(self):
+        """util.print_test_accuracy (util.py:31-45) as main.py:190,196-210 uses it: the central
+        model in eval mode (dropout off) over the whole test split, batches in order.  Returns
+        (accuracy %, [per-class accuracy %] * 10).  The reference logs np.mean of the first as
+        'Avg. Test Accuracy' and means the last class's entry as 'Class 9 Test Accuracy'
+        (main.py:203 indexes the scalar util returns; here the per-class list exists)."""
+        if self._test is None:
+            src = self._test_src if self._test_src is not None else make_test_pool(self.seed)
+            self._test = DevicePool(self.device, self.seed, src)
+        pred = self.engine.evaluate(self.theta, self._test)
+        labels = self._test.labels
+        ok = (pred == labels)
+        acc = 100.0 * int(ok.sum()) / int(labels.numel())
+        per = []
+        for c in range(10):
+            sel = labels == c
+            nc = int(sel.sum())
+            per.append(100.0 * int((ok & sel).sum()) / nc if nc else float("nan"))
+        return acc, per
+
+    def model_state_dict(self):
+        """models.py PerformantNet1 state_dict (torch.save-compatible with the reference's
+        main.py:98-100 / :192-194 load_state_dict / save)."""
+        from collections import OrderedDict
+        from .engine import split_views
+        return OrderedDict((name, v.detach().cpu().clone())
+                           for (name, _), v in zip(PN1_SHAPES, split_views(self.theta)))
+
+    # -- checkpoint / resume ----------------------------------------------------------------------
+    def checkpoint(self):
+        """Everything needed to continue bit-for-bit: theta, Adam m/v/step, the epoch counter,
+        the FIFO'd stale gradients still referenced, the loss log.  The schedule and the numpy
+        k-draws are deterministic scans and are replayed on restore."""
+        return {
+            "format": "flsim-checkpoint-1",
+            "config": {"n": self.n, "delays": torch.from_numpy(self.delays.copy()),
+                       "throttle": self.throttle, "seed": self.seed, "semantics": self.semantics,
+                       "dropout": self.dropout, "lr": self.lr},
+            "epoch": len(self.trace), "step": self.step,
+            "theta": self.theta.detach().cpu(), "m": self.m.detach().cpu(),
+            "v": self.v.detach().cpu(),
+            "stale": {int(src): (slot[:self.P].detach().cpu(), int(rc))
+                      for src, (slot, rc) in self.stale_store.items()},
+            "loss_log": [float(x) for x in self.losses()],
+        }
+
+    def save_checkpoint(self, path):
+        torch.save(self.checkpoint(), path)
+
+    def restore(self, ck):
+        """Resume from checkpoint() / save_checkpoint() output (a dict, or a path loaded with
+        weights_only=True).  The simulation must be fresh and built with the same config."""
+        if isinstance(ck, (str, bytes)) or hasattr(ck, "__fspath__"):
+            ck = torch.load(ck, map_location="cpu", weights_only=True)
+        if ck.get("format") != "flsim-checkpoint-1":
+            raise ValueError("not an flsim checkpoint")
+        cfg = ck["config"]
+        mine = {"n": self.n, "throttle": self.throttle, "seed": self.seed,
+                "semantics": self.semantics, "dropout": self.dropout}
+        for k, v in mine.items():
+            if cfg[k] != v:
+                raise ValueError(f"checkpoint {k}={cfg[k]!r} differs from this run ({v!r})")
+        if not np.array_equal(cfg["delays"].numpy(), self.delays):
+            raise ValueError("checkpoint delays differ from this run")
+        if self.trace:
+            raise ValueError("restore() needs a fresh simulation")
+        T = int(ck["epoch"])
+        for _ in range(T):                    # replay the integer scan and the k-draws
+            self.trace.append(self.sched.next_epoch())
+            self.rs.randint(0, self.n, size=self.n)
+        self.step = int(ck["step"])
+        self.theta.copy_(ck["theta"].to(self.device))
+        self.m.copy_(ck["m"].to(self.device))
+        self.v.copy_(ck["v"].to(self.device))
+        self.stale_store = {}
+        for src, (vals, rc) in ck["stale"].items():
+            slot = self._slot()
+            slot[:self.P].copy_(vals.to(self.device))
+            self.stale_store[int(src)] = [slot, int(rc)]
+        self.loss_log = list(ck["loss_log"])
 
     def executed_worker_steps(self, plan):
         return int(plan.computes.sum())

@@ -7,9 +7,15 @@ Same flags and defaults (main.py:38-53): --n_workers --n_epochs --batch_size --l
 all-reduce per epoch.  'Avg. Loss' per epoch (main.py:185) goes to --log (JSONL; tensorboard is
 not installed) and stdout.
 
-Differences forced by the environment: the data is a seeded synthetic CIFAR-shaped
-pool (no network for CIFAR10); RNG streams are seeded (--seed) and dropout / sampling use the
-counter-based spec; test-accuracy evaluation (main.py:196-210) is not part of the hot path yet.
+Test accuracy every 100 epochs and at the end (main.py:190,196-210) runs on the device
+(FLSimulation.evaluate, dropout off) and is logged as 'Avg. Test Accuracy' and 'Class 9 Test
+Accuracy'.  --save_model writes saved_model_{t}.pt state_dicts every 100 epochs (main.py:192-194,
+reference default off).  --checkpoint / --resume save and continue the whole simulation state.
+
+Differences forced by the environment: without --data_dir the data is a seeded
+synthetic CIFAR-shaped pool (no network for CIFAR10; --data_dir reads a local copy of the
+CIFAR-10 binary distribution); RNG streams are seeded (--seed) and dropout / sampling use the
+counter-based spec.
 """
 import argparse
 import json
@@ -39,7 +45,15 @@ def parse(argv=None):
                    help='stale entry = S_{t-d} (torch>=2 aliasing) or zeros (torch 1.x)')
     p.add_argument('--no-dropout', action='store_true')
     p.add_argument('--chunk', type=int, default=32, help='workers per worker-batched launch')
-    p.add_argument('--log', type=str, default=None, help='JSONL scalar log (Avg. Loss)')
+    p.add_argument('--log', type=str, default=None,
+                   help="JSONL scalar log ('Avg. Loss', 'Avg. Test Accuracy', 'Class 9 ...')")
+    p.add_argument('--data_dir', type=str, default=None,
+                   help='local cifar-10-batches-bin directory (default: synthetic pool)')
+    p.add_argument('--eval_every', type=int, default=100, help='main.py:196 (0 = only at end)')
+    p.add_argument('--save_model', action='store_true', help='main.py:192-194 saved_model_{t}.pt')
+    p.add_argument('--checkpoint', type=str, default=None, help='write a resumable checkpoint')
+    p.add_argument('--checkpoint_every', type=int, default=0)
+    p.add_argument('--resume', type=str, default=None, help='continue from a checkpoint')
     return p.parse_args(argv)
 
 
@@ -65,22 +79,52 @@ def main(argv=None):
         theta0 = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
     if rank == 0:
         print(dev)
+    pool = test_pool = None
+    if args.data_dir:
+        from flsim.data import load_cifar10_bin
+        pool, test_pool = load_cifar10_bin(args.data_dir)
     sim = FLSimulation(args.n_workers, delay=args.delay, throttle=args.throttle,
                        lr=args.learning_rate, seed=args.seed, semantics=args.semantics,
                        dropout=not args.no_dropout, chunk_workers=args.chunk, device=dev,
-                       theta0=theta0)
-    log = open(args.log, "w") if (args.log and rank == 0) else None
+                       theta0=theta0, pool=pool, test_pool=test_pool)
+    if args.resume:
+        sim.restore(args.resume)
+    log = open(args.log, "a" if args.resume else "w") if (args.log and rank == 0) else None
     t0 = time.time()
-    for t in range(args.n_epochs):
+
+    def emit(tag, value, t):
+        if rank != 0:
+            return
+        rec = {"tag": tag, "value": value, "step": t, "wall": time.time() - t0}
+        if log:
+            log.write(json.dumps(rec) + "\n")
+            log.flush()
+
+    t = len(sim.trace) - 1
+    for t in range(len(sim.trace), args.n_epochs):
         loss = sim.epoch()
-        if rank == 0:
-            rec = {"tag": "Avg. Loss", "value": loss, "step": t, "wall": time.time() - t0,
-                   "executed_worker_steps": int(sim.trace[-1].computes.sum())}
-            if log:
-                log.write(json.dumps(rec) + "\n")
-                log.flush()
-            if t % 10 == 0 or t == args.n_epochs - 1:
-                print(f"epoch {t} Avg. Loss {loss:.5f}", flush=True)
+        emit("Avg. Loss", loss, t)                                     # main.py:185
+        if rank == 0 and (t % 10 == 0 or t == args.n_epochs - 1):
+            print(f"epoch {t} Avg. Loss {loss:.5f}", flush=True)
+        if args.save_model and t % 100 == 0 and t > 0 and rank == 0:   # main.py:192-194
+            torch.save(sim.model_state_dict(), "saved_model_{}.pt".format(t))
+        if args.eval_every and t % args.eval_every == 0 and t > 0:     # main.py:196-203
+            acc, per = sim.evaluate()
+            emit("Avg. Test Accuracy", acc, t)
+            emit("Class 9 Test Accuracy", per[-1], t)
+            if rank == 0:
+                print(f"Accuracy of the network on the {len(sim._test.labels)} test images: "
+                      f"{int(acc)} %", flush=True)
+        if args.checkpoint and args.checkpoint_every and (t + 1) % args.checkpoint_every == 0 \
+                and rank == 0:
+            sim.save_checkpoint(args.checkpoint)
+    acc, per = sim.evaluate()                                           # main.py:205-210
+    emit("Avg. Test Accuracy", acc, t)
+    emit("Class 9 Test Accuracy", per[-1], t)
+    if rank == 0:
+        print(f"Accuracy of the network on the {len(sim._test.labels)} test images: {int(acc)} %")
+    if args.checkpoint and rank == 0:
+        sim.save_checkpoint(args.checkpoint)
     if log:
         log.close()
     if rank == 0:

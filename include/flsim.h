@@ -76,6 +76,14 @@ int flsim_pn1_fwd_bwd_input(void* gradstate, void* workspace, int max_samples, c
                             const WorkerRec* workers, uint64_t seed, int dropout,
                             int backward_pass, float* worker_loss, flsim_stream_t stream);
 int flsim_pn1_end_epoch(void* gradstate, float* grad_out, flsim_stream_t stream);
+/* Evaluation: replaces util.print_test_accuracy (util.py:31-45) as called at main.py:196-210
+ * after central.model.eval() (main.py:190: dropout off).  Forward of pool images
+ * [first, first + n_images) (u8 NCHW 3x32x32, normalised through `lut`), predictions = argmax of
+ * the logits (torch.max(outputs, 1): first maximum wins) into pred (device int32[n_images]).
+ * Uses the gradstate's packed-weight area (re-packed from theta). */
+int flsim_pn1_eval_pool(void* gradstate, void* workspace, int max_samples, const float* theta,
+                        const uint8_t* pool, int first, int n_images, const float* lut,
+                        int32_t* pred, flsim_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Fused server step: replaces Agg.rule = rule() (main.py:23-25, agents.py:43-45: per-tensor

@@ -236,3 +236,16 @@ class OracleSim:
 
 def O_init(seed):
     return init_params(seed)
+
+
+def predict(theta_np, imgs_u8, batch=500):
+    """util.py:31-45 forward in eval mode (no dropout): argmax of the logits per image (torch.max
+    -> first maximum), fp32 torch CPU.  imgs_u8: [n, 3, 32, 32] uint8 pool images."""
+    params = [torch.from_numpy(a) for a in split_flat(theta_np.astype(np.float32))]
+    lut = O.normalize_lut()
+    out = []
+    with torch.no_grad():
+        for s in range(0, len(imgs_u8), batch):
+            x = torch.from_numpy(lut[imgs_u8[s:s + batch]])
+            out.append(torch.max(forward(params, x, None), 1)[1].numpy())
+    return np.concatenate(out).astype(np.int32)

@@ -94,11 +94,11 @@ def sample_slots(seed, t, worker, length, n=BATCH):
 # ---------------------------------------------------------------------------------------------
 # Synthetic data spec: CIFAR-shaped uint8 pool (3x32x32), labels j % 10.
 # ---------------------------------------------------------------------------------------------
-def make_pool(seed=0, size=POOL_SIZE):
+def make_pool(seed=0, size=POOL_SIZE, noise_seed=None):
     rs = np.random.RandomState(seed)
     proto = rs.randint(0, 256, size=(10, 3, 32, 32)).astype(np.int16)
     labels = (np.arange(size) % 10).astype(np.int64)
-    rs2 = np.random.RandomState(seed + 1)
+    rs2 = np.random.RandomState(seed + 1 if noise_seed is None else noise_seed)
     imgs = np.empty((size, 3, 32, 32), np.uint8)
     step = 5000
     for s in range(0, size, step):
@@ -106,6 +106,12 @@ def make_pool(seed=0, size=POOL_SIZE):
         noise = rs2.randint(-48, 49, size=(e - s, 3, 32, 32)).astype(np.int16)
         imgs[s:e] = np.clip(proto[labels[s:e]] + noise, 0, 255).astype(np.uint8)
     return imgs, labels
+
+
+def make_test_pool(seed=0, size=10000):
+    """Test split spec (replaces main.py:72-73 CIFAR10(train=False)): same prototypes, noise
+    stream seed + 2."""
+    return make_pool(seed, size, noise_seed=seed + 2)
 
 
 def class_lists(labels):

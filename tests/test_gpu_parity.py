@@ -361,3 +361,54 @@ def test_gradient_teacher_forced_decisions(pool, dropout, items):
         off += n
     np.testing.assert_allclose(loss.cpu().numpy(), lrefs, atol=1e-5)
     assert max(worst.values()) <= 2e-5, worst
+
+
+def test_eval_predictions_match_oracle(pool):
+    """Device evaluation (util.py:31-45, dropout off) vs the oracle's fp32 CPU forward: chunks of
+    256 samples and a ragged last chunk (1000 images), predictions = argmax with first-max ties.
+    Predictions may differ only where two logits are within fp32 noise of each other."""
+    from flsim.data import DevicePool, make_test_pool
+    from flsim.engine import PN1Engine
+    from oracle import model_ref as MR
+    sim = MR.OracleSim(4, delay=2, pool=pool)
+    test = make_test_pool(0, size=1000)
+    eng = PN1Engine(DEV, chunk_workers=2)
+    dtest = DevicePool(DEV, 0, test)
+    theta = torch.from_numpy(sim.theta.copy()).to(DEV)
+    pred = eng.evaluate(theta, dtest).cpu().numpy()
+    ref = MR.predict(sim.theta, test[0])
+    assert pred.shape == (1000,)
+    assert (pred == ref).mean() >= 0.995, (pred != ref).sum()
+    pred2 = eng.evaluate(theta, dtest, first=100, n_images=37).cpu().numpy()
+    assert np.array_equal(pred2, pred[100:137])
+
+
+def test_simulation_evaluate_and_checkpoint_resume(pool, tmp_path):
+    """FLSimulation.evaluate returns the reference's accuracy numbers; a run cut in two by
+    save_checkpoint / restore continues bit for bit (theta, Adam state, FIFO'd stale gradient)."""
+    from flsim.sim import FLSimulation
+    n, d, total, cut = 4, 2, 5, 3
+    ref = FLSimulation(n, delay=d, throttle=True, device=DEV, chunk_workers=2, pool=pool)
+    for _ in range(total):
+        ref.epoch()
+    acc, per = ref.evaluate()
+    assert 0.0 <= acc <= 100.0 and len(per) == 10
+    labels = ref._test.labels.cpu().numpy()
+    assert abs(acc - np.mean([per[c] for c in range(10)])) < 1e-6   # balanced classes
+    a = FLSimulation(n, delay=d, throttle=True, device=DEV, chunk_workers=2, pool=pool)
+    for _ in range(cut):
+        a.epoch()
+    path = str(tmp_path / "ck.pt")
+    a.save_checkpoint(path)
+    b = FLSimulation(n, delay=d, throttle=True, device=DEV, chunk_workers=2, pool=pool)
+    b.restore(path)
+    for _ in range(total - cut):
+        b.epoch()
+    for x, y in ((b.theta, ref.theta), (b.m, ref.m), (b.v, ref.v)):
+        assert torch.equal(x, y)
+    assert b.losses() == ref.losses()
+    sd = b.model_state_dict()
+    from FL.models import PerformantNet1
+    m = PerformantNet1()
+    m.load_state_dict(sd)                     # the reference's load_state_dict contract
+    assert len(labels) == 10000

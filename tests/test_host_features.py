@@ -1,0 +1,77 @@
+"""CPU tests of the host-side features around the hot path: checkpoint / resume (replayed
+schedule + numpy k-draws), the CIFAR-10 binary reader (main.py:70-73 data from a local copy), the
+test-split spec (independent implementations in flsim.data and the oracle agree)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from test_dist_cpu import P, StandInEngine
+
+
+def _sim(n, d, thr):
+    from flsim.sim import FLSimulation
+    return FLSimulation(n, delay=d, throttle=thr, device="cpu", engine=StandInEngine(),
+                        device_pool=object(), theta0=torch.zeros(P))
+
+
+@pytest.mark.parametrize("thr", [False, True])
+def test_checkpoint_resume_continues_bit_for_bit(tmp_path, thr):
+    n, d, total, cut = 11, 3, 9, 4          # the cut leaves a stale gradient in the FIFO
+    ref = _sim(n, d, thr)
+    ref_losses = [ref.epoch() for _ in range(total)]
+    a = _sim(n, d, thr)
+    for _ in range(cut):
+        a.epoch()
+    path = str(tmp_path / "ck.pt")
+    a.save_checkpoint(path)
+    assert a.checkpoint()["stale"], "the cut should hold a FIFO entry"
+    b = _sim(n, d, thr)
+    b.restore(path)                          # torch.load(weights_only=True) inside
+    for _ in range(total - cut):
+        b.epoch()
+    assert np.array_equal(b.theta.numpy().view(np.uint32), ref.theta.numpy().view(np.uint32))
+    assert [(p.t, p.computes.tobytes(), p.stale) for p in b.trace] == \
+           [(p.t, p.computes.tobytes(), p.stale) for p in ref.trace]
+    assert b.losses() == ref_losses
+
+
+def test_restore_rejects_a_different_run(tmp_path):
+    a = _sim(11, 3, False)
+    a.epoch()
+    ck = a.checkpoint()
+    with pytest.raises(ValueError):
+        _sim(11, 4, False).restore(ck)
+    with pytest.raises(ValueError):
+        _sim(12, 3, False).restore(ck)
+
+
+def test_cifar10_binary_reader(tmp_path):
+    from flsim.data import load_cifar10_bin
+    rs = np.random.RandomState(0)
+    want = {}
+    for name, nrec in [(f"data_batch_{i}.bin", 3) for i in range(1, 6)] + [("test_batch.bin", 4)]:
+        lab = rs.randint(0, 10, nrec).astype(np.uint8)
+        img = rs.randint(0, 256, (nrec, 3072)).astype(np.uint8)
+        (tmp_path / name).write_bytes(np.concatenate([lab[:, None], img], 1).tobytes())
+        want[name] = (lab, img)
+    (tr_x, tr_y), (te_x, te_y) = load_cifar10_bin(str(tmp_path))
+    assert tr_x.shape == (15, 3, 32, 32) and tr_x.dtype == np.uint8 and te_x.shape == (4, 3, 32, 32)
+    assert np.array_equal(tr_y[:3], want["data_batch_1.bin"][0])
+    assert np.array_equal(tr_x[3].reshape(-1), want["data_batch_2.bin"][1][0])
+    assert np.array_equal(te_y, want["test_batch.bin"][0])
+    (tmp_path / "test_batch.bin").write_bytes(b"\0" * 100)
+    with pytest.raises(ValueError):
+        load_cifar10_bin(str(tmp_path))
+
+
+def test_test_split_spec_matches_oracle():
+    from flsim.data import make_test_pool
+    from oracle import oracle as O
+    a, la = make_test_pool(3, size=2000)
+    b, lb = O.make_test_pool(3, size=2000)
+    assert np.array_equal(a, b) and np.array_equal(la, lb)
+    tr, _ = O.make_pool(3, size=2000)
+    assert not np.array_equal(a, tr)         # independent noise from the train split
+    assert np.bincount(la, minlength=10).tolist() == [200] * 10

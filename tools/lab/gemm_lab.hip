@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "gemm_variants.h"
+#include "gemm_glds.h"
 
 using namespace flsim;
 
@@ -157,6 +158,55 @@ static void conv_wgrad_v(const char* tag, const float* dz, const float* X, float
     time_gemm_v<FM, FN, WM, WN, KSUB, PRIO, MINW>(tag, al, bl, epi, CO, KP, ceil_div(M, GK), Z, 2.0 * M * CO * kreal);
 }
 
+template <int IH, int CI, int PAD, int FM, int FN, int WM, int WN>
+static void conv_fwd_glds(const char* tag, const float* X, const float* W, const float* b, float* Y,
+                          int S, int CO, int kreal, const float* zp) {
+    constexpr int NW = WM * WN, BM = 16 * FM * WM, BN = 16 * FN * WN;
+    using AL = Im2colGlds<IH, IH, CI, PAD, BM, NW>;
+    using BL = RowsGlds<BN, NW>;
+    AL al;
+    al.X = X;
+    al.zp = zp;
+    al.M = S * AL::OH * AL::OW;
+    BL bl;
+    bl.P = W;
+    bl.zp = zp;
+    const int KP = (9 * CI + 15) / 16 * 16;
+    bl.ld = KP;
+    bl.NR = CO;
+    EpiBiasRelu epi{Y, b, al.M, CO};
+    const int M = al.M, N = CO, ksteps = KP / GK;
+    const int tm = ceil_div(M, BM), tn = ceil_div(N, BN);
+    dim3 grid(tm * tn);
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    auto k = gemm_glds<FM, FN, WM, WN, AL, BL, EpiBiasRelu>;
+    for (int i = 0; i < 2; ++i) hipLaunchKernelGGL(k, grid, dim3(64 * NW), 0, 0, al, bl, epi, ksteps, ksteps, tm, tn);
+    CK(hipDeviceSynchronize());
+    const int iters = 5;
+    CK(hipEventRecord(e0, 0));
+    for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(k, grid, dim3(64 * NW), 0, 0, al, bl, epi, ksteps, ksteps, tm, tn);
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    ms /= iters;
+    printf("%-34s FM%d FN%d W%dx%d GLDS tile %3dx%3d grid %7d  %8.3f ms  %6.1f TF/s\n", tag, FM, FN, WM, WN,
+           BM, BN, grid.x, ms, 2.0 * M * N * kreal / (ms * 1e-3) / 1e12);
+    fflush(stdout);
+}
+
+// copy of Y after the reference kernel, to check the glds kernel's output
+static void check_same(const float* Y, const float* Yref, size_t n, const char* tag) {
+    std::vector<float> a(n), b(n);
+    CK(hipMemcpy(a.data(), Y, n * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(b.data(), Yref, n * 4, hipMemcpyDeviceToHost));
+    size_t bad = 0;
+    for (size_t i = 0; i < n; ++i) bad += a[i] != b[i];
+    printf("  check %s: %zu of %zu differ\n", tag, bad, n);
+}
+
 int main(int argc, char** argv) {
     const int S = 4096;
     const size_t big = (size_t)S * 36 * 36 * 48;   // largest activation
@@ -166,6 +216,8 @@ int main(int argc, char** argv) {
     float* b = dalloc(256, 0.01f);
     float* slab = dalloc((size_t)8192 * 48 * 432 > (size_t)512 * 192 * 1728 ? (size_t)8192 * 48 * 432 : (size_t)512 * 192 * 1728, 0.f);
     float* bsl = dalloc(8192 * 192, 0.f);
+    float* zp = dalloc(64, 0.f);
+    float* Y2 = dalloc(big, 0.f);
     const char* only = argc > 1 ? argv[1] : "";
     auto want = [&](const char* t) { return !*only || strstr(t, only); };
 #define F(tag, IH, CI, PAD, CO, K, FM, FN, WM, WN) \
@@ -178,16 +230,18 @@ int main(int argc, char** argv) {
     if (want(tag)) conv_wgrad_v<IH, CI, FM, FN, WM, WN, KS, PR, MW>(tag, Y, X, slab, bsl, S, CO, Z, K);
 #define FM_(tag, IH, CI, PAD, CO, K, FM, FN, WM, WN, MODE) \
     if (want(tag)) conv_fwd_v<IH, CI, PAD, FM, FN, WM, WN, 1, 0, 1, MODE>(tag, X, W, b, Y, S, CO, K);
-    F("fwd6 cur", 13, 192, 2, 192, 1728, 2, 6, 4, 2)
-    F("fwd6 256x192 4x6 4x2", 13, 192, 2, 192, 1728, 4, 6, 4, 2)
-    FM_("fwd6 256x192 fixedload", 13, 192, 2, 192, 1728, 4, 6, 4, 2, 3)
-    FM_("fwd6 256x192 noload", 13, 192, 2, 192, 1728, 4, 6, 4, 2, 1)
-    F("fwd6 256x192 8x3 2x4", 13, 192, 2, 192, 1728, 8, 3, 2, 4)
-    F("fwd6 256x96 4x3 4x2", 13, 192, 2, 192, 1728, 4, 3, 4, 2)
-    F("fwd6 128x192 4x6 2x2", 13, 192, 2, 192, 1728, 4, 6, 2, 2)
-    F("fwd6 256x192 8x6 2x2", 13, 192, 2, 192, 1728, 8, 6, 2, 2)
-    F("fwd4 cur", 20, 96, 2, 96, 864, 4, 3, 4, 2)
-    F("fwd4 256x96 8x3 2x2", 20, 96, 2, 96, 864, 8, 3, 2, 2)
-    F("fwd4 512x96 8x3 4x2", 20, 96, 2, 96, 864, 8, 3, 4, 2)
+#define FG(tag, IH, CI, PAD, CO, K, FM, FN, WM, WN) \
+    if (want(tag)) { conv_fwd_glds<IH, CI, PAD, FM, FN, WM, WN>(tag, X, W, b, Y2, S, CO, K, zp); \
+                     conv_fwd<IH, CI, PAD, FM, FN, WM, WN>(tag, X, W, b, Y, S, CO, K); \
+                     check_same(Y2, Y, (size_t)S * (IH + 2 * PAD - 2) * (IH + 2 * PAD - 2) * CO, tag); }
+    FG("fwd6 128x192", 13, 192, 2, 192, 1728, 2, 6, 4, 2)
+    FG("fwd6 128x96", 13, 192, 2, 192, 1728, 4, 3, 2, 2)
+    FG("fwd6 256x96", 13, 192, 2, 192, 1728, 4, 3, 4, 2)
+    FG("fwd4 256x96", 20, 96, 2, 96, 864, 4, 3, 4, 2)
+    FG("fwd4 128x96", 20, 96, 2, 96, 864, 4, 3, 2, 2)
+    FG("dg6 128x192", 15, 192, 0, 192, 1728, 2, 6, 4, 2)
+    FG("dg4 256x96", 22, 96, 0, 96, 864, 4, 3, 4, 2)
+    FG("fwd2 256x48", 34, 48, 2, 48, 432, 2, 3, 8, 1)
+    FG("dg2 256x48", 36, 48, 0, 48, 432, 2, 3, 8, 1)
     return 0;
 }
