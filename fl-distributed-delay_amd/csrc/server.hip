@@ -417,3 +417,220 @@ int flsim_aggregate_adam(const float* S, int c, const float* const* stale, int n
 }
 
 }  // extern "C"
+
+// =============================================================================================
+// General entry order (heterogeneous-delay extension): weight_ups appended in
+// worker-index order, so stale entries can sit anywhere among the c_t aliased S_t entries, and
+// a step may pop many FIFOs.  The sequence is given as events (position, array) sorted by
+// position; every other position is S_t.  Same cascade, memoised per pure block / level-1 group
+// / level-2 group wherever no event falls inside; one element per thread; the event list is
+// read with uniform (scalar) loads, so all control flow stays scalar.
+// =============================================================================================
+namespace flsim {
+
+constexpr int SEQ_MAX_TAILS = 64;
+
+struct SeqArgs {
+    const float* S;
+    const int32_t* ev;              // [n_events][2] = (entry position, array index), sorted
+    const float* const* arrays;     // device table of stale arrays (nullptr = zeros)
+    float* p;
+    float* m;
+    float* v;
+    long P;
+    int k, n_events, lp, nb;
+    int ntail;
+    int tail_lo[SEQ_MAX_TAILS], tail_hi[SEQ_MAX_TAILS];
+    float w1, b2, w2, bc2s, rbc2s, eps, neg_ss, fk, rk;
+};
+
+__device__ __forceinline__ float seq_y(const SeqArgs& A, int j, long e) {
+    const float* a = A.arrays[A.ev[2 * j + 1]];
+    return a ? a[e] : 0.f;
+}
+
+// multi_row_sum over the entries of stream `q` of stride `str` (the whole sequence: q = 0,
+// str = 1; row_sum stream q: positions 4r + q, r < kk) -- kk rows in the stream
+__device__ float seq_cascade(const SeqArgs& A, float x, long e, int q, int str, int kk) {
+    int lp = 0;
+    while ((1 << lp) < kk) ++lp;
+    lp /= 4;
+    if (lp < 4) lp = 4;
+    const int L = 1 << lp;
+    const int nb = kk >> lp;
+    const float bx = seq_sum(x, L);
+    const float g1 = seq_sum(bx, L);
+    const float g2 = seq_sum(g1, L);
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int i = 0;                       // stream row
+    int j = 0;                       // next event of the whole sequence
+    auto next_row = [&]() -> int {   // stream row of the next event in this stream, or kk
+        while (j < A.n_events) {
+            const int pos = A.ev[2 * j];
+            if (pos % str == q && pos / str < kk) return pos / str;
+            if (pos / str >= kk && pos % str == q) return kk;
+            ++j;
+        }
+        return kk;
+    };
+    auto close = [&]() {             // i just became a multiple of L
+        const int b = i >> lp;
+        a1 += a0;
+        a0 = 0.f;
+        if ((b & (L - 1)) == 0) {
+            a2 += a1;
+            a1 = 0.f;
+            if (((b >> lp) & (L - 1)) == 0) {
+                a3 += a2;
+                a2 = 0.f;
+            }
+        }
+    };
+    const int full = nb << lp;       // rows inside full blocks
+    while (i < kk) {
+        const int nr = next_row();
+        const int lim = nr < full ? nr : full;
+        const int L2 = L * L, L3 = L * L * L;
+        if ((i & (L3 - 1)) == 0 && i + L3 <= lim) {          // pure level-2 group
+            a3 += g2;
+            i += L3;
+            continue;
+        }
+        if ((i & (L2 - 1)) == 0 && i + L2 <= lim) {          // pure level-1 group
+            a2 += g1;
+            i += L2;
+            if ((((i >> lp) >> lp) & (L - 1)) == 0) {
+                a3 += a2;
+                a2 = 0.f;
+            }
+            continue;
+        }
+        if ((i & (L - 1)) == 0 && i + L <= lim) {            // pure block
+            a1 += bx;
+            i += L;
+            const int b = i >> lp;
+            if ((b & (L - 1)) == 0) {
+                a2 += a1;
+                a1 = 0.f;
+                if (((b >> lp) & (L - 1)) == 0) {
+                    a3 += a2;
+                    a2 = 0.f;
+                }
+            }
+            continue;
+        }
+        if (i == nr) {                                       // a stale entry
+            a0 += seq_y(A, j, e);
+            ++j;
+        } else {
+            a0 += x;
+        }
+        ++i;
+        if ((i & (L - 1)) == 0 && i <= full) close();
+    }
+    a0 += a1;
+    a0 += a2;
+    a0 += a3;
+    return a0;
+}
+
+__global__ void __launch_bounds__(256) k_aggregate_adam_seq(SeqArgs A) {
+    const long e = (long)blockIdx.x * 256 + threadIdx.x;
+    if (e >= A.P) return;
+    bool tail = false;
+#pragma unroll 1
+    for (int t = 0; t < A.ntail; ++t) tail |= e >= A.tail_lo[t] && e < A.tail_hi[t];
+    const float x = A.S[e];
+    float s;
+    if (!tail) {
+        s = seq_cascade(A, x, e, 0, 1, A.k);
+    } else {                         // row_sum: 4 streams of k/4 rows, leftovers into stream 0
+        const int sz = A.k / 4;
+        float ps[4];
+        for (int q = 0; q < 4; ++q) ps[q] = seq_cascade(A, x, e, q, 4, sz);
+        for (int i = sz * 4; i < A.k; ++i) {
+            float val = x;
+            for (int j = 0; j < A.n_events; ++j)
+                if (A.ev[2 * j] == i) val = seq_y(A, j, e);
+            ps[0] += val;
+        }
+        ps[0] += ps[1];
+        ps[0] += ps[2];
+        ps[0] += ps[3];
+        s = ps[0];
+    }
+    const float g = div_const(s, A.fk, A.rk);
+    float p = A.p[e], m = A.m[e], v = A.v[e];
+    const float mi = __fmaf_rn(A.w1, g - m, m);
+    float vi = v * A.b2;
+    vi = __fmaf_rn(A.w2 * g, g, vi);
+    const float den = div_const(sqrt_rn(vi), A.bc2s, A.rbc2s) + A.eps;
+    A.p[e] = p + __fdiv_rn(A.neg_ss * mi, den);
+    A.m[e] = mi;
+    A.v[e] = vi;
+}
+
+}  // namespace flsim
+
+extern "C" {
+
+// weight_ups in general order: k entries, events[j] = (position, array index) of the non-S_t
+// entries (sorted by position); arrays = device table of stale arrays (nullptr = zeros)
+int flsim_aggregate_adam_seq(const float* S, int k, const int32_t* events, int n_events,
+                             const float* const* arrays, float* p, float* m, float* v, long P,
+                             const long* tensor_sizes, int n_tensors, long step, double lr,
+                             double beta1, double beta2, double eps, hipStream_t stream) {
+    FLSIM_REQUIRE(S && p && m && v && tensor_sizes, "null pointer");
+    FLSIM_REQUIRE(k > 0, "empty weight_ups (reference: IndexError in rule, main.py:25)");
+    FLSIM_REQUIRE(k < (1 << 24) && n_events >= 0 && n_events <= k, "bad entry counts k=%d n=%d",
+                  k, n_events);
+    FLSIM_REQUIRE(n_events == 0 || (events && arrays), "null event table");
+    FLSIM_REQUIRE(step >= 1 && P > 0 && P < (1L << 31), "bad step / P");
+    SeqArgs A{};
+    A.S = S;
+    A.ev = events;
+    A.arrays = arrays;
+    A.p = p;
+    A.m = m;
+    A.v = v;
+    A.P = P;
+    A.k = k;
+    A.n_events = n_events;
+    long off = 0;
+    for (int t = 0; t < n_tensors; ++t) {
+        const long n = tensor_sizes[t];
+        FLSIM_REQUIRE(n > 0, "tensor %d has size %ld", t, n);
+        if (n % 32) {
+            FLSIM_REQUIRE(A.ntail < SEQ_MAX_TAILS, "more than %d tensors with a row_sum tail",
+                          SEQ_MAX_TAILS);
+            A.tail_lo[A.ntail] = (int)(off + (n / 32) * 32);
+            A.tail_hi[A.ntail] = (int)(off + n);
+            A.ntail++;
+        }
+        off += n;
+    }
+    FLSIM_REQUIRE(off == P, "tensor sizes sum to %ld, P = %ld", off, P);
+    A.fk = (float)k;
+    {
+        volatile float one = 1.f, fk = (float)k;
+        A.rk = one / fk;
+    }
+    const double bc1 = 1.0 - pow(beta1, (double)step);
+    const double bc2 = 1.0 - pow(beta2, (double)step);
+    A.w1 = (float)(1.0 - beta1);
+    A.b2 = (float)beta2;
+    A.w2 = (float)(1.0 - beta2);
+    A.bc2s = (float)sqrt(bc2);
+    {
+        volatile float one = 1.f, b = A.bc2s;
+        A.rbc2s = one / b;
+    }
+    A.eps = (float)eps;
+    A.neg_ss = (float)(-(lr / bc1));
+    hipLaunchKernelGGL(k_aggregate_adam_seq, dim3((unsigned)((P + 255) / 256)), dim3(256), 0,
+                       stream, A);
+    FLSIM_LAUNCH_CHECK();
+    return 0;
+}
+
+}  // extern "C"

@@ -19,7 +19,7 @@ EXPORTS = [
     "flsim_pn1_workspace_bytes", "flsim_pn1_workspace_offset", "flsim_pn1_begin_epoch",
     "flsim_pn1_fwd_bwd_chunk", "flsim_pn1_fwd_bwd_input", "flsim_pn1_end_epoch",
     "flsim_pn1_eval_pool",
-    "flsim_aggregate_adam", "flsim_probe_enable", "flsim_probe_read", "flsim_probe_disable",
+    "flsim_aggregate_adam", "flsim_aggregate_adam_seq", "flsim_probe_enable", "flsim_probe_read", "flsim_probe_disable",
     "flsim_probe_kernel_count", "flsim_probe_kernel_name",
 ]
 
@@ -68,6 +68,9 @@ def lib():
                                       vp, vp, vp]
     L.flsim_aggregate_adam.argtypes = [
         vp, ctypes.c_int, vp, ctypes.c_int, vp, vp, vp, ctypes.c_long, vp, ctypes.c_int,
+        ctypes.c_long, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp]
+    L.flsim_aggregate_adam_seq.argtypes = [
+        vp, ctypes.c_int, vp, ctypes.c_int, vp, vp, vp, vp, ctypes.c_long, vp, ctypes.c_int,
         ctypes.c_long, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp]
     L.flsim_probe_enable.argtypes = [ctypes.c_int]
     L.flsim_probe_read.argtypes = [vp, vp, vp]

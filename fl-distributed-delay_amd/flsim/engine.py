@@ -104,6 +104,10 @@ class PN1Engine:
         """stale: list of device tensors (or None = zero entry)."""
         aggregate_adam(S, c, stale, theta, m, v, step, PN1_SIZES, lr, betas, eps)
 
+    def aggregate_adam_seq(self, S, k, events, arrays, theta, m, v, step, lr=1e-3,
+                           betas=(0.9, 0.999), eps=1e-8):
+        aggregate_adam_seq(S, k, events, arrays, theta, m, v, step, PN1_SIZES, lr, betas, eps)
+
 
 def aggregate_adam(S, c, stale, theta, m, v, step, sizes, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
     """Fused rule() + Adam (main.py:23-25 + agents.py:9-21) over a flat parameter vector whose
@@ -115,6 +119,22 @@ def aggregate_adam(S, c, stale, theta, m, v, step, sizes, lr=1e-3, betas=(0.9, 0
     check(lib().flsim_aggregate_adam(
         ptr(S), int(c), arr, ns, ptr(theta), ptr(m), ptr(v), sum(int(n) for n in sizes), csz, len(sizes),
         int(step), float(lr), float(betas[0]), float(betas[1]), float(eps), stream_ptr()))
+
+
+def aggregate_adam_seq(S, k, events, arrays, theta, m, v, step, sizes, lr=1e-3,
+                       betas=(0.9, 0.999), eps=1e-8):
+    """rule() + Adam for weight_ups in general order (heterogeneous-delay extension): k entries,
+    events = [(position, array index)] of the non-S_t entries sorted by position, arrays = device
+    tensors (None = zeros).  The small event / pointer tables are copied to the device here."""
+    dev = S.device
+    ev = torch.tensor(np.asarray(events, np.int32).reshape(-1, 2), device=dev)
+    tab = torch.tensor([(a.data_ptr() if a is not None else 0) for a in arrays] or [0],
+                       dtype=torch.int64, device=dev)
+    csz = (ctypes.c_long * len(sizes))(*[int(n) for n in sizes])
+    check(lib().flsim_aggregate_adam_seq(
+        ptr(S), int(k), ptr(ev), len(events), ptr(tab), ptr(theta), ptr(m), ptr(v),
+        sum(int(n) for n in sizes), csz, len(sizes), int(step), float(lr), float(betas[0]),
+        float(betas[1]), float(eps), stream_ptr()))
 
 
 def worker_table(recs, device):

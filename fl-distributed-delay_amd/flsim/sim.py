@@ -121,6 +121,20 @@ class FLSimulation:
             self._wt_ev[j] = ev
         return dev
 
+    @staticmethod
+    def _entry_order(plan):
+        """None when weight_ups is [S_t] * c_t followed by <= 8 stale entries (the reference:
+        one slow worker, index n-1); else (positions of the stale entries in weight_ups, None):
+        entries are appended in worker-index order (main.py:136-178)."""
+        if not plan.stale:
+            return None
+        fast = np.nonzero(plan.fast)[0]
+        sw = np.asarray([w for (w, _) in plan.stale], np.int64)
+        if len(sw) <= 8 and (len(fast) == 0 or fast.max() < sw.min()):
+            return None
+        pos = np.searchsorted(fast, sw) + np.arange(len(sw))
+        return [int(x) for x in pos], None
+
     def shard(self, active):
         lo = (len(active) * self.rank) // self.world
         hi = (len(active) * (self.rank + 1)) // self.world
@@ -162,8 +176,21 @@ class FLSimulation:
             else:
                 stale.append(None)
         self.step += 1
-        eng.aggregate_adam(S, plan.c_t, stale, self.theta, self.m, self.v, self.step, self.lr,
-                           self.betas, self.eps)
+        order = self._entry_order(plan)
+        if order is None:       # reference order: c_t copies of S_t, then the stale entries
+            eng.aggregate_adam(S, plan.c_t, stale, self.theta, self.m, self.v, self.step,
+                               self.lr, self.betas, self.eps)
+        else:                   # stale entries interleaved in worker order (extension)
+            events, arrays = order
+            uniq, ev = [], []
+            for pos, a in zip(events, stale):
+                j = next((q for q, u in enumerate(uniq) if u is a), None)
+                if j is None:
+                    uniq.append(a)
+                    j = len(uniq) - 1
+                ev.append((pos, j))
+            eng.aggregate_adam_seq(S, plan.c_t + plan.s_t, ev, uniq, self.theta, self.m, self.v,
+                                   self.step, self.lr, self.betas, self.eps)
         for (_, src) in plan.stale:
             if self.semantics == "reference":
                 entry = self.stale_store[src]

@@ -97,6 +97,16 @@ int flsim_aggregate_adam(const float* S, int c, const float* const* stale, int n
                          int n_tensors, long step, double lr, double beta1, double beta2,
                          double eps, flsim_stream_t stream);
 
+/* General entry order (the heterogeneous-delay extension of main.py:150-166, SURVEY 8 a1: every
+ * worker with a delay is a slow worker with its own FIFO; weight_ups is appended in worker-index
+ * order, so popped entries sit among the S_t copies).  k entries; events = device int32
+ * [n_events][2] (position in weight_ups, index into `arrays`), sorted by position; every other
+ * position is S.  arrays = device table of stale arrays (nullptr entry = zeros). */
+int flsim_aggregate_adam_seq(const float* S, int k, const int32_t* events, int n_events,
+                             const float* const* arrays, float* p, float* m, float* v, long P,
+                             const long* tensor_sizes, int n_tensors, long step, double lr,
+                             double beta1, double beta2, double eps, flsim_stream_t stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Measurement (no reference counterpart): HIP events around every worker-batched GEMM launch on
  * its stream, for bench.py's live roofline figure.  read() fills flsim_probe_kernel_count()

@@ -213,11 +213,13 @@ class OracleSim:
             if kind == "fast":
                 entries.append(S)
             else:
-                entries.append(self.ring.pop(src) if self.semantics == "reference"
+                entries.append(self.ring[src] if self.semantics == "reference"
                                else np.zeros_like(S))
         if any(self.delays[i] != 0 and (t == 0 or t % abs(int(self.delays[i])) == 0)
                for i in range(n)):
             self.ring[t] = S
+        live = {src for q in self.fifo.values() for src in q}     # entries a FIFO still holds
+        self.ring = {src: a for src, a in self.ring.items() if src in live}
         g = np.empty_like(S)
         off = 0
         for _, shp in _shapes():                          # rule() is per parameter tensor

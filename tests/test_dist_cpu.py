@@ -46,8 +46,16 @@ class StandInEngine:
                 tot = tot + s[:P]
         theta -= lr * tot / (c + len(stale))
 
+    def aggregate_adam_seq(self, S, k, events, arrays, theta, m, v, step, lr=1e-3,
+                           betas=(0.9, 0.999), eps=1e-8):
+        tot = S * (k - len(events))
+        for (_, j) in events:
+            if arrays[j] is not None:
+                tot = tot + arrays[j][:P]
+        theta -= lr * tot / k
 
-def _run(rank, world, n, d, thr, epochs, out, port):
+
+def _run(rank, world, n, d, thr, epochs, out, port, delays=None):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, os.path.dirname(here))
@@ -57,8 +65,8 @@ def _run(rank, world, n, d, thr, epochs, out, port):
         os.environ["MASTER_PORT"] = str(port)
         dist.init_process_group("gloo", rank=rank, world_size=world)
     from flsim.sim import FLSimulation
-    sim = FLSimulation(n, delay=d, throttle=thr, device="cpu", engine=StandInEngine(),
-                       device_pool=object(), theta0=torch.zeros(P))
+    sim = FLSimulation(n, delay=d, delays=delays, throttle=thr, device="cpu",
+                       engine=StandInEngine(), device_pool=object(), theta0=torch.zeros(P))
     losses = [sim.epoch() for _ in range(epochs)]
     res = dict(theta=sim.theta.numpy().copy(), losses=losses,
                trace=[(p.t, p.computes.tobytes(), p.stale) for p in sim.trace])
@@ -67,16 +75,20 @@ def _run(rank, world, n, d, thr, epochs, out, port):
     out[rank] = res
 
 
-@pytest.mark.parametrize("thr", [False, True])
-def test_two_rank_sharding_matches_single(thr):
+@pytest.mark.parametrize("thr,delays", [
+    (False, None), (True, None),
+    (True, [0, 2, 0, 0, 3, 0, 0, 2, 0, 0, 0]),     # heterogeneous delays: interleaved stale entries
+])
+def test_two_rank_sharding_matches_single(thr, delays):
     n, d, epochs = 11, 3, 7
     ctx = mp.get_context("spawn")
     mgr = ctx.Manager()
     single = mgr.dict()
-    _run(0, 1, n, d, thr, epochs, single, 0)
+    _run(0, 1, n, d, thr, epochs, single, 0, delays)
     out = mgr.dict()
-    port = 29500 + (os.getpid() % 1000)
-    procs = [ctx.Process(target=_run, args=(r, 2, n, d, thr, epochs, out, port)) for r in range(2)]
+    port = 29500 + (os.getpid() % 1000) + (7 if delays else 0) + (3 if thr else 0)
+    procs = [ctx.Process(target=_run, args=(r, 2, n, d, thr, epochs, out, port, delays))
+             for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
