@@ -59,6 +59,9 @@ def parse():
     ap.add_argument("--n_workers", type=int, default=1024)
     ap.add_argument("--delay", type=int, default=50)
     ap.add_argument("--no-throttle", action="store_true")
+    ap.add_argument("--delays", choices=["reference", "heterogeneous"], default="reference",
+                    help="reference: one slow worker (n-1) with --delay; heterogeneous: configs[3] "
+                         "spec (10%% slow workers, geometric delays up to 1000)")
     ap.add_argument("--chunk", type=int, default=32, help="workers per worker-batched launch")
     ap.add_argument("--cpu-sample", type=int, default=160,
                     help="worker-steps in the CPU sample (~10-30 s of host work)")
@@ -114,8 +117,12 @@ def main():
     from flsim.sim import FLSimulation
 
     throttle = not args.no_throttle
-    sim = FLSimulation(args.n_workers, delay=args.delay, throttle=throttle, chunk_workers=args.chunk,
-                       device=dev)
+    delays = None
+    if args.delays == "heterogeneous":
+        from flsim.schedule import heterogeneous_delays
+        delays = heterogeneous_delays(args.n_workers)
+    sim = FLSimulation(args.n_workers, delay=args.delay, delays=delays, throttle=throttle,
+                       chunk_workers=args.chunk, device=dev)
     for _ in range(args.warmup):
         sim.epoch(sync_loss=False)
     torch.cuda.synchronize()
@@ -187,7 +194,9 @@ def main():
             "data": "synthetic: seeded CIFAR-shaped u8 pool in HBM, torch-default-init "
                     "PerformantNet1 (no network for CIFAR10)",
             "config": {"workload": f"FL server epochs, n_workers={args.n_workers}, "
-                                   f"delay={args.delay}, throttle={throttle}, PerformantNet1, "
+                                   + (f"delay={args.delay}" if delays is None else
+                                      "heterogeneous delays (configs[3] spec)")
+                                   + f", throttle={throttle}, PerformantNet1, "
                                    f"128 samples/worker-step, Adam lr 1e-3",
                        "executed_worker_steps": ws, "chunk_workers": args.chunk,
                        "parallelism": f"workers sharded over {world} GPU(s), "

@@ -577,7 +577,7 @@ extern "C" {
 // weight_ups in general order: k entries, events[j] = (position, array index) of the non-S_t
 // entries (sorted by position); arrays = device table of stale arrays (nullptr = zeros)
 int flsim_aggregate_adam_seq(const float* S, int k, const int32_t* events, int n_events,
-                             const float* const* arrays, float* p, float* m, float* v, long P,
+                             const float* const* arrays, int n_arrays, float* p, float* m, float* v, long P,
                              const long* tensor_sizes, int n_tensors, long step, double lr,
                              double beta1, double beta2, double eps, hipStream_t stream) {
     FLSIM_REQUIRE(S && p && m && v && tensor_sizes, "null pointer");
@@ -627,10 +627,13 @@ int flsim_aggregate_adam_seq(const float* S, int k, const int32_t* events, int n
     }
     A.eps = (float)eps;
     A.neg_ss = (float)(-(lr / bc1));
-    hipLaunchKernelGGL(k_aggregate_adam_seq, dim3((unsigned)((P + 255) / 256)), dim3(256), 0,
-                       stream, A);
+    // algorithmic HBM bytes: S_t + each distinct stale array once + p, m, v read and written
+    const double bytes = 4.0 * (double)P * (7 + n_arrays);
+    const ProbeSlot ps = probe_begin();
+    hipExtLaunchKernelGGL(k_aggregate_adam_seq, dim3((unsigned)((P + 255) / 256)), dim3(256), 0,
+                          stream, ps.start, ps.stop, 0, A);
     FLSIM_LAUNCH_CHECK();
-    return 0;
+    return probe_end(ps, K_AGG, bytes);
 }
 
 }  // extern "C"

@@ -70,7 +70,8 @@ def lib():
         vp, ctypes.c_int, vp, ctypes.c_int, vp, vp, vp, ctypes.c_long, vp, ctypes.c_int,
         ctypes.c_long, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp]
     L.flsim_aggregate_adam_seq.argtypes = [
-        vp, ctypes.c_int, vp, ctypes.c_int, vp, vp, vp, vp, ctypes.c_long, vp, ctypes.c_int,
+        vp, ctypes.c_int, vp, ctypes.c_int, vp, ctypes.c_int, vp, vp, vp, ctypes.c_long, vp,
+        ctypes.c_int,
         ctypes.c_long, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp]
     L.flsim_probe_enable.argtypes = [ctypes.c_int]
     L.flsim_probe_read.argtypes = [vp, vp, vp]

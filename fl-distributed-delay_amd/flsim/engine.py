@@ -132,7 +132,7 @@ def aggregate_adam_seq(S, k, events, arrays, theta, m, v, step, sizes, lr=1e-3,
                        dtype=torch.int64, device=dev)
     csz = (ctypes.c_long * len(sizes))(*[int(n) for n in sizes])
     check(lib().flsim_aggregate_adam_seq(
-        ptr(S), int(k), ptr(ev), len(events), ptr(tab), ptr(theta), ptr(m), ptr(v),
+        ptr(S), int(k), ptr(ev), len(events), ptr(tab), len(arrays), ptr(theta), ptr(m), ptr(v),
         sum(int(n) for n in sizes), csz, len(sizes), int(step), float(lr), float(betas[0]),
         float(betas[1]), float(eps), stream_ptr()))
 

@@ -27,6 +27,18 @@ def reference_delays(n, delay):
     return d
 
 
+def heterogeneous_delays(n, seed=0, slow_fraction=0.1, mean_delay=100, dmax=1000):
+    """configs[3] / SURVEY 8d C4 spec (the build's): each worker is slow with probability
+    slow_fraction; a slow worker's delay is 1 + Geometric(1 / mean_delay) truncated to dmax
+    (RandomState(seed + 7)); 0 = fast.  The last worker is always slow, as in main.py."""
+    rs = np.random.RandomState(seed + 7)
+    slow = rs.rand(n) < slow_fraction
+    d = np.minimum(rs.geometric(1.0 / mean_delay, size=n), dmax).astype(np.int32)
+    out = np.where(slow, d, 0).astype(np.int32)
+    out[n - 1] = max(int(out[n - 1]), int(d[n - 1]))
+    return out
+
+
 class Schedule:
     def __init__(self, n, delays, throttle=False, max_throttle=32):
         self.n = int(n)

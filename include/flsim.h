@@ -101,9 +101,10 @@ int flsim_aggregate_adam(const float* S, int c, const float* const* stale, int n
  * worker with a delay is a slow worker with its own FIFO; weight_ups is appended in worker-index
  * order, so popped entries sit among the S_t copies).  k entries; events = device int32
  * [n_events][2] (position in weight_ups, index into `arrays`), sorted by position; every other
- * position is S.  arrays = device table of stale arrays (nullptr entry = zeros). */
+ * position is S.  arrays = device table of n_arrays stale arrays (nullptr entry = zeros). */
 int flsim_aggregate_adam_seq(const float* S, int k, const int32_t* events, int n_events,
-                             const float* const* arrays, float* p, float* m, float* v, long P,
+                             const float* const* arrays, int n_arrays, float* p, float* m,
+                             float* v, long P,
                              const long* tensor_sizes, int n_tensors, long step, double lr,
                              double beta1, double beta2, double eps, flsim_stream_t stream);
 
