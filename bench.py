@@ -33,7 +33,6 @@ import torch  # noqa: E402
 METRIC = "simulated worker-steps/sec (node) @1024 workers, delay 50; aggregation HBM GB/s"
 MFMA_F32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: fp32 matrix (v_mfma_f32_16x16x4_f32)
 HBM_PEAK_GBPS = 8000.0           # MI355X_MICROARCH.md: HBM3E spec
-FLOP_PER_WORKER_STEP = 147_641_499_648   # SURVEY 8d (fwd + dgrad + wgrad, B = 128)
 
 
 def _load_traffic():
@@ -63,6 +62,9 @@ def parse():
                     help="reference: one slow worker (n-1) with --delay; heterogeneous: configs[3] "
                          "spec (10%% slow workers, geometric delays up to 1000)")
     ap.add_argument("--chunk", type=int, default=32, help="workers per worker-batched launch")
+    ap.add_argument("--model", choices=["PerformantNet1", "vgg11"], default="PerformantNet1",
+                    help="PerformantNet1 (main.py:97, the metric's model) or vgg11 (configs[4]: "
+                         "--model vgg11 --n_workers 4096 --delay 1000)")
     ap.add_argument("--cpu-sample", type=int, default=160,
                     help="worker-steps in the CPU sample (~10-30 s of host work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -70,7 +72,7 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(n, delay, throttle, n_ws):
+def cpu_baseline(n, delay, throttle, n_ws, model="PerformantNet1"):
     """The oracle's CPU port of the reference loop (torch CPU, all host cores of this job): the
     first n_ws fwd_bkwd of epoch 0 (agents.py:32-40, sequential, accumulating), then rule()
     (torch.stack(...).mean(0) per tensor, main.py:23-25) over those entries and one Adam step
@@ -80,24 +82,24 @@ def cpu_baseline(n, delay, throttle, n_ws):
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
     pool = O.make_pool(0)
-    sim = MR.OracleSim(n, delay=delay, throttle=throttle, pool=pool)
+    sim = MR.OracleSim(n, delay=delay, throttle=throttle, pool=pool, model=model)
     sched = O.schedule(n, O.reference_delays(n, delay), throttle, 1)
     ks = O.worker_k_sequence(0, n, 1)[0]
     active = np.nonzero(sched.computes[0])[0][:n_ws]
     items = [(0, int(i), int(ks[i])) for i in active]
-    params = [torch.tensor(a, requires_grad=True) for a in MR.split_flat(sim.theta)]
+    params = [torch.tensor(a, requires_grad=True) for a in MR.split_flat(sim.theta, model)]
     opt = torch.optim.Adam(params, lr=1e-3)
     sim.grad_of(sim.theta, items[:1])          # warm the CPU kernels
     t0 = time.perf_counter()
     g, _ = sim.grad_of(sim.theta, items)
-    gl = [torch.from_numpy(a) for a in MR.split_flat(g)]
+    gl = [torch.from_numpy(a) for a in MR.split_flat(g, model)]
     fin = [torch.stack([x] * len(items)).mean(0) for x in gl]
     for p, f in zip(params, fin):
         p.grad = f
     opt.step()
     dt = time.perf_counter() - t0
     return dict(value=len(items) / dt, unit="worker-steps/s", cores=threads, kind="port",
-                sample=f"{len(items)} fwd_bkwd of epoch 0 (n={n}, d={delay}, "
+                sample=f"{len(items)} {model} fwd_bkwd of epoch 0 (n={n}, d={delay}, "
                        f"{'throttle' if throttle else 'no throttle'}) + rule() over them + one "
                        f"Adam step; torch CPU, {threads} threads, {dt:.1f} s")
 
@@ -122,7 +124,8 @@ def main():
         from flsim.schedule import heterogeneous_delays
         delays = heterogeneous_delays(args.n_workers)
     sim = FLSimulation(args.n_workers, delay=args.delay, delays=delays, throttle=throttle,
-                       chunk_workers=args.chunk, device=dev)
+                       chunk_workers=args.chunk, device=dev, model=args.model)
+    flop_per_ws = sim.engine.FLOP_PER_WORKER_STEP
     for _ in range(args.warmup):
         sim.epoch(sync_loss=False)
     torch.cuda.synchronize()
@@ -156,7 +159,7 @@ def main():
         achieved = fl / cnt / avg_s / 1e12
         gemm_ms = sum(v[1] for v in kern.values())
         gemm_fl = sum(v[2] for v in kern.values())
-        traffic = TRAFFIC.get(name)
+        traffic = TRAFFIC.get(name) if args.model == "PerformantNet1" else None
         roofline = dict(bound="mfma", kernel=name, achieved=round(achieved, 2),
                         peak=MFMA_F32_PEAK_TFLOPS, unit="TFLOP/s",
                         frac=round(achieved / MFMA_F32_PEAK_TFLOPS, 4),
@@ -173,7 +176,8 @@ def main():
     if agg_rec:
         cnt, ms, byts = agg_rec
         gbps = byts / (ms / 1e3) / 1e9
-        traffic = TRAFFIC.get("aggregate_adam")
+        # profiles/traffic.json is measured on the default (PerformantNet1) workload
+        traffic = TRAFFIC.get("aggregate_adam") if args.model == "PerformantNet1" else None
         agg = dict(kernel="k_aggregate_adam", bound="hbm", achieved=round(gbps, 1),
                    peak=HBM_PEAK_GBPS, unit="GB/s", frac=round(gbps / HBM_PEAK_GBPS, 4),
                    launches=cnt, avg_launch_us=round(ms / cnt * 1e3, 2),
@@ -184,24 +188,24 @@ def main():
     value = ws / elapsed
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.n_workers, args.delay, throttle, args.cpu_sample)
+        cpu = cpu_baseline(args.n_workers, args.delay, throttle, args.cpu_sample, args.model)
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 3), "unit": "worker-steps/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic: seeded CIFAR-shaped u8 pool in HBM, torch-default-init "
-                    "PerformantNet1 (no network for CIFAR10)",
+            "data": f"synthetic: seeded CIFAR-shaped u8 pool in HBM, models.py-init "
+                    f"{args.model} (no network for CIFAR10)",
             "config": {"workload": f"FL server epochs, n_workers={args.n_workers}, "
                                    + (f"delay={args.delay}" if delays is None else
                                       "heterogeneous delays (configs[3] spec)")
-                                   + f", throttle={throttle}, PerformantNet1, "
+                                   + f", throttle={throttle}, {args.model}, "
                                    f"128 samples/worker-step, Adam lr 1e-3",
                        "executed_worker_steps": ws, "chunk_workers": args.chunk,
                        "parallelism": f"workers sharded over {world} GPU(s), "
                                       f"{'1 RCCL all-reduce/step' if world > 1 else 'no collective'}"},
-            "mfma_efficiency_whole_step": round(value * FLOP_PER_WORKER_STEP / 1e12 /
+            "mfma_efficiency_whole_step": round(value * flop_per_ws / 1e12 /
                                                 (MFMA_F32_PEAK_TFLOPS * world), 4),
             "roofline": roofline,
             "aggregation": agg,

@@ -2,8 +2,8 @@
 
 Same classes, signatures and aliasing semantics; the arithmetic runs in libflsim.so:
 
-  Worker.fwd_bkwd(inp, outp)   agents.py:32-40 -> flsim_pn1_fwd_bwd_input (HIP fwd/bwd of the
-                               central PerformantNet1); gradients accumulate over the workers of
+  Worker.fwd_bkwd(inp, outp)   agents.py:32-40 -> flsim_pn1_fwd_bwd_input / flsim_vgg11_*
+                               (HIP fwd/bwd of the central model); gradients accumulate over the workers of
                                an epoch exactly like .grad (agents.py:35) and the returned list
                                holds views of ONE flat buffer (every worker of the epoch gets the
                                same tensors, as in the reference)
@@ -13,9 +13,9 @@ Same classes, signatures and aliasing semantics; the arithmetic runs in libflsim
                                with the optimizer's lr/betas/eps); parameters live in one flat
                                device buffer, model.parameters() are views of it
 
-Requirements (raise otherwise): the model is FL.models.PerformantNet1 on a HIP device, the
-optimizer is torch.optim.Adam without weight decay / amsgrad / maximize, batches are multiples
-of 128 samples.  There is no CPU fallback.
+Requirements (raise otherwise): the model is FL.models.PerformantNet1 or FL.models.vgg11() on a
+HIP device, the optimizer is torch.optim.Adam without weight decay / amsgrad / maximize, batches
+are multiples of 128 samples.  There is no CPU fallback.
 """
 from __future__ import annotations
 
@@ -24,7 +24,7 @@ import itertools
 import numpy as np
 import torch
 
-from flsim.engine import PN1Engine, PN1_SHAPES, PN1_SIZES, split_views, worker_table, padded
+from flsim.engine import engine_for_parameters, padded, split_views, worker_table
 
 _CONTEXTS = {}
 _WORKER_IDS = itertools.count()
@@ -34,9 +34,8 @@ class _ModelContext:
     """Flat parameter / optimizer-state buffers and the engine of one central model."""
 
     def __init__(self, model, seed=0):
-        names = [n for n, _ in model.named_parameters()]
-        if names != [n for n, _ in PN1_SHAPES]:
-            raise NotImplementedError("the HIP engine implements FL.models.PerformantNet1 only")
+        self.engine_cls = engine_for_parameters(n for n, _ in model.named_parameters())
+        self.shapes = self.engine_cls.SHAPES
         dev = next(model.parameters()).device
         if dev.type != "cuda":
             raise RuntimeError("move the model to the GPU first (main.py:105 model.to(device))")
@@ -46,11 +45,11 @@ class _ModelContext:
         self.P = flat.numel()
         self.theta = torch.zeros(padded(self.P), device=dev)
         self.theta[:self.P].copy_(flat)
-        for p, view in zip(model.parameters(), split_views(self.theta[:self.P])):
+        for p, view in zip(model.parameters(), split_views(self.theta[:self.P], self.shapes)):
             p.data = view                       # parameters alias the flat buffer
         self.m = torch.zeros_like(self.theta)
         self.v = torch.zeros_like(self.theta)
-        self.engine = PN1Engine(dev, chunk_workers=1)
+        self.engine = self.engine_cls(dev, chunk_workers=1)
         self.seed = seed
         self.t = 0               # epoch counter (dropout RNG key)
         self.G = None            # flat gradient buffer of the current epoch (p.grad views)
@@ -61,7 +60,7 @@ class _ModelContext:
     def ensure_capacity(self, n_samples):
         cw = n_samples // 128
         if cw > self.engine.chunk_workers:
-            self.engine = PN1Engine(self.device, chunk_workers=cw)
+            self.engine = self.engine_cls(self.device, chunk_workers=cw)
             self.packed = False
         if cw > self.loss_buf.numel():
             self.loss_buf = torch.zeros(cw, device=self.device)
@@ -111,8 +110,8 @@ class Central:
 
     def _sync_optimizer_state(self):
         ctx = self.ctx
-        for p, mv, vv in zip(self.model.parameters(), split_views(ctx.m[:ctx.P]),
-                             split_views(ctx.v[:ctx.P])):
+        for p, mv, vv in zip(self.model.parameters(), split_views(ctx.m[:ctx.P], ctx.shapes),
+                             split_views(ctx.v[:ctx.P], ctx.shapes)):
             self.optim.state[p] = {"step": torch.tensor(float(ctx.step)), "exp_avg": mv,
                                    "exp_avg_sq": vv}
 
@@ -135,7 +134,7 @@ class Central:
                 stale.append(_flat_of(e, ctx))
             S = _flat_of(entries[0], ctx)
         else:
-            if len(ups) != len(PN1_SIZES):
+            if len(ups) != len(ctx.shapes):
                 raise IndexError("list index out of range")
             S = torch.cat([u.detach().reshape(-1).float() for u in ups])
             S = torch.nn.functional.pad(S, (0, padded(ctx.P) - ctx.P))
@@ -190,7 +189,7 @@ class Worker:
         eng.run_input(theta, inp.to(ctx.device, torch.float32), outp.to(ctx.device), wt,
                       ctx.seed, self.model.training, lb)
         eng.end_epoch(ctx.G)                     # running sum of the epoch's gradients
-        grads = split_views(ctx.G[:ctx.P])
+        grads = split_views(ctx.G[:ctx.P], ctx.shapes)
         for p, gv in zip(self.model.parameters(), grads):
             p.grad = gv                          # agents.py:35: accumulated in place
         lossval = lb.mean().detach().cpu().numpy()

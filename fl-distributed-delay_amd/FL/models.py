@@ -44,7 +44,7 @@ class PerformantNet1(nn.Module):
 
 
 class VGG(nn.Module):
-    """models.py:50-75 (config-5 model; the HIP engine for it is a SURVEY 8(f) 'next' row)."""
+    """models.py:50-75 (configs[4]'s larger CNN; vgg11() runs on the flsim_vgg11_* HIP engine)."""
 
     def __init__(self, features):
         super().__init__()

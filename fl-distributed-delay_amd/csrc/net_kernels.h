@@ -1,0 +1,569 @@
+// Kernels and launch helpers shared by the worker-batched networks (pn1_net.hip:
+// PerformantNet1, vgg_net.hip: VGG-11).  Non-template kernels are `static` (one copy per
+// translation unit); templates are instantiated per use.
+//
+// Layout conventions (both nets): activations NHWC fp32, one 128-sample block per simulated
+// worker (main.py:43-44 batch_size); conv weights re-packed once per epoch into
+// Wf[co][(kh*3+kw)*CIP + ci] (forward) and Wd[ci][(kh'*3+kw')*CO + co] = W[co][ci][2-kh'][2-kw']
+// (data gradient).
+#pragma once
+#include "loaders.h"
+#include "pn1.h"
+#include "probe.h"
+
+#define RC(x) do { int _r = (x); if (_r) return _r; } while (0)
+
+namespace flsim {
+
+// =============================================================================================
+// batch assembly: main.py:138-142 (k-th dataset, 128 samples with replacement, ToTensor +
+// Normalize) -> x0 NHWC [S][32][32][4] (4th channel zero), y [S]
+// =============================================================================================
+static __global__ void __launch_bounds__(256)
+k_fill_batch(const uint8_t* __restrict__ pool, const int32_t* __restrict__ labels,
+             const int32_t* __restrict__ list_a, int len_a, const int32_t* __restrict__ list_b,
+             int len_b, const WorkerRec* __restrict__ workers, int n_workers_total, uint64_t seed,
+             const float* __restrict__ lut, float* __restrict__ x0, int32_t* __restrict__ y) {
+    const int s = blockIdx.x;  // sample within chunk
+    const int w = s / SAMPLES_PER_WORKER;
+    const int j = s - w * SAMPLES_PER_WORKER;
+    const WorkerRec wr = workers[w];
+    const bool use_b = (int)wr.k == n_workers_total - 1;   // main.py:78-80: last dataset = {1,9}
+    const int len = use_b ? len_b : len_a;
+    const uint32_t u = philox_word(seed, wr.t, wr.i, SITE_DATA, (uint32_t)j);
+    const int idx = use_b ? list_b[u % (uint32_t)len] : list_a[u % (uint32_t)len];
+    if (threadIdx.x == 0) y[s] = labels[idx];
+    const uint8_t* img = pool + (long)idx * 3072;
+    float* out = x0 + (long)s * 4096;
+    for (int p = threadIdx.x; p < 1024; p += 256) {
+        f32x4 v;
+        v.x = lut[img[p]];
+        v.y = lut[img[1024 + p]];
+        v.z = lut[img[2048 + p]];
+        v.w = 0.f;
+        *reinterpret_cast<f32x4*>(out + 4 * p) = v;
+    }
+}
+
+// evaluation batches (util.py:31-45 testloader, shuffle=False): sample s of the chunk is pool
+// image first + s (samples past n_images repeat the last image; their predictions are dropped)
+static __global__ void __launch_bounds__(256)
+k_fill_seq(const uint8_t* __restrict__ pool, int first, int n_images, const float* __restrict__ lut,
+           float* __restrict__ x0, int32_t* __restrict__ y) {
+    const int s = blockIdx.x;
+    const int idx = first + (s < n_images ? s : n_images - 1);
+    if (threadIdx.x == 0) y[s] = 0;
+    const uint8_t* img = pool + (long)idx * 3072;
+    float* out = x0 + (long)s * 4096;
+    for (int p = threadIdx.x; p < 1024; p += 256) {
+        f32x4 v;
+        v.x = lut[img[p]];
+        v.y = lut[img[1024 + p]];
+        v.z = lut[img[2048 + p]];
+        v.w = 0.f;
+        *reinterpret_cast<f32x4*>(out + 4 * p) = v;
+    }
+}
+
+// explicit input (Worker.fwd_bkwd(inp, outp) facade): x NCHW fp32 [S][3][32][32], y int64
+static __global__ void __launch_bounds__(256)
+k_load_input(const float* __restrict__ x, const int64_t* __restrict__ yin, float* __restrict__ x0,
+             int32_t* __restrict__ y) {
+    const int s = blockIdx.x;
+    if (threadIdx.x == 0) y[s] = (int32_t)yin[s];
+    const float* img = x + (long)s * 3072;
+    float* out = x0 + (long)s * 4096;
+    for (int p = threadIdx.x; p < 1024; p += 256) {
+        f32x4 v;
+        v.x = img[p];
+        v.y = img[1024 + p];
+        v.z = img[2048 + p];
+        v.w = 0.f;
+        *reinterpret_cast<f32x4*>(out + 4 * p) = v;
+    }
+}
+
+// =============================================================================================
+// gradient through max_pool2d (+ dropout): dz[n][h][w][c] = gy[n][h/2][w/2][c] at the window's
+// argmax, 0 elsewhere and on the floor-mode border.  One thread per (window, 4 channels): one gy
+// float4 (or 4 NCHW scalars), one idx word, four float4 stores.  gy is already masked / scaled
+// by the consumer's epilogue.
+// =============================================================================================
+template <int H, int W, int C, bool NCHW_G>
+__global__ void __launch_bounds__(256)
+k_pool_scatter(const float* __restrict__ gy, const uint8_t* __restrict__ idx,
+               float* __restrict__ dz, long total) {
+    constexpr int PH = H / 2, PW = W / 2;
+    constexpr int CH = (H + 1) / 2, CW = (W + 1) / 2;   // cells incl. the border
+    constexpr int C4 = C / 4;
+    const long e = (long)blockIdx.x * 256 + threadIdx.x;
+    if (e >= total) return;
+    const int c = 4 * (int)(e % C4);
+    const long cell = e / C4;
+    const int cw = (int)(cell % CW);
+    const int ch = (int)((cell / CW) % CH);
+    const int n = (int)(cell / (CW * CH));
+    f32x4 g = f32x4{0.f, 0.f, 0.f, 0.f};
+    uint32_t id = 0xffffffffu;
+    if (ch < PH && cw < PW) {
+        const long pe = (((long)n * PH + ch) * PW + cw) * C + c;
+        id = *reinterpret_cast<const uint32_t*>(idx + pe);
+        if constexpr (NCHW_G) {
+            const float* b = gy + (long)n * (C * PH * PW) + (long)c * (PH * PW) + ch * PW + cw;
+            g.x = b[0];
+            g.y = b[PH * PW];
+            g.z = b[2 * PH * PW];
+            g.w = b[3 * PH * PW];
+        } else {
+            g = *reinterpret_cast<const f32x4*>(gy + pe);
+        }
+    }
+#pragma unroll
+    for (int pos = 0; pos < 4; ++pos) {
+        const int h = 2 * ch + (pos >> 1), w = 2 * cw + (pos & 1);
+        if (h >= H || w >= W) continue;
+        f32x4 v;
+        v.x = ((id & 0xff) == (uint32_t)pos) ? g.x : 0.f;
+        v.y = (((id >> 8) & 0xff) == (uint32_t)pos) ? g.y : 0.f;
+        v.z = (((id >> 16) & 0xff) == (uint32_t)pos) ? g.z : 0.f;
+        v.w = ((id >> 24) == (uint32_t)pos) ? g.w : 0.f;
+        *reinterpret_cast<f32x4*>(dz + (((long)n * H + h) * W + w) * C + c) = v;
+    }
+}
+
+template <int H, int W, int C, bool NCHW_G>
+static int pool_scatter(const float* gy, const uint8_t* idx, float* dz, int S, hipStream_t st) {
+    const long total = (long)S * ((H + 1) / 2) * ((W + 1) / 2) * (C / 4);
+    hipLaunchKernelGGL((k_pool_scatter<H, W, C, NCHW_G>), dim3(ceil_div(total, 256)), dim3(256), 0,
+                       st, gy, idx, dz, total);
+    FLSIM_LAUNCH_CHECK();
+    return 0;
+}
+
+// =============================================================================================
+// linear split-K finish: e[m][n] = dropout(relu(sum_z part[z][m][n] + b[n]))
+// (PerformantNet1 models.py:42-45; VGG classifier models.py:59-63)
+// =============================================================================================
+static __global__ void __launch_bounds__(256)
+k_linear_finish(const float* __restrict__ part, int Z, const float* __restrict__ bias,
+                float* __restrict__ out, int M, int N, const WorkerRec* __restrict__ workers,
+                uint64_t seed, uint32_t site, uint32_t thr, float scale, int dropout) {
+    const long e = (long)blockIdx.x * 256 + threadIdx.x;
+    if (e >= (long)M * N) return;
+    const int n = (int)(e % N);
+    const int m = (int)(e / N);
+    float acc = part[e];
+    for (int z = 1; z < Z; ++z) acc += part[(long)z * M * N + e];
+    float v = fmaxf(acc + bias[n], 0.f);
+    if (dropout) {
+        const int w = m / SAMPLES_PER_WORKER;
+        const int nl = m - w * SAMPLES_PER_WORKER;
+        const WorkerRec wr = workers[w];
+        v = philox_word(seed, wr.t, wr.i, site, (uint32_t)(nl * N + n)) >= thr ? v * scale : 0.f;
+    }
+    out[e] = v;
+}
+
+static int linear_finish(const float* part, int Z, const float* bias, float* out, int M, int N,
+                         const WorkerRec* workers, uint64_t seed, uint32_t site, uint32_t thr,
+                         float scale, int dropout, hipStream_t st) {
+    hipLaunchKernelGGL(k_linear_finish, dim3(ceil_div((long)M * N, 256)), dim3(256), 0, st, part, Z,
+                       bias, out, M, N, workers, seed, site, thr, scale, dropout);
+    FLSIM_LAUNCH_CHECK();
+    return 0;
+}
+
+// =============================================================================================
+// head: last linear (K -> 10) + CrossEntropyLoss(mean over the worker's 128) forward and
+// backward (PerformantNet1 models.py:46 / VGG models.py:64, main.py:107, agents.py:34-35).
+// One wave per sample; lane l holds features 4l + 256c (c < K/256).
+//   loss_s[s] = logsumexp(z) - z_y ; dlog[s][j] = (softmax - onehot) / 128
+//   dh[s][k] = (sum_j dlog[s][j] W[j][k]) * sdrop * (e[s][k] > 0)   (dropout / ReLU backward)
+// =============================================================================================
+template <int K>
+__global__ void __launch_bounds__(256)
+k_head(const float* __restrict__ e2, const float* __restrict__ W3, const float* __restrict__ b3,
+       const int32_t* __restrict__ y, float* __restrict__ loss_s, float* __restrict__ dlog,
+       float* __restrict__ dh2, int S, int backward, float sdrop,
+       int32_t* __restrict__ pred, int n_pred) {
+    constexpr int NC = K / 256;
+    static_assert(K % 256 == 0, "head width must be a multiple of 256");
+    const int s = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (s >= S) return;
+    f32x4 x[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+        x[c] = *reinterpret_cast<const f32x4*>(e2 + (long)s * K + 4 * lane + 256 * c);
+    float z[10];
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+        float p = 0.f;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const f32x4 wv = *reinterpret_cast<const f32x4*>(W3 + j * K + 4 * lane + 256 * c);
+            p += x[c].x * wv.x + x[c].y * wv.y + x[c].z * wv.z + x[c].w * wv.w;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) p += __shfl_xor(p, o, 64);
+        z[j] = p + b3[j];
+    }
+    float mx = z[0];
+#pragma unroll
+    for (int j = 1; j < 10; ++j) mx = fmaxf(mx, z[j]);
+    float se = 0.f;
+#pragma unroll
+    for (int j = 0; j < 10; ++j) se += expf(z[j] - mx);
+    const int lab = y[s];
+    float zy = 0.f;
+#pragma unroll
+    for (int j = 0; j < 10; ++j) zy = (j == lab) ? z[j] : zy;
+    if (lane == 0) loss_s[s] = (mx + logf(se)) - zy;
+    if (pred && lane == 0 && s < n_pred) {       // torch.max(outputs, 1): first max wins
+        int am = 0;
+#pragma unroll
+        for (int j = 1; j < 10; ++j) am = z[j] > z[am] ? j : am;
+        pred[s] = am;
+    }
+    if (!backward) return;
+    float g[10];
+    const float inv = 1.f / se;
+#pragma unroll
+    for (int j = 0; j < 10; ++j)
+        g[j] = (expf(z[j] - mx) * inv - (j == lab ? 1.f : 0.f)) * (1.f / SAMPLES_PER_WORKER);
+    if (lane < 10) {
+        float gv = 0.f;
+#pragma unroll
+        for (int j = 0; j < 10; ++j) gv = (j == lane) ? g[j] : gv;
+        dlog[(long)s * 16 + lane] = gv;
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        f32x4 d = zero4();
+#pragma unroll
+        for (int j = 0; j < 10; ++j) {
+            const f32x4 wv = *reinterpret_cast<const f32x4*>(W3 + j * K + 4 * lane + 256 * c);
+            d.x += g[j] * wv.x;
+            d.y += g[j] * wv.y;
+            d.z += g[j] * wv.z;
+            d.w += g[j] * wv.w;
+        }
+        d.x = x[c].x > 0.f ? d.x * sdrop : 0.f;
+        d.y = x[c].y > 0.f ? d.y * sdrop : 0.f;
+        d.z = x[c].z > 0.f ? d.z * sdrop : 0.f;
+        d.w = x[c].w > 0.f ? d.w * sdrop : 0.f;
+        *reinterpret_cast<f32x4*>(dh2 + (long)s * K + 4 * lane + 256 * c) = d;
+    }
+}
+
+// per-worker mean loss (fixed-order tree over the worker's 128 samples)
+static __global__ void __launch_bounds__(128)
+k_worker_loss(const float* __restrict__ loss_s, float* __restrict__ out) {
+    __shared__ float sh[128];
+    const int w = blockIdx.x;
+    sh[threadIdx.x] = loss_s[(long)w * 128 + threadIdx.x];
+    __syncthreads();
+    for (int o = 64; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[w] = sh[0] / 128.f;
+}
+
+// head forward (+ backward) and the per-worker losses of a chunk of S samples
+template <int K>
+static int head_and_loss(const float* e, const float* W, const float* b, const int32_t* y,
+                         float* loss_s, float* dlog, float* dh, int S, int backward, float sdrop,
+                         float* worker_loss, hipStream_t st) {
+    hipLaunchKernelGGL(k_head<K>, dim3(ceil_div(S, 4)), dim3(256), 0, st, e, W, b, y, loss_s, dlog,
+                       dh, S, backward, sdrop, (int32_t*)nullptr, 0);
+    FLSIM_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_worker_loss, dim3(S / SAMPLES_PER_WORKER), dim3(128), 0, st, loss_s,
+                       worker_loss);
+    FLSIM_LAUNCH_CHECK();
+    return 0;
+}
+
+// head forward only, argmax predictions for the first n_pred samples (evaluation)
+template <int K>
+static int head_predict(const float* e, const float* W, const float* b, const int32_t* y,
+                        float* loss_s, int S, int32_t* pred, int n_pred, hipStream_t st) {
+    hipLaunchKernelGGL(k_head<K>, dim3(ceil_div(S, 4)), dim3(256), 0, st, e, W, b, y, loss_s,
+                       (float*)nullptr, (float*)nullptr, S, 0, 1.f, pred, n_pred);
+    FLSIM_LAUNCH_CHECK();
+    return 0;
+}
+
+// last-linear weight/bias gradient, accumulated: slab[z][j][0..K) += sum_s dlog[s][j] e[s][k];
+// slab_b[z][j] += sum_s dlog[s][j].  Block (j, z) sums a row range of samples.
+template <int K>
+__global__ void __launch_bounds__(256)
+k_head_wgrad(const float* __restrict__ dlog, const float* __restrict__ e2, float* __restrict__ slab,
+             float* __restrict__ slab_b, int S, int Z) {
+    constexpr int NC = K / 256;
+    const int j = blockIdx.x;
+    const int z = blockIdx.y;
+    const int k = threadIdx.x;
+    const int per = (S + Z - 1) / Z;
+    const int s0 = z * per;
+    const int s1 = min(S, s0 + per);
+    float acc[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) acc[c] = 0.f;
+    float accb = 0.f;
+    for (int s = s0; s < s1; ++s) {
+        const float g = dlog[(long)s * 16 + j];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) acc[c] += g * e2[(long)s * K + k + 256 * c];
+        accb += g;
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) slab[((long)z * 10 + j) * K + k + 256 * c] += acc[c];
+    if (k == 0) slab_b[z * 10 + j] += accb;
+}
+
+template <int K>
+static int head_wgrad(const float* dlog, const float* e, float* slab, float* slab_b, int S, int Z,
+                      hipStream_t st) {
+    hipLaunchKernelGGL(k_head_wgrad<K>, dim3(10, Z), dim3(256), 0, st, dlog, e, slab, slab_b, S, Z);
+    FLSIM_LAUNCH_CHECK();
+    return 0;
+}
+
+// =============================================================================================
+// per-epoch weight packing (theta in torch layout -> kernel layouts)
+// =============================================================================================
+// forward: Wf[co][khkw*CIP + ci] = W[co][ci][kh][kw]   (ci < CI; zero padding ci in [CI, CIP)
+// and k >= 9*CIP up to KP)
+static __global__ void k_pack_fwd(const float* __restrict__ W, float* __restrict__ Wf, int CO,
+                                  int CI, int CIP, int KP) {
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= CO * KP) return;
+    const int co = e / KP;
+    const int k = e - co * KP;
+    const int khkw = k / CIP;
+    const int ci = k - khkw * CIP;
+    float v = 0.f;
+    if (khkw < 9 && ci < CI) v = W[(co * CI + ci) * 9 + khkw];
+    Wf[e] = v;
+}
+// data gradient: Wd[ci][khkw'*CO + co] = W[co][ci][8 - khkw']
+static __global__ void k_pack_dgrad(const float* __restrict__ W, float* __restrict__ Wd, int CO,
+                                    int CI) {
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    const int KD = 9 * CO;
+    if (e >= CI * KD) return;
+    const int ci = e / KD;
+    const int k = e - ci * KD;
+    const int khkw = k / CO;
+    const int co = k - khkw * CO;
+    Wd[e] = W[(co * CI + ci) * 9 + (8 - khkw)];
+}
+
+// both packings of one conv layer (wd == nullptr: no data gradient needed, first layer)
+static int pack_conv(const float* W, float* wf, float* wd, int CO, int CI, int CIP, int KP,
+                     hipStream_t st) {
+    hipLaunchKernelGGL(k_pack_fwd, dim3(ceil_div((long)CO * KP, 256)), dim3(256), 0, st, W, wf, CO,
+                       CI, CIP, KP);
+    FLSIM_LAUNCH_CHECK();
+    if (wd) {
+        hipLaunchKernelGGL(k_pack_dgrad, dim3(ceil_div((long)CI * 9 * CO, 256)), dim3(256), 0, st,
+                           W, wd, CO, CI);
+        FLSIM_LAUNCH_CHECK();
+    }
+    return 0;
+}
+
+// =============================================================================================
+// epoch-end finalize: S_t (torch layout) = sum_z slab[z]  (fixed z order: deterministic)
+// =============================================================================================
+// Block = `cols` element columns x `zl` z-lanes: lane tz sums slabs z = tz, tz + zl, ... (V
+// consecutive elements, one vector load per slab), then the zl partials are added in z-lane
+// order.  The order is fixed, so S_t is deterministic; every slab byte is read once, coalesced.
+// CO > 0 remaps the packed conv layout [co][khkw*CIP + ci] to torch's [co][ci][kh][kw].
+template <int V>
+__global__ void __launch_bounds__(256)
+k_fin_sum(const float* __restrict__ slab, int Z, long n, int zl, float* __restrict__ out, int CO,
+          int CI, int CIP, int KP) {
+    __shared__ float red[256 * V];
+    const int cols = 256 / zl;
+    const int tx = threadIdx.x % cols, tz = threadIdx.x / cols;
+    const long e0 = ((long)blockIdx.x * cols + tx) * V;
+    float acc[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) acc[v] = 0.f;
+    if (e0 < n) {
+        for (int z = tz; z < Z; z += zl) {
+            const float* p = slab + (long)z * n + e0;
+            if constexpr (V == 4) {
+                const f32x4 x = *reinterpret_cast<const f32x4*>(p);
+                acc[0] += x.x;
+                acc[1] += x.y;
+                acc[2] += x.z;
+                acc[3] += x.w;
+            } else {
+                acc[0] += p[0];
+            }
+        }
+    }
+#pragma unroll
+    for (int v = 0; v < V; ++v) red[threadIdx.x * V + v] = acc[v];
+    __syncthreads();
+    if (tz != 0 || e0 >= n) return;
+    for (int j = 1; j < zl; ++j)
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[v] += red[(j * cols + tx) * V + v];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        const long s = e0 + v;
+        if (CO > 0) {
+            const int co = (int)(s / KP);
+            const int k = (int)(s - (long)co * KP);
+            const int khkw = k / CIP, ci = k - (k / CIP) * CIP;
+            if (khkw < 9 && ci < CI) out[((long)co * CI + ci) * 9 + khkw] = acc[v];
+        } else {
+            out[s] = acc[v];
+        }
+    }
+}
+
+static int fin_sum(const float* slab, int Z, long n, float* out, hipStream_t st, int CO = 0,
+                   int CI = 0, int CIP = 1, int KP = 1) {
+    int zl = 1;
+    while (zl < Z && zl < 16) zl *= 2;
+    const int cols = 256 / zl;
+    if (n % 4 == 0) {
+        hipLaunchKernelGGL(k_fin_sum<4>, dim3(ceil_div(n, 4L * cols)), dim3(256), 0, st, slab, Z, n,
+                           zl, out, CO, CI, CIP, KP);
+    } else {
+        hipLaunchKernelGGL(k_fin_sum<1>, dim3(ceil_div(n, (long)cols)), dim3(256), 0, st, slab, Z,
+                           n, zl, out, CO, CI, CIP, KP);
+    }
+    FLSIM_LAUNCH_CHECK();
+    return 0;
+}
+
+// =============================================================================================
+// GEMM launch helpers
+// =============================================================================================
+template <int FM, int FN, int WM, int WN, class AL, class BL, class EPI>
+static int launch_gemm(const AL& al, const BL& bl, const EPI& epi, int M, int N, int ksteps, int Z,
+                       hipStream_t st, int kid, double alg_flops) {
+    constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
+    const int per = (ksteps + Z - 1) / Z;
+    const int tm = ceil_div(M, BM), tn = ceil_div(N, BN);
+    dim3 grid(tm * tn * Z);
+    const ProbeSlot ps = probe_begin();
+    hipExtLaunchKernelGGL((gemm_kernel<FM, FN, WM, WN, AL, BL, EPI>), grid, dim3(64 * WM * WN), 0,
+                          st, ps.start, ps.stop, 0, al, bl, epi, ksteps, per, tm, tn);
+    FLSIM_LAUNCH_CHECK();
+    return probe_end(ps, kid, alg_flops);
+}
+
+// forward conv (also the data-gradient conv): out[m][n] for m < S*OH*OW, n < N
+template <int IH, int IW, int CI, int PAD, int FM, int FN, int WM, int WN, class EPI>
+static int conv_like(const float* X, int S, const float* Wpk, int N, int KP, const EPI& epi,
+                     hipStream_t st, int kid, int kreal) {
+    constexpr int NT = 64 * WM * WN;
+    constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
+    using AL = Im2colKC<IH, IW, CI, PAD, BM, NT>;
+    using BL = RowsKC<BN, NT>;
+    AL al;
+    al.X = X;
+    al.M = S * AL::OH * AL::OW;
+    BL bl;
+    bl.P = Wpk;
+    bl.ld = KP;
+    bl.NR = N;
+    return launch_gemm<FM, FN, WM, WN>(al, bl, epi, al.M, N, KP / GK, 1, st, kid,
+                                       2.0 * al.M * N * kreal);
+}
+
+// weight gradient: slab[z][co][kk] += sum_p dz[p][co] * im2col(X)[p][kk]  (conv padding PAD)
+template <int IH, int IW, int CI, int PAD, int FM, int FN, int WM, int WN>
+static int conv_wgrad(const float* dz, const float* X, int S, int CO, int KP, float* slab,
+                      float* bslab, int Z, hipStream_t st, int kid, int kreal) {
+    constexpr int NT = 64 * WM * WN;
+    constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
+    using AL = RowsKM<BM, NT>;
+    using BL = Im2colKM<IH, IW, CI, PAD, BN, NT>;
+    const int M = S * BL::OH * BL::OW;
+    AL al;
+    al.P = dz;
+    al.ld = CO;
+    al.NK = M;
+    al.NC = CO;
+    BL bl;
+    bl.X = X;
+    bl.M = M;
+    EpiSlabAcc epi{slab, CO, KP, (long)CO * KP, bslab};
+    return launch_gemm<FM, FN, WM, WN>(al, bl, epi, CO, KP, ceil_div(M, GK), Z, st, kid,
+                                       2.0 * M * CO * kreal);
+}
+
+// forward conv fused with bias + ReLU + 2x2 max-pool (+ dropout: keep iff philox >= thr, kept
+// values * scale): GEMM rows in pool-window order
+template <int IH, int IW, int CI, int CO, int PAD, int FM, int FN, int WM, int WN, bool NCHW_OUT>
+static int conv_pool_fwd(const float* X, int S, const float* Wpk, int KP, float* d, uint8_t* idx,
+                         const float* bias, const WorkerRec* workers, uint64_t seed, uint32_t site,
+                         uint32_t thr, float scale, int dropout, hipStream_t st, int kid,
+                         int kreal) {
+    constexpr int NT = 64 * WM * WN;
+    constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
+    using AL = Im2colKC<IH, IW, CI, PAD, BM, NT, true>;
+    using BL = RowsKC<BN, NT>;
+    AL al;
+    al.X = X;
+    al.M = S * AL::ROWS_PER_IMG;
+    BL bl;
+    bl.P = Wpk;
+    bl.ld = KP;
+    bl.NR = CO;
+    EpiPoolDrop<AL::PH, AL::PW, CO, NCHW_OUT> epi{d, idx, bias, workers, seed, site, thr,
+                                                  scale, dropout, al.M};
+    return launch_gemm<FM, FN, WM, WN>(al, bl, epi, al.M, CO, KP / GK, 1, st, kid,
+                                       2.0 * al.M * CO * kreal);
+}
+
+// linear layer part[z] = x W^T over the z-th K range (x [M][K] rows, W [N][K] torch layout)
+template <int FM, int FN, int WM, int WN>
+static int linear_fwd(const float* x, const float* W, float* part, int M, int N, int K, int Z,
+                      hipStream_t st, int kid) {
+    constexpr int NT = 64 * WM * WN;
+    RowsKC<16 * FM * WM, NT> al{};
+    al.P = x; al.ld = K; al.NR = M;
+    RowsKC<16 * FN * WN, NT> bl{};
+    bl.P = W; bl.ld = K; bl.NR = N;
+    EpiSlabStore epi{part, M, N, (long)M * N};
+    return launch_gemm<FM, FN, WM, WN>(al, bl, epi, M, N, K / GK, Z, st, kid, 2.0 * M * N * K);
+}
+
+// linear weight gradient: slab[z][n][k] += sum_s dy[s][n] x[s][k]; bias slab[z][n] += sum_s dy
+template <int FM, int FN, int WM, int WN>
+static int linear_wgrad(const float* dy, const float* x, float* slab, float* bslab, int S, int N,
+                        int K, int Z, hipStream_t st, int kid) {
+    constexpr int NT = 64 * WM * WN;
+    RowsKM<16 * FM * WM, NT> al{};
+    al.P = dy; al.ld = N; al.NK = S; al.NC = N;
+    RowsKM<16 * FN * WN, NT> bl{};
+    bl.P = x; bl.ld = K; bl.NK = S; bl.NC = K;
+    EpiSlabAcc epi{slab, N, K, (long)N * K, bslab};
+    return launch_gemm<FM, FN, WM, WN>(al, bl, epi, N, K, ceil_div(S, GK), Z, st, kid,
+                                       2.0 * S * N * K);
+}
+
+// linear data gradient through the producer's dropout / ReLU:
+// dx[s][k] = (sum_n dy[s][n] W[n][k]) * scale * (act[s][k] > 0)
+template <int FM, int FN, int WM, int WN>
+static int linear_dgrad(const float* dy, const float* W, float* dx, const float* act, float scale,
+                        int S, int N, int K, hipStream_t st, int kid) {
+    constexpr int NT = 64 * WM * WN;
+    RowsKC<16 * FM * WM, NT> dl{};
+    dl.P = dy; dl.ld = N; dl.NR = S;
+    RowsKM<16 * FN * WN, NT> wl{};
+    wl.P = W; wl.ld = K; wl.NK = N; wl.NC = K;
+    EpiDropMask de{dx, act, scale, S, K};
+    return launch_gemm<FM, FN, WM, WN>(dl, wl, de, S, K, N / GK, 1, st, kid, 2.0 * S * N * K);
+}
+
+}  // namespace flsim

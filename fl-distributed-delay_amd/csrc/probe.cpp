@@ -9,7 +9,13 @@ static const char* KNAME[K_COUNT] = {
     "conv1_fwd", "conv2_fwd", "conv3_fwd", "conv4_fwd", "conv5_fwd", "conv6_fwd", "linear1_fwd",
     "linear2_fwd", "conv2_dgrad", "conv3_dgrad", "conv4_dgrad", "conv5_dgrad", "conv6_dgrad",
     "conv1_wgrad", "conv2_wgrad", "conv3_wgrad", "conv4_wgrad", "conv5_wgrad", "conv6_wgrad",
-    "linear1_wgrad", "linear1_dgrad", "linear2_wgrad", "linear2_dgrad", "aggregate_adam"};
+    "linear1_wgrad", "linear1_dgrad", "linear2_wgrad", "linear2_dgrad", "aggregate_adam",
+    "vgg_conv1_fwd", "vgg_conv2_fwd", "vgg_conv3_fwd", "vgg_conv4_fwd", "vgg_conv5_fwd",
+    "vgg_conv6_fwd", "vgg_conv7_fwd", "vgg_conv8_fwd", "vgg_linear1_fwd", "vgg_linear2_fwd",
+    "vgg_conv2_dgrad", "vgg_conv3_dgrad", "vgg_conv4_dgrad", "vgg_conv5_dgrad", "vgg_conv6_dgrad",
+    "vgg_conv7_dgrad", "vgg_conv8_dgrad", "vgg_conv1_wgrad", "vgg_conv2_wgrad", "vgg_conv3_wgrad",
+    "vgg_conv4_wgrad", "vgg_conv5_wgrad", "vgg_conv6_wgrad", "vgg_conv7_wgrad", "vgg_conv8_wgrad",
+    "vgg_linear1_wgrad", "vgg_linear1_dgrad", "vgg_linear2_wgrad", "vgg_linear2_dgrad"};
 
 struct Probe {
     bool on = false;

@@ -12,7 +12,12 @@ enum KernelId {
     K_FWD1 = 0, K_FWD2, K_FWD3, K_FWD4, K_FWD5, K_FWD6, K_L1F, K_L2F,
     K_DG2, K_DG3, K_DG4, K_DG5, K_DG6,
     K_WG1, K_WG2, K_WG3, K_WG4, K_WG5, K_WG6,
-    K_L1W, K_L1D, K_L2W, K_L2D, K_AGG, K_COUNT
+    K_L1W, K_L1D, K_L2W, K_L2D, K_AGG,
+    // VGG-11 (vgg_net.hip)
+    K_VF1, K_VF2, K_VF3, K_VF4, K_VF5, K_VF6, K_VF7, K_VF8, K_VL1F, K_VL2F,
+    K_VDG2, K_VDG3, K_VDG4, K_VDG5, K_VDG6, K_VDG7, K_VDG8,
+    K_VWG1, K_VWG2, K_VWG3, K_VWG4, K_VWG5, K_VWG6, K_VWG7, K_VWG8,
+    K_VL1W, K_VL1D, K_VL2W, K_VL2D, K_COUNT
 };
 
 // Event pair for the launch that follows (nullptr events when the probe is off or full).  The

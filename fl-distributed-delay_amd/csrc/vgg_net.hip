@@ -1,0 +1,396 @@
+// VGG-11 (reference FL/models.py:50-103: VGG(make_layers(cfg['A'])), vgg11()) forward + backward
+// for a chunk of simulated workers on gfx950 -- configs[4]'s "larger CNN" (SURVEY 8 f2).  Same
+// engine structure as pn1_net.hip: every worker of an epoch runs on the central model theta_t
+// (main.py:154,159,169), so a chunk of W workers is ONE batch of W*128 samples whose gradients
+// add up along the weight-gradient GEMMs' reduction dimension (agents.py:35).
+//
+// Network on 3x32x32 input (models.py:80-98: conv3x3 padding 1 + ReLU, 'M' = 2x2 max-pool):
+//   conv1 3->64 @32 +pool | conv2 64->128 @16 +pool | conv3 128->256 @8 | conv4 256->256 @8
+//   +pool | conv5 256->512 @4 | conv6 512->512 @4 +pool | conv7 512->512 @2 | conv8 512->512 @2
+//   +pool -> 512 features (models.py:75 flatten of a 1x1 map = channel order)
+//   classifier (models.py:57-65): Dropout(.5) -> Linear(512,512) -> ReLU -> Dropout(.5) ->
+//   Linear(512,512) -> ReLU -> Linear(512,10)
+// Each conv + ReLU (+ pool) is one fused MFMA launch (pooled layers: GEMM rows in pool-window
+// order, argmax kept for the backward); the classifier's first Dropout is fused into conv8's pool
+// epilogue.  Activations NHWC fp32.
+#include "net_kernels.h"
+
+namespace flsim {
+
+// Philox sites of the classifier dropouts (models.py:58,61); the oracle uses the same
+enum : uint32_t { SITE_VDROP1 = 6, SITE_VDROP2 = 7 };
+
+struct VConv {
+    int CI, CIP, CO, H;  // input channels (real / padded), output channels, spatial size (in = out)
+    int KP;              // packed forward K = 9*CIP rounded up to 16
+    int ZW;              // weight-gradient pixel splits: thousands of blocks per launch
+};
+static const VConv VG[8] = {
+    {3, 4, 64, 32, 48, 2048},      {64, 64, 128, 16, 576, 256},
+    {128, 128, 256, 8, 1152, 128}, {256, 256, 256, 8, 2304, 64},
+    {256, 256, 512, 4, 2304, 32},  {512, 512, 512, 4, 4608, 16},
+    {512, 512, 512, 2, 4608, 16},  {512, 512, 512, 2, 4608, 16},
+};
+constexpr int VFEAT = 512;   // classifier width
+constexpr int VZL = 16;      // classifier weight-gradient splits
+constexpr int VZH = 32;      // head weight-gradient splits
+
+// flat parameter offsets in named_parameters order: features.{0,3,6,8,11,13,16,18}.{weight,bias},
+// classifier.{1,4,6}.{weight,bias}
+struct VOff {
+    long w[8], b[8], l1w, l1b, l2w, l2b, l3w, l3b, total;
+};
+static VOff voff() {
+    VOff o;
+    long p = 0;
+    for (int l = 0; l < 8; ++l) {
+        o.w[l] = p;
+        p += (long)VG[l].CO * VG[l].CI * 9;
+        o.b[l] = p;
+        p += VG[l].CO;
+    }
+    o.l1w = p; p += (long)VFEAT * VFEAT;
+    o.l1b = p; p += VFEAT;
+    o.l2w = p; p += (long)VFEAT * VFEAT;
+    o.l2b = p; p += VFEAT;
+    o.l3w = p; p += 10L * VFEAT;
+    o.l3b = p; p += 10;
+    o.total = p;
+    return o;
+}
+
+// gradient state (floats): packed weights + weight-gradient slabs
+struct VGrad {
+    float* wf[8];
+    float* wd[8];   // wd[0] unused (the input needs no gradient)
+    float* sw[8];   // [ZW][CO][KP]
+    float* sb[8];   // [ZW][CO]
+    float *l1w, *l1b, *l2w, *l2b, *l3w, *l3b;
+    float* slab_begin;
+    long slab_floats, total_floats;
+};
+
+static VGrad vgs_layout(float* base) {
+    VGrad g;
+    long o = 0;
+    auto take = [&](long n) {
+        float* p = base ? base + o : nullptr;
+        o += (n + 63) / 64 * 64;
+        return p;
+    };
+    for (int l = 0; l < 8; ++l) {
+        g.wf[l] = take((long)VG[l].CO * VG[l].KP);
+        g.wd[l] = l ? take((long)VG[l].CI * 9 * VG[l].CO) : nullptr;
+    }
+    const long slab0 = o;
+    g.slab_begin = base ? base + o : nullptr;
+    for (int l = 0; l < 8; ++l) {
+        g.sw[l] = take((long)VG[l].ZW * VG[l].CO * VG[l].KP);
+        g.sb[l] = take((long)VG[l].ZW * VG[l].CO);
+    }
+    g.l1w = take((long)VZL * VFEAT * VFEAT);
+    g.l1b = take((long)VZL * VFEAT);
+    g.l2w = take((long)VZL * VFEAT * VFEAT);
+    g.l2b = take((long)VZL * VFEAT);
+    g.l3w = take((long)VZH * 10 * VFEAT);
+    g.l3b = take((long)VZH * 10);
+    g.slab_floats = o - slab0;
+    g.total_floats = o;
+    return g;
+}
+
+// workspace (per chunk of S samples).  Forward: x0, pooled maps d*, unpooled a*, f0 = dropped
+// features, e1 = dropped relu(linear1), e2 = relu(linear2), argmax bytes i*.  Backward: dz of a
+// conv output goes to ga (full-resolution maps after a pool scatter) or gb, pooled gradients to gy.
+struct VWS {
+    float *x0, *d1, *d2, *a3, *d4, *a5, *d6, *a7, *f0, *e1, *e2, *part, *dh1, *dh2;
+    float *ga, *gb, *gy, *loss_s, *dlog;
+    int32_t* y;
+    uint8_t *i1, *i2, *i4, *i6, *i8;
+    long bytes;
+};
+
+static VWS vws_layout(char* base, int S) {
+    VWS w;
+    long o = 0;
+    auto take = [&](long bytes) {
+        char* p = base ? base + o : nullptr;
+        o += (bytes + 255) / 256 * 256;
+        return p;
+    };
+    auto tf = [&](long per) { return (float*)take(per * (long)S * 4); };
+    auto tb = [&](long per) { return (uint8_t*)take(per * (long)S); };
+    w.x0 = tf(4096);
+    w.d1 = tf(16 * 16 * 64);
+    w.d2 = tf(8 * 8 * 128);
+    w.a3 = tf(8 * 8 * 256);
+    w.d4 = tf(4 * 4 * 256);
+    w.a5 = tf(4 * 4 * 512);
+    w.d6 = tf(2 * 2 * 512);
+    w.a7 = tf(2 * 2 * 512);
+    w.f0 = tf(VFEAT);
+    w.e1 = tf(VFEAT);
+    w.e2 = tf(VFEAT);
+    w.part = tf(VFEAT);
+    w.dh1 = tf(VFEAT);
+    w.dh2 = tf(VFEAT);
+    w.ga = tf(32 * 32 * 64);
+    w.gb = tf(8 * 8 * 256);
+    w.gy = tf(16 * 16 * 64);
+    w.loss_s = tf(1);
+    w.dlog = tf(16);
+    w.y = (int32_t*)take(4L * S);
+    w.i1 = tb(16 * 16 * 64);
+    w.i2 = tb(8 * 8 * 128);
+    w.i4 = tb(4 * 4 * 256);
+    w.i6 = tb(2 * 2 * 512);
+    w.i8 = tb(VFEAT);
+    w.bytes = o;
+    return w;
+}
+
+static int vpack(const VGrad& g, const float* th, hipStream_t st) {
+    const VOff o = voff();
+    for (int l = 0; l < 8; ++l)
+        RC(pack_conv(th + o.w[l], g.wf[l], g.wd[l], VG[l].CO, VG[l].CI, VG[l].CIP, VG[l].KP, st));
+    return 0;
+}
+
+// models.py:73-77 (features, flatten, classifier) up to the last ReLU; the head follows
+static int vforward(const VGrad& g, const VWS& w, const float* th, int S, const WorkerRec* workers,
+                    uint64_t seed, int dropout, hipStream_t st) {
+    const VOff o = voff();
+    // conv1 + ReLU + pool (features.0-2)
+    RC((conv_pool_fwd<32, 32, 4, 64, 1, 2, 4, 4, 1, false>(w.x0, S, g.wf[0], 48, w.d1, w.i1,
+        th + o.b[0], workers, seed, 0, 0, 1.f, 0, st, K_VF1, 27)));
+    // conv2 + ReLU + pool (features.3-5)
+    RC((conv_pool_fwd<16, 16, 64, 128, 1, 4, 4, 2, 2, false>(w.d1, S, g.wf[1], 576, w.d2, w.i2,
+        th + o.b[1], workers, seed, 0, 0, 1.f, 0, st, K_VF2, 576)));
+    // conv3 + ReLU (features.6-7)
+    RC((conv_like<8, 8, 128, 1, 4, 4, 2, 2>(w.d2, S, g.wf[2], 256, 1152,
+        EpiBiasRelu{w.a3, th + o.b[2], S * 64, 256}, st, K_VF3, 1152)));
+    // conv4 + ReLU + pool (features.8-10)
+    RC((conv_pool_fwd<8, 8, 256, 256, 1, 4, 4, 2, 2, false>(w.a3, S, g.wf[3], 2304, w.d4, w.i4,
+        th + o.b[3], workers, seed, 0, 0, 1.f, 0, st, K_VF4, 2304)));
+    // conv5 + ReLU (features.11-12)
+    RC((conv_like<4, 4, 256, 1, 4, 4, 2, 2>(w.d4, S, g.wf[4], 512, 2304,
+        EpiBiasRelu{w.a5, th + o.b[4], S * 16, 512}, st, K_VF5, 2304)));
+    // conv6 + ReLU + pool (features.13-15)
+    RC((conv_pool_fwd<4, 4, 512, 512, 1, 4, 4, 2, 2, false>(w.a5, S, g.wf[5], 4608, w.d6, w.i6,
+        th + o.b[5], workers, seed, 0, 0, 1.f, 0, st, K_VF6, 4608)));
+    // conv7 + ReLU (features.16-17)
+    RC((conv_like<2, 2, 512, 1, 4, 4, 2, 2>(w.d6, S, g.wf[6], 512, 4608,
+        EpiBiasRelu{w.a7, th + o.b[6], S * 4, 512}, st, K_VF7, 4608)));
+    // conv8 + ReLU + pool (features.18-20) + classifier Dropout (models.py:58): the 1x1 pooled map
+    // is the flattened feature vector
+    RC((conv_pool_fwd<2, 2, 512, 512, 1, 4, 4, 2, 2, false>(w.a7, S, g.wf[7], 4608, w.f0, w.i8,
+        th + o.b[7], workers, seed, SITE_VDROP1, THR_P50, SCALE_P50, dropout, st, K_VF8, 4608)));
+    // Linear + ReLU + Dropout (models.py:59-61)
+    RC((linear_fwd<4, 4, 2, 2>(w.f0, th + o.l1w, w.part, S, VFEAT, VFEAT, 1, st, K_VL1F)));
+    RC(linear_finish(w.part, 1, th + o.l1b, w.e1, S, VFEAT, workers, seed, SITE_VDROP2, THR_P50,
+                     SCALE_P50, dropout, st));
+    // Linear + ReLU (models.py:62-63)
+    RC((linear_fwd<4, 4, 2, 2>(w.e1, th + o.l2w, w.part, S, VFEAT, VFEAT, 1, st, K_VL2F)));
+    RC(linear_finish(w.part, 1, th + o.l2b, w.e2, S, VFEAT, workers, seed, 0, 0, 1.f, 0, st));
+    return 0;
+}
+
+// backward from the head's dlog / dh2 (gradient wrt linear2's pre-activation)
+static int vbackward(const VGrad& g, const VWS& w, const float* th, int S, int dropout,
+                     hipStream_t st) {
+    const VOff o = voff();
+    const float s50 = dropout ? SCALE_P50 : 1.f;
+    // Linear(512,10) weight / bias
+    RC(head_wgrad<VFEAT>(w.dlog, w.e2, g.l3w, g.l3b, S, VZH, st));
+    // Linear2: wgrad (input e1), dgrad through Dropout + ReLU of Linear1 (e1 is the dropped output)
+    RC((linear_wgrad<4, 4, 2, 2>(w.dh2, w.e1, g.l2w, g.l2b, S, VFEAT, VFEAT, VZL, st, K_VL2W)));
+    RC((linear_dgrad<4, 4, 2, 2>(w.dh2, th + o.l2w, w.dh1, w.e1, s50, S, VFEAT, VFEAT, st,
+                                 K_VL2D)));
+    // Linear1: wgrad (input f0 = dropped features), dgrad through the first Dropout and conv8's
+    // pooled ReLU (f0 > 0), then the pool scatter -> dz8
+    RC((linear_wgrad<4, 4, 2, 2>(w.dh1, w.f0, g.l1w, g.l1b, S, VFEAT, VFEAT, VZL, st, K_VL1W)));
+    RC((linear_dgrad<4, 4, 2, 2>(w.dh1, th + o.l1w, w.gy, w.f0, s50, S, VFEAT, VFEAT, st,
+                                 K_VL1D)));
+    RC((pool_scatter<2, 2, 512, false>(w.gy, w.i8, w.ga, S, st)));
+    // conv8: wgrad (input a7), dgrad -> dz7 = . * (a7 > 0)
+    RC((conv_wgrad<2, 2, 512, 1, 4, 4, 2, 2>(w.ga, w.a7, S, 512, 4608, g.sw[7], g.sb[7], VG[7].ZW,
+                                            st, K_VWG8, 4608)));
+    RC((conv_like<2, 2, 512, 1, 4, 4, 2, 2>(w.ga, S, g.wd[7], 512, 4608,
+        EpiMask<true>{w.gb, w.a7, S * 4, 512}, st, K_VDG8, 4608)));
+    // conv7: wgrad (input d6), dgrad -> gradient wrt d6 (d6 > 0), pool scatter -> dz6
+    RC((conv_wgrad<2, 2, 512, 1, 4, 4, 2, 2>(w.gb, w.d6, S, 512, 4608, g.sw[6], g.sb[6], VG[6].ZW,
+                                            st, K_VWG7, 4608)));
+    RC((conv_like<2, 2, 512, 1, 4, 4, 2, 2>(w.gb, S, g.wd[6], 512, 4608,
+        EpiDropMask{w.gy, w.d6, 1.f, S * 4, 512}, st, K_VDG7, 4608)));
+    RC((pool_scatter<4, 4, 512, false>(w.gy, w.i6, w.ga, S, st)));
+    // conv6: wgrad (input a5), dgrad -> dz5 = . * (a5 > 0)
+    RC((conv_wgrad<4, 4, 512, 1, 4, 4, 2, 2>(w.ga, w.a5, S, 512, 4608, g.sw[5], g.sb[5], VG[5].ZW,
+                                            st, K_VWG6, 4608)));
+    RC((conv_like<4, 4, 512, 1, 4, 4, 2, 2>(w.ga, S, g.wd[5], 512, 4608,
+        EpiMask<true>{w.gb, w.a5, S * 16, 512}, st, K_VDG6, 4608)));
+    // conv5: wgrad (input d4), dgrad -> gradient wrt d4, pool scatter -> dz4
+    RC((conv_wgrad<4, 4, 256, 1, 4, 4, 2, 2>(w.gb, w.d4, S, 512, 2304, g.sw[4], g.sb[4], VG[4].ZW,
+                                            st, K_VWG5, 2304)));
+    RC((conv_like<4, 4, 512, 1, 4, 4, 2, 2>(w.gb, S, g.wd[4], 256, 4608,
+        EpiDropMask{w.gy, w.d4, 1.f, S * 16, 256}, st, K_VDG5, 4608)));
+    RC((pool_scatter<8, 8, 256, false>(w.gy, w.i4, w.ga, S, st)));
+    // conv4: wgrad (input a3), dgrad -> dz3 = . * (a3 > 0)
+    RC((conv_wgrad<8, 8, 256, 1, 4, 4, 2, 2>(w.ga, w.a3, S, 256, 2304, g.sw[3], g.sb[3], VG[3].ZW,
+                                            st, K_VWG4, 2304)));
+    RC((conv_like<8, 8, 256, 1, 4, 4, 2, 2>(w.ga, S, g.wd[3], 256, 2304,
+        EpiMask<true>{w.gb, w.a3, S * 64, 256}, st, K_VDG4, 2304)));
+    // conv3: wgrad (input d2), dgrad -> gradient wrt d2, pool scatter -> dz2
+    RC((conv_wgrad<8, 8, 128, 1, 4, 4, 2, 2>(w.gb, w.d2, S, 256, 1152, g.sw[2], g.sb[2], VG[2].ZW,
+                                            st, K_VWG3, 1152)));
+    RC((conv_like<8, 8, 256, 1, 4, 4, 2, 2>(w.gb, S, g.wd[2], 128, 2304,
+        EpiDropMask{w.gy, w.d2, 1.f, S * 64, 128}, st, K_VDG3, 2304)));
+    RC((pool_scatter<16, 16, 128, false>(w.gy, w.i2, w.ga, S, st)));
+    // conv2: wgrad (input d1), dgrad -> gradient wrt d1, pool scatter -> dz1
+    RC((conv_wgrad<16, 16, 64, 1, 4, 4, 2, 2>(w.ga, w.d1, S, 128, 576, g.sw[1], g.sb[1], VG[1].ZW,
+                                             st, K_VWG2, 576)));
+    RC((conv_like<16, 16, 128, 1, 2, 4, 4, 1>(w.ga, S, g.wd[1], 64, 1152,
+        EpiDropMask{w.gy, w.d1, 1.f, S * 256, 64}, st, K_VDG2, 1152)));
+    RC((pool_scatter<32, 32, 64, false>(w.gy, w.i1, w.ga, S, st)));
+    // conv1: wgrad (input x0)
+    RC((conv_wgrad<32, 32, 4, 1, 4, 3, 1, 1>(w.ga, w.x0, S, 64, 48, g.sw[0], g.sb[0], VG[0].ZW, st,
+                                            K_VWG1, 27)));
+    return 0;
+}
+
+static int vrun_chunk(void* gradstate, const VWS& w, const float* theta, const WorkerRec* workers,
+                      int n_chunk_workers, uint64_t seed, int dropout, int backward_pass,
+                      float* worker_loss, hipStream_t stream) {
+    const int S = n_chunk_workers * SAMPLES_PER_WORKER;
+    const VOff o = voff();
+    VGrad g = vgs_layout((float*)gradstate);
+    RC(vforward(g, w, theta, S, workers, seed, dropout, stream));
+    // Linear(512,10) + CrossEntropyLoss (models.py:64, main.py:107); no dropout after the ReLU
+    RC(head_and_loss<VFEAT>(w.e2, theta + o.l3w, theta + o.l3b, w.y, w.loss_s, w.dlog, w.dh2, S,
+                            backward_pass, 1.f, worker_loss, stream));
+    if (backward_pass) RC(vbackward(g, w, theta, S, dropout, stream));
+    return 0;
+}
+
+}  // namespace flsim
+
+using namespace flsim;
+
+// =============================================================================================
+// C-ABI (declared in include/flsim.h): the flsim_pn1_* contract for vgg11()
+// =============================================================================================
+extern "C" {
+
+long flsim_vgg11_param_count(void) { return voff().total; }
+
+long flsim_vgg11_gradstate_bytes(void) { return vgs_layout(nullptr).total_floats * 4; }
+
+long flsim_vgg11_workspace_bytes(int max_samples) { return vws_layout(nullptr, max_samples).bytes; }
+
+int flsim_vgg11_workspace_offset(int which, int samples, long* offset_bytes) {
+    char* const fake = reinterpret_cast<char*>(4096);   // layout only; never dereferenced
+    VWS w = vws_layout(fake, samples);
+    const void* p[] = {w.x0, w.d1, w.d2, w.a3, w.d4, w.a5, w.d6, w.a7, w.f0, w.e1, w.e2, w.dh1,
+                       w.dh2, w.ga, w.gb, w.gy, w.loss_s, w.dlog, w.y, w.i1, w.i2, w.i4, w.i6,
+                       w.i8};
+    FLSIM_REQUIRE(offset_bytes, "null pointer");
+    FLSIM_REQUIRE(which >= 0 && which < (int)(sizeof(p) / sizeof(p[0])), "bad workspace id %d",
+                  which);
+    *offset_bytes = (long)((const char*)p[which] - fake);
+    return 0;
+}
+
+int flsim_vgg11_begin_epoch(void* gradstate, const float* theta, hipStream_t stream) {
+    FLSIM_REQUIRE(gradstate && theta, "null pointer");
+    VGrad g = vgs_layout((float*)gradstate);
+    RC(vpack(g, theta, stream));
+    FLSIM_CHECK_HIP(hipMemsetAsync(g.slab_begin, 0, g.slab_floats * 4, stream));
+    return 0;
+}
+
+int flsim_vgg11_fwd_bwd_chunk(void* gradstate, void* workspace, int max_samples,
+                              const float* theta, const uint8_t* pool, const int32_t* labels,
+                              const int32_t* list_a, int len_a, const int32_t* list_b, int len_b,
+                              const float* lut, const WorkerRec* workers, int n_chunk_workers,
+                              int n_workers_total, uint64_t seed, int dropout, int backward_pass,
+                              float* worker_loss, hipStream_t stream) {
+    FLSIM_REQUIRE(gradstate && workspace && theta && pool && labels && list_a && list_b && lut &&
+                  workers && worker_loss, "null pointer");
+    FLSIM_REQUIRE(n_chunk_workers > 0, "empty chunk");
+    const int S = n_chunk_workers * SAMPLES_PER_WORKER;
+    FLSIM_REQUIRE(S <= max_samples, "chunk of %d samples exceeds workspace (%d)", S, max_samples);
+    FLSIM_REQUIRE(S <= 16384, "chunk of %d samples exceeds the 32-bit index budget", S);
+    FLSIM_REQUIRE(len_a > 0 && len_b > 0, "empty class list");
+    VWS w = vws_layout((char*)workspace, max_samples);
+    hipLaunchKernelGGL(k_fill_batch, dim3(S), dim3(256), 0, stream, pool, labels, list_a, len_a,
+                       list_b, len_b, workers, n_workers_total, seed, lut, w.x0, w.y);
+    FLSIM_LAUNCH_CHECK();
+    return vrun_chunk(gradstate, w, theta, workers, n_chunk_workers, seed, dropout, backward_pass,
+                      worker_loss, stream);
+}
+
+int flsim_vgg11_fwd_bwd_input(void* gradstate, void* workspace, int max_samples,
+                              const float* theta, const float* x, const int64_t* y, int n_samples,
+                              const WorkerRec* workers, uint64_t seed, int dropout,
+                              int backward_pass, float* worker_loss, hipStream_t stream) {
+    FLSIM_REQUIRE(gradstate && workspace && theta && x && y && workers && worker_loss,
+                  "null pointer");
+    FLSIM_REQUIRE(n_samples > 0 && n_samples % SAMPLES_PER_WORKER == 0,
+                  "batch of %d samples: must be a positive multiple of %d", n_samples,
+                  SAMPLES_PER_WORKER);
+    FLSIM_REQUIRE(n_samples <= max_samples, "batch of %d samples exceeds workspace (%d)", n_samples,
+                  max_samples);
+    FLSIM_REQUIRE(n_samples <= 16384, "batch of %d samples exceeds the 32-bit index budget",
+                  n_samples);
+    VWS w = vws_layout((char*)workspace, max_samples);
+    hipLaunchKernelGGL(k_load_input, dim3(n_samples), dim3(256), 0, stream, x, y, w.x0, w.y);
+    FLSIM_LAUNCH_CHECK();
+    return vrun_chunk(gradstate, w, theta, workers, n_samples / SAMPLES_PER_WORKER, seed, dropout,
+                      backward_pass, worker_loss, stream);
+}
+
+// Evaluation (util.py:31-45 after central.model.eval(), main.py:190: dropout off)
+int flsim_vgg11_eval_pool(void* gradstate, void* workspace, int max_samples, const float* theta,
+                          const uint8_t* pool, int first, int n_images, const float* lut,
+                          int32_t* pred, hipStream_t stream) {
+    FLSIM_REQUIRE(gradstate && workspace && theta && pool && lut && pred, "null pointer");
+    FLSIM_REQUIRE(n_images > 0 && first >= 0, "bad image range");
+    FLSIM_REQUIRE(max_samples >= SAMPLES_PER_WORKER && max_samples % SAMPLES_PER_WORKER == 0,
+                  "max_samples must be a positive multiple of %d", SAMPLES_PER_WORKER);
+    const VOff o = voff();
+    VGrad g = vgs_layout((float*)gradstate);
+    VWS w = vws_layout((char*)workspace, max_samples);
+    RC(vpack(g, theta, stream));
+    for (int c0 = 0; c0 < n_images; c0 += max_samples) {
+        const int n = n_images - c0 < max_samples ? n_images - c0 : max_samples;
+        const int S = ceil_div(n, SAMPLES_PER_WORKER) * SAMPLES_PER_WORKER;
+        hipLaunchKernelGGL(k_fill_seq, dim3(S), dim3(256), 0, stream, pool, first + c0, n, lut,
+                           w.x0, w.y);
+        FLSIM_LAUNCH_CHECK();
+        RC(vforward(g, w, theta, S, nullptr, 0, 0, stream));
+        RC(head_predict<VFEAT>(w.e2, theta + o.l3w, theta + o.l3b, w.y, w.loss_s, S, pred + c0, n,
+                               stream));
+    }
+    return 0;
+}
+
+// S_t (torch named_parameters layout) = sum of the epoch's slabs (fixed order)
+int flsim_vgg11_end_epoch(void* gradstate, float* grad_out, hipStream_t stream) {
+    FLSIM_REQUIRE(gradstate && grad_out, "null pointer");
+    const VOff o = voff();
+    VGrad g = vgs_layout((float*)gradstate);
+    for (int l = 0; l < 8; ++l) {
+        const VConv& c = VG[l];
+        RC(fin_sum(g.sw[l], c.ZW, (long)c.CO * c.KP, grad_out + o.w[l], stream, c.CO, c.CI, c.CIP,
+                   c.KP));
+        RC(fin_sum(g.sb[l], c.ZW, c.CO, grad_out + o.b[l], stream));
+    }
+    RC(fin_sum(g.l1w, VZL, (long)VFEAT * VFEAT, grad_out + o.l1w, stream));
+    RC(fin_sum(g.l1b, VZL, VFEAT, grad_out + o.l1b, stream));
+    RC(fin_sum(g.l2w, VZL, (long)VFEAT * VFEAT, grad_out + o.l2w, stream));
+    RC(fin_sum(g.l2b, VZL, VFEAT, grad_out + o.l2b, stream));
+    RC(fin_sum(g.l3w, VZH, 10L * VFEAT, grad_out + o.l3w, stream));
+    RC(fin_sum(g.l3b, VZH, 10, grad_out + o.l3b, stream));
+    return 0;
+}
+
+}  // extern "C"

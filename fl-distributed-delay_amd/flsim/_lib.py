@@ -18,7 +18,10 @@ EXPORTS = [
     "flsim_sched_state", "flsim_pn1_param_count", "flsim_pn1_gradstate_bytes",
     "flsim_pn1_workspace_bytes", "flsim_pn1_workspace_offset", "flsim_pn1_begin_epoch",
     "flsim_pn1_fwd_bwd_chunk", "flsim_pn1_fwd_bwd_input", "flsim_pn1_end_epoch",
-    "flsim_pn1_eval_pool",
+    "flsim_pn1_eval_pool", "flsim_vgg11_param_count", "flsim_vgg11_gradstate_bytes",
+    "flsim_vgg11_workspace_bytes", "flsim_vgg11_workspace_offset", "flsim_vgg11_begin_epoch",
+    "flsim_vgg11_fwd_bwd_chunk", "flsim_vgg11_fwd_bwd_input", "flsim_vgg11_end_epoch",
+    "flsim_vgg11_eval_pool",
     "flsim_aggregate_adam", "flsim_aggregate_adam_seq", "flsim_probe_enable", "flsim_probe_read", "flsim_probe_disable",
     "flsim_probe_kernel_count", "flsim_probe_kernel_name",
 ]
@@ -51,21 +54,24 @@ def lib():
     L.flsim_sched_destroy.argtypes = [vp]
     L.flsim_sched_epoch.argtypes = [vp] * 6
     L.flsim_sched_state.argtypes = [vp, vp]
-    L.flsim_pn1_param_count.restype = ctypes.c_long
-    L.flsim_pn1_gradstate_bytes.restype = ctypes.c_long
-    L.flsim_pn1_workspace_bytes.restype = ctypes.c_long
-    L.flsim_pn1_workspace_bytes.argtypes = [ctypes.c_int]
-    L.flsim_pn1_workspace_offset.argtypes = [ctypes.c_int, ctypes.c_int, vp]
-    L.flsim_pn1_begin_epoch.argtypes = [vp, vp, vp]
-    L.flsim_pn1_fwd_bwd_chunk.argtypes = [
-        vp, vp, ctypes.c_int, vp, vp, vp, vp, ctypes.c_int, vp, ctypes.c_int, vp, vp,
-        ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, vp, vp]
-    L.flsim_pn1_fwd_bwd_input.argtypes = [
-        vp, vp, ctypes.c_int, vp, vp, vp, ctypes.c_int, vp, ctypes.c_uint64, ctypes.c_int,
-        ctypes.c_int, vp, vp]
-    L.flsim_pn1_end_epoch.argtypes = [vp, vp, vp]
-    L.flsim_pn1_eval_pool.argtypes = [vp, vp, ctypes.c_int, vp, vp, ctypes.c_int, ctypes.c_int,
-                                      vp, vp, vp]
+    for net in ("pn1", "vgg11"):          # the same per-network contract (include/flsim.h)
+        def f(name):
+            return getattr(L, f"flsim_{net}_{name}")
+        f("param_count").restype = ctypes.c_long
+        f("gradstate_bytes").restype = ctypes.c_long
+        f("workspace_bytes").restype = ctypes.c_long
+        f("workspace_bytes").argtypes = [ctypes.c_int]
+        f("workspace_offset").argtypes = [ctypes.c_int, ctypes.c_int, vp]
+        f("begin_epoch").argtypes = [vp, vp, vp]
+        f("fwd_bwd_chunk").argtypes = [
+            vp, vp, ctypes.c_int, vp, vp, vp, vp, ctypes.c_int, vp, ctypes.c_int, vp, vp,
+            ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, vp, vp]
+        f("fwd_bwd_input").argtypes = [
+            vp, vp, ctypes.c_int, vp, vp, vp, ctypes.c_int, vp, ctypes.c_uint64, ctypes.c_int,
+            ctypes.c_int, vp, vp]
+        f("end_epoch").argtypes = [vp, vp, vp]
+        f("eval_pool").argtypes = [vp, vp, ctypes.c_int, vp, vp, ctypes.c_int, ctypes.c_int,
+                                   vp, vp, vp]
     L.flsim_aggregate_adam.argtypes = [
         vp, ctypes.c_int, vp, ctypes.c_int, vp, vp, vp, ctypes.c_long, vp, ctypes.c_int,
         ctypes.c_long, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp]

@@ -1,9 +1,13 @@
-"""PerformantNet1 engine: device buffers + the C-ABI calls of one epoch.
+"""Worker-batched network engines: device buffers + the C-ABI calls of one epoch.
 
   begin_epoch(theta)      pack theta_t, zero the gradient slabs        (start of main.py:126)
   run_chunk(...)          worker-batched fwd/bwd of a chunk of workers (agents.py:32-40, xN)
   end_epoch(S)            S_t = sum of the epoch's gradients           (agents.py:35 accumulation)
   aggregate_adam(...)     fused rule() + Central.update_model          (main.py:23-25,184,188)
+
+PN1Engine runs models.py:PerformantNet1 (the model main.py:97 builds) through flsim_pn1_*;
+VGG11Engine runs models.py:vgg11() (models.py:50-103, configs[4]'s larger CNN) through
+flsim_vgg11_*.  Both entry-point families share one contract (include/flsim.h).
 """
 from __future__ import annotations
 
@@ -26,7 +30,23 @@ PN1_SHAPES = [
     ("linear2.weight", (256, 512)), ("linear2.bias", (256,)),
     ("linear3.weight", (10, 256)), ("linear3.bias", (10,)),
 ]
+# named_parameters() order of models.py:vgg11() (features = make_layers(cfg 'A'),
+# models.py:80-98; classifier models.py:57-65)
+VGG11_SHAPES = [
+    ("features.0.weight", (64, 3, 3, 3)), ("features.0.bias", (64,)),
+    ("features.3.weight", (128, 64, 3, 3)), ("features.3.bias", (128,)),
+    ("features.6.weight", (256, 128, 3, 3)), ("features.6.bias", (256,)),
+    ("features.8.weight", (256, 256, 3, 3)), ("features.8.bias", (256,)),
+    ("features.11.weight", (512, 256, 3, 3)), ("features.11.bias", (512,)),
+    ("features.13.weight", (512, 512, 3, 3)), ("features.13.bias", (512,)),
+    ("features.16.weight", (512, 512, 3, 3)), ("features.16.bias", (512,)),
+    ("features.18.weight", (512, 512, 3, 3)), ("features.18.bias", (512,)),
+    ("classifier.1.weight", (512, 512)), ("classifier.1.bias", (512,)),
+    ("classifier.4.weight", (512, 512)), ("classifier.4.bias", (512,)),
+    ("classifier.6.weight", (10, 512)), ("classifier.6.bias", (10,)),
+]
 PN1_SIZES = [int(np.prod(s)) for _, s in PN1_SHAPES]
+VGG11_SIZES = [int(np.prod(s)) for _, s in VGG11_SHAPES]
 SAMPLES_PER_WORKER = 128
 
 
@@ -34,35 +54,46 @@ def padded(n, q=64):
     return (n + q - 1) // q * q
 
 
-def split_views(flat):
+def split_views(flat, shapes=PN1_SHAPES):
     out, off = [], 0
-    for (_, shp), n in zip(PN1_SHAPES, PN1_SIZES):
+    for _, shp in shapes:
+        n = int(np.prod(shp))
         out.append(flat[off:off + n].view(shp))
         off += n
     return out
 
 
-class PN1Engine:
+class NetEngine:
+    """Gradient state + chunk workspace of one network on one device; PREFIX selects the C-ABI
+    family (flsim_<PREFIX>_*), SHAPES its named_parameters layout."""
+
+    PREFIX = None
+    MODEL = None
+    SHAPES = None
+    FLOP_PER_WORKER_STEP = None     # algorithmic fwd + dgrad + wgrad FLOPs of 128 samples
+
     def __init__(self, device, chunk_workers=32):
-        L = lib()
         self.device = torch.device(device)
-        self.P = int(L.flsim_pn1_param_count())
-        assert self.P == sum(PN1_SIZES)
+        self.SIZES = [int(np.prod(s)) for _, s in self.SHAPES]
+        self.P = int(self._fn("param_count")())
+        assert self.P == sum(self.SIZES)
         self.chunk_workers = int(chunk_workers)
         self.max_samples = self.chunk_workers * SAMPLES_PER_WORKER
-        self.gradstate = torch.empty(int(L.flsim_pn1_gradstate_bytes()), dtype=torch.uint8,
+        self.gradstate = torch.empty(int(self._fn("gradstate_bytes")()), dtype=torch.uint8,
                                      device=self.device)
-        self.workspace = torch.empty(int(L.flsim_pn1_workspace_bytes(self.max_samples)),
+        self.workspace = torch.empty(int(self._fn("workspace_bytes")(self.max_samples)),
                                      dtype=torch.uint8, device=self.device)
-        self.sizes = (ctypes.c_long * len(PN1_SIZES))(*PN1_SIZES)
+
+    def _fn(self, name):
+        return getattr(lib(), f"flsim_{self.PREFIX}_{name}")
 
     # -- per-epoch gradient --------------------------------------------------------------------
     def begin_epoch(self, theta):
-        check(lib().flsim_pn1_begin_epoch(ptr(self.gradstate), ptr(theta), stream_ptr()))
+        check(self._fn("begin_epoch")(ptr(self.gradstate), ptr(theta), stream_ptr()))
 
     def run_chunk(self, theta, pool, workers_dev, n_chunk, n_workers_total, seed, dropout,
                   loss_out, backward=True):
-        check(lib().flsim_pn1_fwd_bwd_chunk(
+        check(self._fn("fwd_bwd_chunk")(
             ptr(self.gradstate), ptr(self.workspace), self.max_samples, ptr(theta),
             ptr(pool.imgs), ptr(pool.labels), ptr(pool.list_a), int(pool.list_a.numel()),
             ptr(pool.list_b), int(pool.list_b.numel()), ptr(pool.lut), ptr(workers_dev),
@@ -72,7 +103,7 @@ class PN1Engine:
     def run_input(self, theta, x, y, workers_dev, seed, dropout, loss_out, backward=True):
         x = x.contiguous()
         y = y.to(torch.int64).contiguous()
-        check(lib().flsim_pn1_fwd_bwd_input(
+        check(self._fn("fwd_bwd_input")(
             ptr(self.gradstate), ptr(self.workspace), self.max_samples, ptr(theta), ptr(x), ptr(y),
             int(x.shape[0]), ptr(workers_dev), ctypes.c_uint64(seed), int(bool(dropout)),
             int(bool(backward)), ptr(loss_out), stream_ptr()))
@@ -82,19 +113,18 @@ class PN1Engine:
         util.print_test_accuracy's forward (util.py:31-45).  Returns a device int32 tensor."""
         n = int(pool.imgs.shape[0]) - first if n_images is None else int(n_images)
         pred = torch.empty(n, dtype=torch.int32, device=self.device)
-        check(lib().flsim_pn1_eval_pool(
+        check(self._fn("eval_pool")(
             ptr(self.gradstate), ptr(self.workspace), self.max_samples, ptr(theta), ptr(pool.imgs),
             int(first), n, ptr(pool.lut), ptr(pred), stream_ptr()))
         return pred
 
     def end_epoch(self, grad_out):
-        check(lib().flsim_pn1_end_epoch(ptr(self.gradstate), ptr(grad_out), stream_ptr()))
+        check(self._fn("end_epoch")(ptr(self.gradstate), ptr(grad_out), stream_ptr()))
 
     def workspace_view(self, which, shape, dtype=torch.float32, samples=None):
-        """Debug view of a workspace tensor (ids: x0 a1 a2 d1 a3 a4 d2 a5 a6 d3 e1 e2 dh1 dh2
-        gx gy loss_s dlog y i1 i2 i3 = 0..21)."""
+        """Debug view of a workspace tensor by id (PN1Engine.WORKSPACE / VGG11Engine.WORKSPACE)."""
         off = ctypes.c_long()
-        check(lib().flsim_pn1_workspace_offset(which, self.max_samples, ctypes.byref(off)))
+        check(self._fn("workspace_offset")(which, self.max_samples, ctypes.byref(off)))
         n = int(np.prod(shape)) * torch.tensor([], dtype=dtype).element_size()
         return self.workspace[off.value:off.value + n].view(dtype).view(shape)
 
@@ -102,11 +132,46 @@ class PN1Engine:
     def aggregate_adam(self, S, c, stale, theta, m, v, step, lr=1e-3, betas=(0.9, 0.999),
                        eps=1e-8):
         """stale: list of device tensors (or None = zero entry)."""
-        aggregate_adam(S, c, stale, theta, m, v, step, PN1_SIZES, lr, betas, eps)
+        aggregate_adam(S, c, stale, theta, m, v, step, self.SIZES, lr, betas, eps)
 
     def aggregate_adam_seq(self, S, k, events, arrays, theta, m, v, step, lr=1e-3,
                            betas=(0.9, 0.999), eps=1e-8):
-        aggregate_adam_seq(S, k, events, arrays, theta, m, v, step, PN1_SIZES, lr, betas, eps)
+        aggregate_adam_seq(S, k, events, arrays, theta, m, v, step, self.SIZES, lr, betas, eps)
+
+
+class PN1Engine(NetEngine):
+    PREFIX = "pn1"
+    MODEL = "PerformantNet1"
+    SHAPES = PN1_SHAPES
+    FLOP_PER_WORKER_STEP = 147_641_499_648          # SURVEY 8d
+    WORKSPACE = ("x0 a1 a2 d1 a3 a4 d2 a5 a6 d3 e1 e2 dh1 dh2 gx gy loss_s dlog y i1 i2 i3").split()
+
+
+class VGG11Engine(NetEngine):
+    PREFIX = "vgg11"
+    MODEL = "vgg11"
+    SHAPES = VGG11_SHAPES
+    FLOP_PER_WORKER_STEP = 117_276_672_000          # SURVEY 8d: 916,224,000 FLOP/sample x 128
+    WORKSPACE = ("x0 d1 d2 a3 d4 a5 d6 a7 f0 e1 e2 dh1 dh2 ga gb gy loss_s dlog y "
+                 "i1 i2 i4 i6 i8").split()
+
+
+ENGINES = {"PerformantNet1": PN1Engine, "vgg11": VGG11Engine}
+
+
+def engine_class(model):
+    if model not in ENGINES:
+        raise NotImplementedError(f"model {model!r}: the HIP engine implements {sorted(ENGINES)}")
+    return ENGINES[model]
+
+
+def engine_for_parameters(names):
+    """The engine class whose named_parameters layout is `names` (a models.py module)."""
+    names = list(names)
+    for cls in ENGINES.values():
+        if names == [n for n, _ in cls.SHAPES]:
+            return cls
+    raise NotImplementedError("the HIP engine implements FL.models.PerformantNet1 and vgg11")
 
 
 def aggregate_adam(S, c, stale, theta, m, v, step, sizes, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):

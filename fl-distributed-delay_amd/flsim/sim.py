@@ -20,18 +20,18 @@ import numpy as np
 import torch
 
 from .data import DevicePool, make_test_pool
-from .engine import PN1Engine, PN1_SHAPES, PN1_SIZES, padded, worker_table
+from .engine import PN1_SIZES, engine_class, padded, split_views
 from .schedule import Schedule, reference_delays
 
 SEMANTICS = ("reference", "torch1")
 
 
-def default_theta(seed=0):
-    """torch default init of PerformantNet1 under torch.manual_seed(seed) (CPU RNG, like main.py:97
-    with a seed), flattened in named_parameters order."""
-    from FL.models import PerformantNet1
+def default_theta(seed=0, model="PerformantNet1"):
+    """torch default init of the model (PerformantNet1 as main.py:97 builds it, or vgg11) under
+    torch.manual_seed(seed) (CPU RNG), flattened in named_parameters order."""
+    from FL import models
     torch.manual_seed(seed)
-    m = PerformantNet1()
+    m = models.PerformantNet1() if model == "PerformantNet1" else getattr(models, model)()
     return torch.cat([p.detach().reshape(-1) for p in m.parameters()])
 
 
@@ -39,7 +39,7 @@ class FLSimulation:
     def __init__(self, n_workers, delay=100, delays=None, throttle=False, lr=1e-3, seed=0,
                  semantics="reference", dropout=True, chunk_workers=32, device=None, theta0=None,
                  group=None, max_throttle=32, pool=None, betas=(0.9, 0.999), eps=1e-8,
-                 engine=None, device_pool=None, test_pool=None):
+                 engine=None, device_pool=None, test_pool=None, model="PerformantNet1"):
         if semantics not in SEMANTICS:
             raise NotImplementedError(f"semantics {semantics!r} (supported: {SEMANTICS})")
         self.n = int(n_workers)
@@ -54,6 +54,7 @@ class FLSimulation:
         self.semantics = semantics
         self.dropout = bool(dropout)
         self.group = group
+        self.model = model
         dist = torch.distributed
         if dist.is_available() and dist.is_initialized():
             self.rank = dist.get_rank(group)
@@ -64,7 +65,8 @@ class FLSimulation:
             torch.device("cuda", torch.cuda.current_device())
         # engine / device_pool are injectable only so tests can drive the sharding and
         # collective logic with a CPU stand-in (gloo); the product path always builds PN1Engine
-        self.engine = engine if engine is not None else PN1Engine(self.device, chunk_workers)
+        self.engine = engine if engine is not None else \
+            engine_class(model)(self.device, chunk_workers)
         self.pool = device_pool if device_pool is not None else \
             DevicePool(self.device, self.seed, pool)
         self.sched = Schedule(self.n, self.delays, self.throttle, max_throttle)
@@ -72,7 +74,7 @@ class FLSimulation:
         P = self.engine.P
         self.P = P
         self.Ppad = padded(P)
-        th = default_theta(self.seed) if theta0 is None else torch.as_tensor(theta0)
+        th = default_theta(self.seed, model) if theta0 is None else torch.as_tensor(theta0)
         self.theta = th.to(self.device, torch.float32).contiguous().clone()
         self.m = torch.zeros_like(self.theta)
         self.v = torch.zeros_like(self.theta)
@@ -135,6 +137,16 @@ class FLSimulation:
         pos = np.searchsorted(fast, sw) + np.arange(len(sw))
         return [int(x) for x in pos], None
 
+    def chunks(self, lo, hi):
+        """[lo, hi) in the fewest launches of <= chunk_workers workers, sizes within one of each
+        other (no short tail chunk running the GEMMs at low occupancy)."""
+        n = hi - lo
+        if n <= 0:
+            return []
+        k = -(-n // self.engine.chunk_workers)
+        b = [lo + (j * n) // k for j in range(k + 1)]
+        return list(zip(b[:-1], b[1:]))
+
     def shard(self, active):
         lo = (len(active) * self.rank) // self.world
         hi = (len(active) * (self.rank + 1)) // self.world
@@ -154,10 +166,8 @@ class FLSimulation:
         if self.world > 1:
             losses.zero_()
         eng.begin_epoch(self.theta)
-        cw = eng.chunk_workers
         wt = self._worker_table(t, active[lo:hi], ks)      # one async upload per epoch
-        for c0 in range(lo, hi, cw):
-            c1 = min(hi, c0 + cw)
+        for c0, c1 in self.chunks(lo, hi):
             eng.run_chunk(self.theta, self.pool, wt[c0 - lo:c1 - lo], c1 - c0, self.n, self.seed,
                           self.dropout, losses[c0:c1])
         eng.end_epoch(S)
@@ -244,9 +254,9 @@ class FLSimulation:
         """models.py PerformantNet1 state_dict (torch.save-compatible with the reference's
         main.py:98-100 / :192-194 load_state_dict / save)."""
         from collections import OrderedDict
-        from .engine import split_views
+        shapes = self.engine.SHAPES
         return OrderedDict((name, v.detach().cpu().clone())
-                           for (name, _), v in zip(PN1_SHAPES, split_views(self.theta)))
+                           for (name, _), v in zip(shapes, split_views(self.theta, shapes)))
 
     # -- checkpoint / resume ----------------------------------------------------------------------
     def checkpoint(self):
@@ -256,6 +266,7 @@ class FLSimulation:
         return {
             "format": "flsim-checkpoint-1",
             "config": {"n": self.n, "delays": torch.from_numpy(self.delays.copy()),
+                       "model": self.model,
                        "throttle": self.throttle, "seed": self.seed, "semantics": self.semantics,
                        "dropout": self.dropout, "lr": self.lr},
             "epoch": len(self.trace), "step": self.step,
@@ -278,9 +289,9 @@ class FLSimulation:
             raise ValueError("not an flsim checkpoint")
         cfg = ck["config"]
         mine = {"n": self.n, "throttle": self.throttle, "seed": self.seed,
-                "semantics": self.semantics, "dropout": self.dropout}
+                "semantics": self.semantics, "dropout": self.dropout, "model": self.model}
         for k, v in mine.items():
-            if cfg[k] != v:
+            if cfg.get(k, "PerformantNet1" if k == "model" else None) != v:
                 raise ValueError(f"checkpoint {k}={cfg[k]!r} differs from this run ({v!r})")
         if not np.array_equal(cfg["delays"].numpy(), self.delays):
             raise ValueError("checkpoint delays differ from this run")
@@ -305,8 +316,7 @@ class FLSimulation:
         return int(plan.computes.sum())
 
     def param_views(self):
-        from .engine import split_views
-        return split_views(self.theta)
+        return split_views(self.theta, self.engine.SHAPES)
 
 
 __all__ = ["FLSimulation", "default_theta", "PN1_SIZES"]

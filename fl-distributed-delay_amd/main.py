@@ -45,6 +45,8 @@ def parse(argv=None):
                    help='stale entry = S_{t-d} (torch>=2 aliasing) or zeros (torch 1.x)')
     p.add_argument('--no-dropout', action='store_true')
     p.add_argument('--chunk', type=int, default=32, help='workers per worker-batched launch')
+    p.add_argument('--model', default='PerformantNet1', choices=['PerformantNet1', 'vgg11'],
+                   help='models.py network (main.py:97 builds PerformantNet1; vgg11 = configs[4])')
     p.add_argument('--log', type=str, default=None,
                    help="JSONL scalar log ('Avg. Loss', 'Avg. Test Accuracy', 'Class 9 ...')")
     p.add_argument('--data_dir', type=str, default=None,
@@ -71,10 +73,10 @@ def main(argv=None):
         torch.distributed.init_process_group("nccl", device_id=dev)
     rank = torch.distributed.get_rank() if world > 1 else 0
     from flsim.sim import FLSimulation, default_theta
-    theta0 = default_theta(args.seed)
+    theta0 = default_theta(args.seed, args.model)
     if args.model_file is not None:                       # main.py:98-100
-        from FL.models import PerformantNet1
-        m = PerformantNet1()
+        from FL import models
+        m = getattr(models, args.model)()
         m.load_state_dict(torch.load(args.model_file, map_location="cpu", weights_only=True))
         theta0 = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
     if rank == 0:
@@ -86,7 +88,7 @@ def main(argv=None):
     sim = FLSimulation(args.n_workers, delay=args.delay, throttle=args.throttle,
                        lr=args.learning_rate, seed=args.seed, semantics=args.semantics,
                        dropout=not args.no_dropout, chunk_workers=args.chunk, device=dev,
-                       theta0=theta0, pool=pool, test_pool=test_pool)
+                       theta0=theta0, pool=pool, test_pool=test_pool, model=args.model)
     if args.resume:
         sim.restore(args.resume)
     log = open(args.log, "a" if args.resume else "w") if (args.log and rank == 0) else None

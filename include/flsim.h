@@ -86,6 +86,34 @@ int flsim_pn1_eval_pool(void* gradstate, void* workspace, int max_samples, const
                         int32_t* pred, flsim_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * VGG-11 worker-batched forward/backward (configs[4]'s larger CNN): replaces Worker.fwd_bkwd
+ * (agents.py:32-40) when the central model is models.py:101-103 vgg11() (cfg 'A': 8 conv3x3
+ * padding 1 + ReLU, 5 max-pools; classifier Dropout / Linear / ReLU twice + Linear,
+ * models.py:50-98).  Same contract, argument meaning and errors as the flsim_pn1_* entry points
+ * above; parameters flat in vgg11().named_parameters() order, P = flsim_vgg11_param_count()
+ * = 9,750,922.  The classifier's dropouts use RNG sites 6 and 7 of the Philox spec.
+ * ------------------------------------------------------------------------------------------- */
+long flsim_vgg11_param_count(void);
+long flsim_vgg11_gradstate_bytes(void);
+long flsim_vgg11_workspace_bytes(int max_samples);
+int flsim_vgg11_workspace_offset(int which, int samples, long* offset_bytes);
+int flsim_vgg11_begin_epoch(void* gradstate, const float* theta, flsim_stream_t stream);
+int flsim_vgg11_fwd_bwd_chunk(void* gradstate, void* workspace, int max_samples,
+                              const float* theta, const uint8_t* pool, const int32_t* labels,
+                              const int32_t* list_a, int len_a, const int32_t* list_b, int len_b,
+                              const float* lut, const WorkerRec* workers, int n_chunk_workers,
+                              int n_workers_total, uint64_t seed, int dropout, int backward_pass,
+                              float* worker_loss, flsim_stream_t stream);
+int flsim_vgg11_fwd_bwd_input(void* gradstate, void* workspace, int max_samples,
+                              const float* theta, const float* x, const int64_t* y, int n_samples,
+                              const WorkerRec* workers, uint64_t seed, int dropout,
+                              int backward_pass, float* worker_loss, flsim_stream_t stream);
+int flsim_vgg11_end_epoch(void* gradstate, float* grad_out, flsim_stream_t stream);
+int flsim_vgg11_eval_pool(void* gradstate, void* workspace, int max_samples, const float* theta,
+                          const uint8_t* pool, int first, int n_images, const float* lut,
+                          int32_t* pred, flsim_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
  * Fused server step: replaces Agg.rule = rule() (main.py:23-25, agents.py:43-45: per-tensor
  * torch.stack(weight_ups).mean(0)) + Central.update_model (agents.py:9-21: Adam step,
  * main.py:106).  weight_ups = c copies of S (the aliased fast entries) followed by n_stale stale

@@ -1,17 +1,23 @@
-"""PerformantNet1 + Worker.fwd_bkwd + the server step, restated on torch-CPU -- TEST INFRASTRUCTURE.
+"""The networks + Worker.fwd_bkwd + the server step, restated on torch-CPU -- TEST INFRASTRUCTURE.
 
 Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module.
 
   PerformantNet1Ref    models.py:11-25 (layer construction order => identical default init under
                        torch.manual_seed) and models.py:27-47 (forward) with dropout masks injected
                        from the build's Philox spec instead of torch's RNG
+  VGG11Ref             models.py:101-103 vgg11(): make_layers(cfg 'A') then the classifier, then
+                       the He-normal conv init of models.py:67-71 (same RNG draw order); forward
+                       models.py:73-77; the classifier's two Dropouts use Philox sites 6 and 7
   fwd_bkwd             agents.py:32-40 (forward, CrossEntropyLoss mean, backward accumulating into
                        the shared .grad, returns the loss)
   OracleSim            main.py:126-188: per-epoch worker loop (schedule from oracle.schedule),
                        aggregation rule main.py:23-25 (oracle.cascade_mean == torch stack-mean),
-                       Central.update_model agents.py:9-21 (oracle.adam_step == torch Adam)
+                       Central.update_model agents.py:9-21 (oracle.adam_step == torch Adam); the
+                       model is PerformantNet1 (main.py:97) or vgg11 (configs[4])
 """
 from __future__ import annotations
+
+import math
 
 import numpy as np
 import torch
@@ -30,6 +36,10 @@ PARAM_NAMES = [
 # NCHW shapes (per sample) at the five dropout sites, models.py:32,36,40,43,45
 DROPOUT_SHAPES = [(48, 18, 18), (96, 11, 11), (192, 7, 7), (512,), (256,)]
 
+# models.py:96-98 cfg 'A'; the classifier's Dropout() x2 (models.py:58,61): (site, p, shape)
+VGG_CFG = (64, "M", 128, "M", 256, 256, "M", 512, 512, "M", 512, 512, "M")
+VGG_DROPOUT = tuple((site, 0.5, (512,)) for site in O.SITE_VGG_DROPOUT)
+
 
 class PerformantNet1Ref(nn.Module):
     """Same parameter set and construction order as models.py:13-25."""
@@ -47,47 +57,30 @@ class PerformantNet1Ref(nn.Module):
         self.linear3 = nn.Linear(256, 10)
 
 
-def init_params(seed=0):
-    """torch default init of PerformantNet1 under torch.manual_seed(seed) -> flat fp32 numpy."""
-    torch.manual_seed(seed)
-    m = PerformantNet1Ref()
-    return torch.cat([p.detach().reshape(-1) for _, p in m.named_parameters()]).numpy().copy()
+class VGG11Ref(nn.Module):
+    """vgg11() of models.py:101-103: the feature layers are built first (models.py:80-93; each
+    Conv2d's default init draws from the RNG), then the classifier's Linears (models.py:57-65),
+    then every conv weight is redrawn N(0, sqrt(2 / (9 * out_channels))) and its bias zeroed
+    (models.py:67-71).  Parameter names match (features.0, ..., classifier.6)."""
 
-
-def param_shapes():
-    m = PerformantNet1Ref()
-    return [(n, tuple(p.shape)) for n, p in m.named_parameters()]
-
-
-SHAPES = None
-
-
-def _shapes():
-    global SHAPES
-    if SHAPES is None:
-        SHAPES = param_shapes()
-    return SHAPES
-
-
-def split_flat(flat):
-    """flat numpy/torch vector -> list of per-tensor views (named_parameters order)."""
-    out, off = [], 0
-    for _, shp in _shapes():
-        n = int(np.prod(shp))
-        out.append(flat[off:off + n].reshape(shp))
-        off += n
-    return out
-
-
-def dropout_noise(seed, t, worker, nsamples, dtype=torch.float32):
-    """The five noise tensors (keep * fp32(1/(1-p))) for one worker-step, NCHW."""
-    res = []
-    for site, p, shp in zip(O.SITE_DROPOUT, O.DROPOUT_P, DROPOUT_SHAPES):
-        numel = nsamples * int(np.prod(shp))
-        keep = O.dropout_keep(seed, t, worker, site, p, numel)
-        noise = torch.from_numpy(keep).reshape((nsamples,) + shp).to(torch.float32).div_(1 - p)
-        res.append(noise.to(dtype))
-    return res
+    def __init__(self):
+        super().__init__()
+        layers, c = [], 3
+        for v in VGG_CFG:
+            if v == "M":
+                layers.append(nn.MaxPool2d(kernel_size=2, stride=2))
+            else:
+                layers += [nn.Conv2d(c, v, kernel_size=3, padding=1), nn.ReLU(inplace=True)]
+                c = v
+        self.features = nn.Sequential(*layers)
+        self.classifier = nn.Sequential(
+            nn.Dropout(), nn.Linear(512, 512), nn.ReLU(True),
+            nn.Dropout(), nn.Linear(512, 512), nn.ReLU(True), nn.Linear(512, 10))
+        for mod in self.modules():
+            if isinstance(mod, nn.Conv2d):
+                fan = mod.kernel_size[0] * mod.kernel_size[1] * mod.out_channels
+                mod.weight.data.normal_(0, math.sqrt(2.0 / fan))
+                mod.bias.data.zero_()
 
 
 def forward(params, x, noise):
@@ -110,9 +103,88 @@ def forward(params, x, noise):
     return F.linear(h, l3w, l3b)
 
 
-def fwd_bkwd(params, x, y, noise):
+def vgg_forward(params, x, noise):
+    """models.py:73-77: make_layers' conv3x3 (padding 1) + ReLU and 2x2 max-pools
+    (models.py:80-93), flatten, classifier Dropout -> Linear -> ReLU -> Dropout -> Linear -> ReLU
+    -> Linear (models.py:57-65); dropout = x * noise (noise None -> eval mode)."""
+    convs = params[:16]
+    l1w, l1b, l2w, l2b, l3w, l3b = params[16:]
+    d = (lambda h, i: h) if noise is None else (lambda h, i: h * noise[i])
+    h, j = x, 0
+    for v in VGG_CFG:
+        if v == "M":
+            h = F.max_pool2d(h, 2, 2)
+        else:
+            h = F.relu(F.conv2d(h, convs[2 * j], convs[2 * j + 1], padding=1))
+            j += 1
+    h = h.reshape(x.shape[0], -1)
+    h = F.relu(F.linear(d(h, 0), l1w, l1b))
+    h = F.relu(F.linear(d(h, 1), l2w, l2b))
+    return F.linear(h, l3w, l3b)
+
+
+class _Net:
+    """One models.py network: module (parameter set + init), forward, and its dropout sites in
+    call order as (Philox site, p, per-sample shape)."""
+
+    def __init__(self, module, fwd, dropout):
+        self.module, self.forward, self.dropout = module, fwd, dropout
+        self._shapes = None
+
+    def shapes(self):
+        if self._shapes is None:
+            state = torch.random.get_rng_state()     # a shape probe must not move the RNG
+            self._shapes = [(n, tuple(p.shape)) for n, p in self.module().named_parameters()]
+            torch.random.set_rng_state(state)
+        return self._shapes
+
+
+NETS = {
+    "PerformantNet1": _Net(PerformantNet1Ref, forward,
+                           tuple(zip(O.SITE_DROPOUT, O.DROPOUT_P, DROPOUT_SHAPES))),
+    "vgg11": _Net(VGG11Ref, vgg_forward, VGG_DROPOUT),
+}
+
+
+def init_params(seed=0, model="PerformantNet1"):
+    """torch default init of the model under torch.manual_seed(seed) -> flat fp32 numpy."""
+    torch.manual_seed(seed)
+    m = NETS[model].module()
+    return torch.cat([p.detach().reshape(-1) for _, p in m.named_parameters()]).numpy().copy()
+
+
+def param_shapes(model="PerformantNet1"):
+    return list(NETS[model].shapes())
+
+
+def _shapes(model="PerformantNet1"):
+    return NETS[model].shapes()
+
+
+def split_flat(flat, model="PerformantNet1"):
+    """flat numpy/torch vector -> list of per-tensor views (named_parameters order)."""
+    out, off = [], 0
+    for _, shp in _shapes(model):
+        n = int(np.prod(shp))
+        out.append(flat[off:off + n].reshape(shp))
+        off += n
+    return out
+
+
+def dropout_noise(seed, t, worker, nsamples, dtype=torch.float32, model="PerformantNet1"):
+    """The model's dropout noise tensors (keep * fp32(1/(1-p))) for one worker-step, NCHW."""
+    res = []
+    for site, p, shp in NETS[model].dropout:
+        numel = nsamples * int(np.prod(shp))
+        keep = O.dropout_keep(seed, t, worker, site, p, numel)
+        noise = torch.from_numpy(keep).reshape((nsamples,) + shp).to(torch.float32).div_(1 - p)
+        res.append(noise.to(dtype))
+    return res
+
+
+def fwd_bkwd(params, x, y, noise, fwd=forward):
     """agents.py:32-40: loss = CE(mean) ; backward() accumulates into p.grad ; returns loss."""
-    pred = forward(params, x, noise)
+    pred = fwd(params, x, noise)
     loss = F.cross_entropy(pred, y)
     loss.backward()
     return loss.detach()
@@ -123,7 +195,7 @@ class OracleSim:
 
     def __init__(self, n, delay=None, delays=None, throttle=False, seed=0, dtype=torch.float32,
                  semantics="reference", dropout=True, pool=None, lr=1e-3, theta0=None,
-                 max_throttle=32):
+                 max_throttle=32, model="PerformantNet1"):
         self.n = n
         self.delays = np.asarray(delays if delays is not None else O.reference_delays(n, delay),
                                  np.int32)
@@ -134,11 +206,13 @@ class OracleSim:
         self.dropout = dropout
         self.lr = lr
         self.max_throttle = max_throttle
+        self.model = model
+        self.net = NETS[model]
         imgs, labels = pool if pool is not None else O.make_pool(seed)
         self.imgs, self.labels = imgs, labels
         self.lists = O.class_lists(labels)
         self.lut = O.normalize_lut()
-        theta0 = O_init(seed) if theta0 is None else theta0
+        theta0 = init_params(seed, model) if theta0 is None else theta0
         self.theta = np.ascontiguousarray(theta0, np.float32).copy()
         self.m = np.zeros_like(self.theta)
         self.v = np.zeros_like(self.theta)
@@ -164,12 +238,13 @@ class OracleSim:
         dt = dtype or self.dtype
         params = [torch.tensor(a, dtype=dt, requires_grad=True)
                   for a in split_flat(theta_np.astype(np.float64 if dt == torch.float64
-                                                      else np.float32))]
+                                                      else np.float32), self.model)]
         losses = []
         for (t, i, k) in items:
             x, y = self.batch(t, i, k, dt)
-            noise = dropout_noise(self.seed, t, i, x.shape[0], dt) if self.dropout else None
-            losses.append(float(fwd_bkwd(params, x, y, noise)))
+            noise = dropout_noise(self.seed, t, i, x.shape[0], dt, self.model) \
+                if self.dropout else None
+            losses.append(float(fwd_bkwd(params, x, y, noise, self.net.forward)))
         g = torch.cat([p.grad.reshape(-1) for p in params]).numpy()
         return g, losses
 
@@ -222,7 +297,7 @@ class OracleSim:
         self.ring = {src: a for src, a in self.ring.items() if src in live}
         g = np.empty_like(S)
         off = 0
-        for _, shp in _shapes():                          # rule() is per parameter tensor
+        for _, shp in _shapes(self.model):                # rule() is per parameter tensor
             nel = int(np.prod(shp))
             g[off:off + nel] = O.cascade_mean([e[off:off + nel] for e in entries])
             off += nel
@@ -240,14 +315,15 @@ def O_init(seed):
     return init_params(seed)
 
 
-def predict(theta_np, imgs_u8, batch=500):
+def predict(theta_np, imgs_u8, batch=500, model="PerformantNet1"):
     """util.py:31-45 forward in eval mode (no dropout): argmax of the logits per image (torch.max
     -> first maximum), fp32 torch CPU.  imgs_u8: [n, 3, 32, 32] uint8 pool images."""
-    params = [torch.from_numpy(a) for a in split_flat(theta_np.astype(np.float32))]
+    params = [torch.from_numpy(a) for a in split_flat(theta_np.astype(np.float32), model)]
     lut = O.normalize_lut()
+    fwd = NETS[model].forward
     out = []
     with torch.no_grad():
         for s in range(0, len(imgs_u8), batch):
             x = torch.from_numpy(lut[imgs_u8[s:s + batch]])
-            out.append(torch.max(forward(params, x, None), 1)[1].numpy())
+            out.append(torch.max(fwd(params, x, None), 1)[1].numpy())
     return np.concatenate(out).astype(np.int32)

@@ -30,6 +30,7 @@ _LIB = None
 SITE_DATA = 0x10                  # sample-slot draws
 SITE_DROPOUT = (1, 2, 3, 4, 5)    # dropout1 x3 (models.py:32,36,40), dropout2 x2 (models.py:43,45)
 DROPOUT_P = (0.25, 0.25, 0.25, 0.5, 0.5)
+SITE_VGG_DROPOUT = (6, 7)         # vgg11 classifier Dropout() x2, p = 0.5 (models.py:58,61)
 POOL_SIZE = 50000
 CLASSES_A = (0, 2, 3, 4, 5, 6, 7, 8)   # main.py:78 targets[0]
 CLASSES_B = (1, 9)                      # main.py:78 targets[1]

@@ -4,7 +4,7 @@ Run:  python tests/golden/make_golden.py   (needs /root/reference; never runs on
 
 What is executed from the reference (read-only, imported/exec'd, never copied):
   * FL/agents.py  Central / Worker / Agg          (real classes)
-  * FL/models.py  PerformantNet1                  (real module, torch default init)
+  * FL/models.py  PerformantNet1, vgg11           (real modules, their own init)
   * main.py:23-25 rule()                          (exec'd from the parsed AST)
   * main.py:126-203 the training loop `for t in tqdm(range(n_epochs)):` (exec'd from the AST)
 with stubs for the I/O the container cannot provide (main.py:8,15,70-73,141 -- torchvision,
@@ -273,13 +273,13 @@ def tensor_stats(ts):
 
 
 def train_run(n, delay, throttle, n_epochs, seed=0, dtype=torch.float32, dropout=True,
-              pool=None):
+              pool=None, model_fn=PerformantNet1, sites=O.SITE_DROPOUT):
     imgs, labels = pool
     lists = O.class_lists(labels)
     lut = O.normalize_lut()
     np.random.seed(seed)
     torch.manual_seed(seed)
-    model = PerformantNet1()
+    model = model_fn()
     theta0 = torch.cat([p.detach().reshape(-1) for p in model.parameters()]).numpy().copy()
     if dtype == torch.float64:
         model = model.double()
@@ -319,7 +319,7 @@ def train_run(n, delay, throttle, n_epochs, seed=0, dtype=torch.float32, dropout
     def spec_dropout(input, p=0.5, training=True, inplace=False):
         if not training or not dropout:
             return input
-        site = O.SITE_DROPOUT[ctx.calls]
+        site = sites[ctx.calls]
         ctx.calls += 1
         keep = O.dropout_keep(seed, ctx.t, ctx.i, site, p, input.numel())
         noise = torch.from_numpy(keep).reshape(input.shape).to(input.dtype).div_(1 - p)
@@ -423,10 +423,60 @@ def make_grad_fixture(pool):
     print("grad fixture loss", out["f32_loss"], out["f64_loss"])
 
 
+def make_vgg_fixtures(pool):
+    """configs[4]'s vgg11 (models.py:101-103), the reference's own module: init under
+    torch.manual_seed(0) (sha), one worker-step gradient through the reference Worker.fwd_bkwd
+    (f32 and f64; the classifier's two Dropouts get the spec's masks, sites 6 and 7), and a 3-epoch
+    run of the verbatim loop main.py:126-203 with the model swapped for vgg11 (f32)."""
+    from FL.models import vgg11  # noqa: E402  (reference)
+    imgs, labels = pool
+    lists = O.class_lists(labels)
+    lut = O.normalize_lut()
+    out = {}
+    for dt, tag in ((torch.float32, "f32"), (torch.float64, "f64")):
+        torch.manual_seed(0)
+        model = vgg11()
+        if dt == torch.float32:
+            theta0 = torch.cat([p.detach().reshape(-1) for p in model.parameters()]).numpy()
+            out["theta0_sha"] = np.frombuffer(bytes.fromhex(_sha(theta0)), np.uint8)
+        else:
+            model = model.double()
+        model.train()
+        idx = O.batch_indices(0, 0, 0, 0, 4, lists)
+        x = torch.from_numpy(lut[imgs[idx]]).to(dt)
+        y = torch.from_numpy(labels[idx])
+        real = F.dropout
+        calls = [0]
+
+        def spec(input, p=0.5, training=True, inplace=False):
+            site = O.SITE_VGG_DROPOUT[calls[0]]
+            calls[0] += 1
+            keep = O.dropout_keep(0, 0, 0, site, p, input.numel())
+            return input * torch.from_numpy(keep).reshape(input.shape).to(input.dtype).div_(1 - p)
+
+        torch.nn.functional.dropout = spec
+        try:
+            w = Worker(torch.nn.CrossEntropyLoss())
+            w.model = model
+            grads, lossval = w.fwd_bkwd(x, y)
+        finally:
+            torch.nn.functional.dropout = real
+        assert calls[0] == 2
+        out[f"{tag}_loss"] = np.asarray(lossval, np.float64)
+        out[f"{tag}_stats"], out[f"{tag}_samp"] = tensor_stats(grads)
+    theta0, losses, agg_log, theta_log = train_run(3, 2, True, 3, pool=pool, model_fn=vgg11,
+                                                   sites=O.SITE_VGG_DROPOUT)
+    out["train_losses"] = losses
+    for t, th in enumerate(theta_log):
+        out[f"train_theta{t}_stats"] = th[0]
+    np.savez_compressed(os.path.join(HERE, "vgg.npz"), **out)
+    print("vgg fixtures: loss", out["f32_loss"], out["f64_loss"], "train", losses)
+
+
 def main():
-    what = sys.argv[1:] or ["schedule", "cascade", "adam", "train", "grad"]
+    what = sys.argv[1:] or ["schedule", "cascade", "adam", "train", "grad", "vgg"]
     pool = None
-    if "train" in what or "grad" in what:
+    if "train" in what or "grad" in what or "vgg" in what:
         pool = O.make_pool(0)
     if "schedule" in what:
         make_schedule_fixtures()
@@ -438,6 +488,8 @@ def main():
         make_grad_fixture(pool)
     if "train" in what:
         make_train_fixtures(pool)
+    if "vgg" in what:
+        make_vgg_fixtures(pool)
     meta = dict(torch=torch.__version__, threads=torch.get_num_threads(),
                 cpu_capability=torch.backends.cpu.get_cpu_capability(),
                 numpy=np.__version__, pool_sha=_sha(pool[0]) if pool is not None else None,

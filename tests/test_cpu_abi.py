@@ -26,6 +26,7 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(L, n), n
     assert set(names) == set(_lib.EXPORTS)
     assert L.flsim_pn1_param_count() == 5596090
+    assert L.flsim_vgg11_param_count() == 9750922          # models.py:101-103 vgg11()
 
 
 def test_workspace_sizes():
@@ -33,6 +34,28 @@ def test_workspace_sizes():
     L = _lib.lib()
     assert L.flsim_pn1_workspace_bytes(4096) > 4096 * 1_500_000
     assert L.flsim_pn1_gradstate_bytes() > 0
+    assert L.flsim_vgg11_workspace_bytes(4096) > 4096 * 600_000
+    assert L.flsim_vgg11_gradstate_bytes() > 4 * 9750922
+
+
+def test_engine_layouts_match_models():
+    """The engines' flat layouts are the models' named_parameters order (FL/models.py, the
+    reference's parameter sets) and the C-ABI's parameter counts."""
+    import torch
+    from FL.models import PerformantNet1, vgg11
+    from flsim import _lib
+    from flsim.engine import PN1Engine, VGG11Engine, engine_for_parameters
+    for cls, ctor in ((PN1Engine, PerformantNet1), (VGG11Engine, vgg11)):
+        m = ctor()
+        assert [(n, tuple(p.shape)) for n, p in m.named_parameters()] == \
+            [(n, tuple(s)) for n, s in cls.SHAPES]
+        assert engine_for_parameters(n for n, _ in m.named_parameters()) is cls
+        assert getattr(_lib.lib(), f"flsim_{cls.PREFIX}_param_count")() == \
+            sum(p.numel() for p in m.parameters())
+    with pytest.raises(NotImplementedError):
+        engine_for_parameters(["fc.weight"])
+    off = ctypes.c_long()
+    assert _lib.lib().flsim_vgg11_workspace_offset(99, 128, ctypes.byref(off)) == 1
 
 
 def _parse(key):

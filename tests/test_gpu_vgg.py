@@ -1,0 +1,212 @@
+"""GPU parity of the VGG-11 engine (configs[4]; models.py:50-103, flsim_vgg11_* in
+csrc/vgg_net.hip) through the C-ABI, against the oracle's torch-CPU restatement (oracle/model_ref.py
+VGG11Ref, itself pinned to the reference's own vgg11() by tests/golden/vgg.npz).
+
+Tolerances (as tests/test_gpu_parity.py):
+  * one worker-step gradient: per-tensor rel-L2 vs fp64 <= 5e-3; whole gradient within
+    2.5e-4 of |g64| (or 4x the CPU's own fp32 error);
+  * teacher-forced (the GPU's own ReLU / argmax / dropout decisions in an fp64 reference):
+    per-tensor rel-L2 <= 2e-5, losses to 1e-5;
+  * losses |dloss| <= 1e-4 on the first step, <= 1e-3 over the first epochs; trace bit-exact.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import has_gpu
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not has_gpu(), reason="needs an MI355X")]
+
+DEV = "cuda:0"
+M = "vgg11"
+
+
+@pytest.fixture(scope="module")
+def pool():
+    from oracle import oracle as O
+    return O.make_pool(0)
+
+
+def _rel_l2(a, b):
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def _run(theta_np, items, dropout, pool, n_total=4):
+    """One chunk of len(items) worker-steps through flsim_vgg11_fwd_bwd_chunk -> S, losses."""
+    from flsim.data import DevicePool
+    from flsim.engine import VGG11Engine, worker_table
+    nw = len(items)
+    eng = VGG11Engine(DEV, chunk_workers=nw)
+    dpool = DevicePool(DEV, 0, pool)
+    theta = torch.from_numpy(theta_np.copy()).to(DEV)
+    eng.begin_epoch(theta)
+    loss = torch.zeros(nw, device=DEV)
+    eng.run_chunk(theta, dpool, worker_table(items, DEV), nw, n_total, 0, dropout, loss)
+    S = torch.zeros(eng.P, device=DEV)
+    eng.end_epoch(S)
+    torch.cuda.synchronize()
+    return eng, S.cpu().numpy().astype(np.float64), loss.cpu().numpy()
+
+
+@pytest.mark.parametrize("dropout", [False, True])
+def test_vgg_single_worker_step_gradient(pool, dropout):
+    from flsim.engine import VGG11_SHAPES
+    from oracle import model_ref as MR
+    sim = MR.OracleSim(4, delay=2, pool=pool, dropout=dropout, model=M)
+    items = [(0, 0, 0)]
+    g32, l32 = sim.grad_of(sim.theta, items)
+    g64, l64 = sim.grad_of(sim.theta, items, dtype=torch.float64)
+    _, g, loss = _run(sim.theta, items, dropout, pool)
+    assert abs(float(loss[0]) - l64[0]) <= 1e-4, (loss[0], l64[0])
+    off = 0
+    for (name, shp) in VGG11_SHAPES:
+        n = int(np.prod(shp))
+        r = _rel_l2(g[off:off + n], g64[off:off + n])
+        off += n
+        assert r <= 5e-3, (name, r)
+    e_gpu = np.linalg.norm(g - g64)
+    e_cpu = np.linalg.norm(g32.astype(np.float64) - g64)
+    assert e_gpu <= max(2.5e-4 * np.linalg.norm(g64), 4 * e_cpu), (e_gpu, e_cpu)
+
+
+@pytest.mark.parametrize("dropout,items", [
+    (False, [(0, 1, 2)]), (True, [(0, 1, 2)]), (True, [(1, 0, 3), (1, 2, 0)])])
+def test_vgg_gradient_teacher_forced_decisions(pool, dropout, items):
+    """Every backward kernel checked tightly: an fp64 reference that takes the GPU's own forward
+    decisions (ReLU signs, max-pool argmax, dropout masks, read back from the workspace) must give
+    the GPU's gradient to fp32 accumulation accuracy.  The two-item case is ONE chunk of 256
+    samples whose gradient must be the sum of the per-worker mean-CE gradients (agents.py:35)."""
+    import torch.nn.functional as F
+    from flsim.engine import VGG11_SHAPES, VGG11Engine
+    from oracle import model_ref as MR
+    from test_gpu_parity import _gather_pool
+    NS = 128 * len(items)
+    sim = MR.OracleSim(4, delay=2, pool=pool, dropout=dropout, model=M)
+    eng, g, loss = _run(sim.theta, items, dropout, pool)
+    ids = {name: j for j, name in enumerate(VGG11Engine.WORKSPACE)}
+
+    def W(name, shp, dt=torch.float32):
+        return eng.workspace_view(ids[name], shp, dt).cpu().numpy()
+
+    def nchw(a):
+        return torch.from_numpy(np.ascontiguousarray(a.transpose(0, 3, 1, 2))).double()
+
+    A = dict(d1=nchw(W("d1", (NS, 16, 16, 64))), d2=nchw(W("d2", (NS, 8, 8, 128))),
+             a3=nchw(W("a3", (NS, 8, 8, 256))), d4=nchw(W("d4", (NS, 4, 4, 256))),
+             a5=nchw(W("a5", (NS, 4, 4, 512))), d6=nchw(W("d6", (NS, 2, 2, 512))),
+             a7=nchw(W("a7", (NS, 2, 2, 512))), f0=torch.from_numpy(W("f0", (NS, 512))).double(),
+             e1=torch.from_numpy(W("e1", (NS, 512))).double(),
+             e2=torch.from_numpy(W("e2", (NS, 512))).double(),
+             i1=W("i1", (NS, 16, 16, 64), torch.uint8), i2=W("i2", (NS, 8, 8, 128), torch.uint8),
+             i4=W("i4", (NS, 4, 4, 256), torch.uint8), i6=W("i6", (NS, 2, 2, 512), torch.uint8),
+             i8=W("i8", (NS, 1, 1, 512), torch.uint8))
+    P = [torch.tensor(a, requires_grad=True)
+         for a in MR.split_flat(sim.theta.astype(np.float64), M)]
+    cw, cb = P[0:16:2], P[1:16:2]
+    l1w, l1b, l2w, l2b, l3w, l3b = P[16:]
+
+    def m(t):
+        return (t > 0).to(torch.float64)
+
+    def conv(h, j):
+        return F.conv2d(h, cw[j], cb[j], padding=1)
+
+    s50 = 2.0 if dropout else 1.0
+    lrefs = []
+    for wi, it in enumerate(items):
+        sl = slice(128 * wi, 128 * (wi + 1))
+        a = {k: v[sl] for k, v in A.items()}
+        x, y = sim.batch(*it, dtype=torch.float64)
+        h = _gather_pool(conv(x, 0), a["i1"]) * m(a["d1"])
+        h = _gather_pool(conv(h, 1), a["i2"]) * m(a["d2"])
+        h = conv(h, 2) * m(a["a3"])
+        h = _gather_pool(conv(h, 3), a["i4"]) * m(a["d4"])
+        h = conv(h, 4) * m(a["a5"])
+        h = _gather_pool(conv(h, 5), a["i6"]) * m(a["d6"])
+        h = conv(h, 6) * m(a["a7"])
+        h = _gather_pool(conv(h, 7), a["i8"]).reshape(128, 512) * m(a["f0"]) * s50
+        h = F.linear(h, l1w, l1b) * m(a["e1"]) * s50
+        h = F.linear(h, l2w, l2b) * m(a["e2"])
+        lref = F.cross_entropy(F.linear(h, l3w, l3b), y)
+        lref.backward()
+        lrefs.append(lref.item())
+    off = 0
+    worst = {}
+    for (name, _), p in zip(VGG11_SHAPES, P):
+        n = p.numel()
+        worst[name] = _rel_l2(g[off:off + n], p.grad.reshape(-1).numpy())
+        off += n
+    np.testing.assert_allclose(loss, lrefs, atol=1e-5)
+    assert max(worst.values()) <= 2e-5, worst
+
+
+def test_vgg_simulation_matches_oracle_trajectory(pool):
+    """The batched server loop with vgg11 (FLSimulation(model='vgg11')) against the oracle loop:
+    bit-exact staleness trace, losses within the fp32 tolerance."""
+    from flsim.sim import FLSimulation
+    from oracle import model_ref as MR
+    n, d, ep = 3, 2, 4
+    osim = MR.OracleSim(n, delay=d, throttle=True, pool=pool, model=M)
+    gsim = FLSimulation(n, delay=d, throttle=True, device=DEV, chunk_workers=2, pool=pool, model=M)
+    assert np.array_equal(gsim.theta.cpu().numpy(), osim.theta)
+    for t in range(ep):
+        lo = osim.epoch()
+        lg = gsim.epoch()
+        tr_o = osim.trace[-1]
+        plan = gsim.trace[-1]
+        assert [i for (_, i, _) in tr_o["items"]] == list(np.nonzero(plan.computes)[0])
+        assert [s for (k, s) in tr_o["appended"] if k == "stale"] == [s for (_, s) in plan.stale]
+        assert abs(lg - lo) <= (1e-4 if t == 0 else 1e-3), (t, lg, lo)
+
+
+def test_vgg_eval_predictions_match_oracle(pool):
+    """Device evaluation (util.py:31-45, dropout off) of vgg11 vs the oracle's fp32 forward over a
+    ragged 600-image range (chunks of 256); differences only at fp32 near-ties."""
+    from flsim.data import DevicePool, make_test_pool
+    from flsim.engine import VGG11Engine
+    from oracle import model_ref as MR
+    theta = MR.init_params(0, M)
+    test = make_test_pool(0, size=600)
+    eng = VGG11Engine(DEV, chunk_workers=2)
+    pred = eng.evaluate(torch.from_numpy(theta).to(DEV), DevicePool(DEV, 0, test)).cpu().numpy()
+    ref = MR.predict(theta, test[0], model=M)
+    assert (pred == ref).mean() >= 0.99, (pred != ref).sum()
+
+
+def test_vgg_reference_api_facade(pool):
+    """FL.agents drop-in with the reference's vgg11 module: Worker.fwd_bkwd per worker (one
+    aliased gradient buffer), Agg(rule), Central.update_model -- one epoch against the oracle."""
+    import torch.nn as nn
+    from FL.agents import Agg, Central, Worker, rule
+    from FL.models import vgg11
+    from oracle import model_ref as MR
+    from oracle import oracle as O
+    n = 3
+    osim = MR.OracleSim(n, delay=2, throttle=False, pool=pool, model=M)
+    torch.manual_seed(0)
+    model = vgg11().to(DEV)
+    central = Central(model, torch.optim.Adam(model.parameters(), lr=0.001))
+    workers = [Worker(nn.CrossEntropyLoss()) for _ in range(n)]
+    for i, w in enumerate(workers):
+        w.index = i
+    rs = np.random.RandomState(0)
+    lists = O.class_lists(pool[1])
+    lut = O.normalize_lut()
+    model.train()
+    ups, losses = [], []
+    for i in range(n):
+        k = rs.randint(0, n)
+        idx = O.batch_indices(0, 0, i, k, n, lists)
+        workers[i].model = central.model
+        g, lv = workers[i].fwd_bkwd(torch.from_numpy(lut[pool[0][idx]]).to(DEV),
+                                    torch.from_numpy(pool[1][idx]).to(DEV))
+        if i < n - 1:               # the slow worker's t == 0 entry goes to its FIFO
+            ups.append(g)
+            losses.append(lv)
+    central.update_model(Agg(rule).rule(ups))
+    lo = osim.epoch()
+    assert abs(float(np.mean(losses)) - lo) <= 1e-4, (np.mean(losses), lo)
+    th = torch.cat([p.detach().reshape(-1) for p in model.parameters()]).cpu().numpy()
+    # Adam's first step is ~lr * sign(g): near-zero gradients flip, so theta is
+    # compared loosely, as in test_gpu_parity.test_reference_api_facade_loop
+    assert _rel_l2(th.astype(np.float64), osim.theta.astype(np.float64)) < 0.03

@@ -160,3 +160,46 @@ def test_training_trajectory(golden, thr):
             ts.append([a.sum(), (a * a).sum(), a.min(), a.max()])
         np.testing.assert_allclose(np.asarray(ts)[:, 1], g[f"{key}_theta{t}_stats"][:, 1],
                                    rtol=1e-3)  # Adam amplifies 1-ulp sqrt diffs
+
+
+def _sampled(grad, model):
+    """The golden sampling of make_golden.tensor_stats: <= 256 fixed indices per tensor."""
+    off, samp = 0, []
+    for (_, shp) in MR._shapes(model):
+        n = int(np.prod(shp))
+        a = grad[off:off + n].astype(np.float64)
+        off += n
+        rs = np.random.RandomState(123 + n)
+        idx = np.arange(n) if n <= 256 else np.sort(rs.choice(n, 256, replace=False))
+        samp.append(a[idx])
+    return np.concatenate(samp)
+
+
+def test_vgg11_oracle_matches_reference(golden):
+    """configs[4]: the oracle's VGG11Ref / vgg_forward against the reference's own vgg11()
+    (models.py:50-103): identical init under torch.manual_seed(0), one worker-step gradient
+    through Worker.fwd_bkwd with the spec's classifier dropout masks (f32 and f64 runs)."""
+    g = golden.vgg
+    imgs, labels = O.make_pool(0)
+    sim = MR.OracleSim(4, delay=2, pool=(imgs, labels), model="vgg11")
+    assert _sha(sim.theta) == g["theta0_sha"].tobytes()
+    assert sim.theta.size == 9750922
+    grad, losses = sim.grad_of(sim.theta, [(0, 0, 0)])
+    assert abs(losses[0] - float(g["f32_loss"])) < 1e-6
+    np.testing.assert_allclose(_sampled(grad, "vgg11"), g["f32_samp"], rtol=1e-4, atol=1e-7)
+    g64, l64 = sim.grad_of(sim.theta, [(0, 0, 0)], dtype=torch.float64)
+    assert abs(l64[0] - float(g["f64_loss"])) < 1e-12
+    np.testing.assert_allclose(_sampled(g64, "vgg11"), g["f64_samp"], rtol=1e-9, atol=1e-13)
+
+
+def test_vgg11_oracle_trajectory(golden):
+    """3 epochs of the reference's verbatim loop with vgg11 (n=3, d=2, throttle): same losses."""
+    g = golden.vgg
+    imgs, labels = O.make_pool(0)
+    sim = MR.OracleSim(3, delay=2, throttle=True, pool=(imgs, labels), model="vgg11")
+    for t, ref in enumerate(g["train_losses"]):
+        loss = sim.epoch()
+        assert abs(loss - ref) <= 1e-5, (t, loss, ref)
+        np.testing.assert_allclose(
+            [float((a.astype(np.float64) ** 2).sum()) for a in MR.split_flat(sim.theta, "vgg11")],
+            g[f"train_theta{t}_stats"][:, 1], rtol=1e-3)
