@@ -13,6 +13,9 @@
 //   * Adam: m = fma(1-b1, g-m, m); v = fma((1-b2)*g, g, v*b2); den = sqrt(v)/sqrt(bc2) + eps;
 //     p += (-lr/bc1 * m) / den  (correctly rounded sqrt; torch CPU's sqrt is not).
 // Compiled with -ffp-contract=off: the only fused multiply-adds are the explicit ones.
+#include <stdio.h>
+#include <stdlib.h>
+
 #include "common.h"
 #include "flsim.h"
 #include "probe.h"
@@ -21,7 +24,8 @@ namespace flsim {
 
 constexpr int MAX_STALE = 8;
 constexpr int MAX_TAILS = 8;                  // tail ranges per launch (host splits longer lists)
-constexpr int MAX_EDGE = 4 * (2 * MAX_TAILS + 2);  // 256-element pieces on the element path
+constexpr int MAX_GROUPS = 4;                  // float4 groups per thread on the streaming path
+constexpr int MAX_EDGE = 4 * MAX_GROUPS * (2 * MAX_TAILS + 2);  // 256-element element-path pieces
 
 // Memoised multi_row_sum of k = c + ns rows whose first c rows are the same value x (S_t) and
 // whose last ns rows are stale entries.  ATen's cascade: 4 accumulators, level step
@@ -48,12 +52,14 @@ struct AggArgs {
     int tail_lo[MAX_TAILS];         // [lo, hi) element ranges summed with row_sum
     int tail_hi[MAX_TAILS];
     int nedge;                      // blocks 0..nedge-1: 256-element edge pieces starting at
-    long edge_lo[MAX_EDGE];         // edge_lo[b] (the 4 quarters of each edge block)
+    long edge_lo[MAX_EDGE];         // edge_lo[b] (the 4G quarters of each edge block)
+    long bspan;                     // elements per streaming block (1024 * G)
     int c, k;
     Casc main;                      // multi_row_sum over all k rows (tensor body)
     Casc rs[4];                     // row_sum: stream q = rows 4r + q, r < k / 4 (tensor tail)
     float w1, b2, w2, bc2s, rbc2s, eps, neg_ss, fk, rk;
 };
+static_assert(sizeof(AggArgs) <= 4096, "kernel argument block");
 
 template <class T>
 __device__ __forceinline__ T seq_sum(T v, int n) {
@@ -211,7 +217,7 @@ __device__ __forceinline__ bool in_tail(const AggArgs& A, long e) {
 }
 
 __device__ __forceinline__ bool block_touch(const AggArgs& A, long blo) {
-    const long bhi = blo + 1024;
+    const long bhi = blo + A.bspan;
     bool touch = blo < A.lo || bhi > A.hi;
 #pragma unroll
     for (int t = 0; t < MAX_TAILS; ++t)
@@ -224,8 +230,10 @@ __device__ __forceinline__ bool block_touch(const AggArgs& A, long blo) {
 // elements; they start first and overlap the stream.  The other blocks are the streaming path, one thread per
 // aligned float4 group; a streaming block that is also an edge block returns at once.
 // LP: 4 = the level step of every k < 2^20, 0 = read at run time.  NSR: stale entries held in
-// registers by the streaming path (1 covers the reference's single slow worker).
-template <int LP, int NSR>
+// registers by the streaming path (1 covers the reference's single slow worker).  G: float4
+// groups per thread (a block streams 1024 G elements; every load of all G groups is issued
+// before the arithmetic).  NT: non-temporal loads / stores (each byte is touched once).
+template <int LP, int NSR, int G, bool NT>
 __global__ void __launch_bounds__(256) k_aggregate_adam(AggArgs A) {
     if ((int)blockIdx.x < A.nedge) {
         // edge piece: 256 elements, one per thread, every load issued before the arithmetic
@@ -244,30 +252,75 @@ __global__ void __launch_bounds__(256) k_aggregate_adam(AggArgs A) {
         A.v[e] = v;
         return;
     }
-    const long blo = 4 * (A.g0 + (long)(blockIdx.x - A.nedge) * 256);
+    const long blo = 4 * (A.g0 + (long)(blockIdx.x - A.nedge) * 256 * G);
     if (block_touch(A, blo)) return;
-    const long e0 = blo + 4 * threadIdx.x;
-    const f32x4 xs = *reinterpret_cast<const f32x4*>(A.S + e0);
-    f32x4 ys[NSR];
+    auto ld = [](const float* ptr) -> f32x4 {
+        if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(ptr));
+        else return *reinterpret_cast<const f32x4*>(ptr);
+    };
+    auto st = [](float* ptr, f32x4 val) {
+        if constexpr (NT) __builtin_nontemporal_store(val, reinterpret_cast<f32x4*>(ptr));
+        else *reinterpret_cast<f32x4*>(ptr) = val;
+    };
+    f32x4 xs[G], ys[G][NSR], p[G], m[G], v[G];
 #pragma unroll
-    for (int q = 0; q < NSR; ++q)
-        ys[q] = (q < A.main.ns && A.stale[q]) ? *reinterpret_cast<const f32x4*>(A.stale[q] + e0)
-                                              : f32x4{0.f, 0.f, 0.f, 0.f};
-    f32x4 p = *reinterpret_cast<const f32x4*>(A.p + e0);
-    f32x4 m = *reinterpret_cast<const f32x4*>(A.m + e0);
-    f32x4 v = *reinterpret_cast<const f32x4*>(A.v + e0);
-    const f32x4 sum = multi_row_sum_regs4<LP, NSR>(xs, ys, A.main);
+    for (int g = 0; g < G; ++g) {
+        const long e0 = blo + 1024 * g + 4 * threadIdx.x;
+        xs[g] = ld(A.S + e0);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        float pp = p[u], mm = m[u], vv = v[u];
-        adam_elem(A, sum[u], pp, mm, vv);
-        p[u] = pp;
-        m[u] = mm;
-        v[u] = vv;
+        for (int q = 0; q < NSR; ++q)
+            ys[g][q] = (q < A.main.ns && A.stale[q]) ? ld(A.stale[q] + e0)
+                                                     : f32x4{0.f, 0.f, 0.f, 0.f};
+        p[g] = ld(A.p + e0);
+        m[g] = ld(A.m + e0);
+        v[g] = ld(A.v + e0);
     }
-    *reinterpret_cast<f32x4*>(A.p + e0) = p;
-    *reinterpret_cast<f32x4*>(A.m + e0) = m;
-    *reinterpret_cast<f32x4*>(A.v + e0) = v;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const long e0 = blo + 1024 * g + 4 * threadIdx.x;
+        const f32x4 sum = multi_row_sum_regs4<LP, NSR>(xs[g], ys[g], A.main);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            float pp = p[g][u], mm = m[g][u], vv = v[g][u];
+            adam_elem(A, sum[u], pp, mm, vv);
+            p[g][u] = pp;
+            m[g][u] = mm;
+            v[g][u] = vv;
+        }
+        st(A.p + e0, p[g]);
+        st(A.m + e0, m[g]);
+        st(A.v + e0, v[g]);
+    }
+}
+
+// streaming-path shape: float4 groups per thread and non-temporal access.  Default measured on
+// MI355X inside the training step (tools/agg_instep.sh, theta/m/v/S cold in HBM): G=1 with
+// non-temporal access 27.6 us, plain 29.0 us, G=2 28.5 us, G=4 29.8 us.  (Warm, back-to-back
+// in tools/agg_bench.py the plain form is faster: 25.3 vs 26.5 us.)  FLSIM_AGG_VARIANT="G,NT"
+// overrides the default for tuning.
+struct AggVariant {
+    int groups;
+    bool nt;
+};
+static AggVariant agg_variant() {
+    static AggVariant v = [] {
+        AggVariant d{1, true};
+        if (const char* s = getenv("FLSIM_AGG_VARIANT")) {
+            int g = 1, nt = 0;
+            if (sscanf(s, "%d,%d", &g, &nt) >= 1 && (g == 1 || g == 2 || g == 4)) d = {g, nt != 0};
+        }
+        return d;
+    }();
+    return v;
+}
+
+template <int LP, int NSR>
+static auto pick_kernel(AggVariant v) {
+    auto k = k_aggregate_adam<LP, NSR, 1, false>;
+    if (v.groups == 2) k = v.nt ? k_aggregate_adam<LP, NSR, 2, true> : k_aggregate_adam<LP, NSR, 2, false>;
+    else if (v.groups == 4) k = v.nt ? k_aggregate_adam<LP, NSR, 4, true> : k_aggregate_adam<LP, NSR, 4, false>;
+    else if (v.nt) k = k_aggregate_adam<LP, NSR, 1, true>;
+    return k;
 }
 
 // host: memo constants of a multi_row_sum over k rows, the first c of them copies of x
@@ -375,24 +428,27 @@ int flsim_aggregate_adam(const float* S, int c, const float* const* stale, int n
         A.lo = lo;
         A.hi = hi;
         A.g0 = lo / 4;
+        const AggVariant var = agg_variant();
+        const long G = var.groups;
+        A.bspan = 1024 * G;
         const long groups = (hi + 3) / 4 - A.g0;
-        const long nblk = (groups + 255) / 256;
+        const long nblk = (groups + 256 * G - 1) / (256 * G);
         // edge blocks: the first and last block when they cross the launch range, and every
         // block holding a tail range (host copy of block_touch)
         A.nedge = 0;
         auto add_block = [&](long b) {
-            const long blo = 4 * (A.g0 + b * 256);
-            for (int j = 0; j < A.nedge; j += 4)
+            const long blo = 4 * (A.g0 + b * 256 * G);
+            for (int j = 0; j < A.nedge; j += 4 * G)
                 if (A.edge_lo[j] == blo) return;
-            for (int j = 0; j < 4; ++j) A.edge_lo[A.nedge++] = blo + 256 * j;
+            for (int j = 0; j < 4 * G; ++j) A.edge_lo[A.nedge++] = blo + 256 * j;
         };
         for (long b : {0L, nblk - 1}) {
-            const long blo = 4 * (A.g0 + b * 256);
-            if (blo < A.lo || blo + 1024 > A.hi) add_block(b);
+            const long blo = 4 * (A.g0 + b * 256 * G);
+            if (blo < A.lo || blo + A.bspan > A.hi) add_block(b);
         }
         for (int j = 0; j < A.ntail; ++j) {
-            const long b0 = (A.tail_lo[j] / 4 - A.g0) / 256;
-            const long b1 = ((A.tail_hi[j] - 1) / 4 - A.g0) / 256;
+            const long b0 = (A.tail_lo[j] / 4 - A.g0) / (256 * G);
+            const long b1 = ((A.tail_hi[j] - 1) / 4 - A.g0) / (256 * G);
             for (long b = b0; b <= b1; ++b) add_block(b);
         }
         const dim3 grid((unsigned)(nblk + A.nedge));
@@ -406,8 +462,8 @@ int flsim_aggregate_adam(const float* S, int c, const float* const* stale, int n
         const double bytes = 4.0 * (double)(hi - lo) * (7 + distinct);
         const ProbeSlot ps = probe_begin();
         const bool lp4 = A.main.lp == 4, ns1 = n_stale <= 1;
-        auto kern = lp4 ? (ns1 ? k_aggregate_adam<4, 1> : k_aggregate_adam<4, MAX_STALE>)
-                        : (ns1 ? k_aggregate_adam<0, 1> : k_aggregate_adam<0, MAX_STALE>);
+        auto kern = lp4 ? (ns1 ? pick_kernel<4, 1>(var) : pick_kernel<4, MAX_STALE>(var))
+                        : (ns1 ? pick_kernel<0, 1>(var) : pick_kernel<0, MAX_STALE>(var));
         hipExtLaunchKernelGGL(kern, grid, dim3(256), 0, stream, ps.start, ps.stop, 0, A);
         FLSIM_LAUNCH_CHECK();
         if (probe_end(ps, K_AGG, bytes)) return 2;
