@@ -1,5 +1,6 @@
 // fp32 MFMA GEMM core for gfx950 (v_mfma_f32_16x16x4_f32), LDS-tiled, register-staged
-// double buffer, one barrier per 16-deep K step.
+// double buffer (loads issued a full k-step ahead of their LDS write), one barrier per 16-deep
+// K step.
 //
 // C[m][n] = sum_k A[m][k] * B[k][n]; each operand is produced by a Loader that knows the
 // implicit-GEMM address math (im2col for convolutions, plain rows for the linear layers) and
@@ -134,19 +135,30 @@ gemm_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, int t
     f32x4 rb[BL::UNITS];
     constexpr int BUF = A_FL + B_FL;
 
+    // Staging pipeline: the registers hold the NEXT tile's loads for a whole k-step.  At the top
+    // of step ks (after the barrier that ended step ks-1, so nobody still reads that buffer) the
+    // tile ks+1 loaded during step ks-1 is written to the other LDS buffer and the loads of tile
+    // ks+2 are issued at once; the MFMAs of step ks then hide their latency.
     if (ks0 < ks1) {
         al.load(ks0, ra);
         bl.load(ks0, rb);
         al.store(lds, ra);
         bl.store(lds + A_FL, rb);
+        if (ks0 + 1 < ks1) {
+            al.load(ks0 + 1, ra);
+            bl.load(ks0 + 1, rb);
+        }
     }
     __syncthreads();
     int cur = 0;
     for (int ks = ks0; ks < ks1; ++ks) {
-        const bool more = ks + 1 < ks1;
-        if (more) {
-            al.load(ks + 1, ra);
-            bl.load(ks + 1, rb);
+        if (ks + 1 < ks1) {
+            al.store(lds + (cur ^ 1) * BUF, ra);
+            bl.store(lds + (cur ^ 1) * BUF + A_FL, rb);
+            if (ks + 2 < ks1) {
+                al.load(ks + 2, ra);
+                bl.load(ks + 2, rb);
+            }
         }
         const float* A = lds + cur * BUF;
         const float* B = A + A_FL;
@@ -170,10 +182,6 @@ gemm_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, int t
             for (int i = 0; i < FM; ++i)
 #pragma unroll
                 for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(af[i][kk], bf[j][kk], acc[i][j]);
-        if (more) {
-            al.store(lds + (cur ^ 1) * BUF, ra);
-            bl.store(lds + (cur ^ 1) * BUF + A_FL, rb);
-        }
         __syncthreads();
         cur ^= 1;
     }
