@@ -8,6 +8,11 @@ Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import 
   VGG11Ref             models.py:101-103 vgg11(): make_layers(cfg 'A') then the classifier, then
                        the He-normal conv init of models.py:67-71 (same RNG draw order); forward
                        models.py:73-77; the classifier's two Dropouts use Philox sites 6 and 7
+  VGG11BNRef           models.py:106-108 vgg11_bn(): make_layers(cfg 'A', batch_norm=True) -- Conv2d,
+                       BatchNorm2d, ReLU per conv (models.py:88-89); BatchNorm in train mode uses
+                       the batch statistics of each fwd_bkwd call (one worker's 128 samples) and
+                       updates running_mean / running_var (momentum 0.1, unbiased var) on every
+                       call, in worker order; eval mode (util.py:31-45) normalises with them
   fwd_bkwd             agents.py:32-40 (forward, CrossEntropyLoss mean, backward accumulating into
                        the shared .grad, returns the loss)
   OracleSim            main.py:126-188: per-epoch worker loop (schedule from oracle.schedule),
@@ -83,6 +88,57 @@ class VGG11Ref(nn.Module):
                 mod.bias.data.zero_()
 
 
+class VGG11BNRef(nn.Module):
+    """vgg11_bn() of models.py:106-108: as VGG11Ref with a BatchNorm2d(v) after every conv
+    (models.py:88-89; weight 1, bias 0, no RNG draw).  Parameter names match (features.0,
+    features.1, features.4, ...)."""
+
+    def __init__(self):
+        super().__init__()
+        layers, c = [], 3
+        for v in VGG_CFG:
+            if v == "M":
+                layers.append(nn.MaxPool2d(kernel_size=2, stride=2))
+            else:
+                layers += [nn.Conv2d(c, v, kernel_size=3, padding=1), nn.BatchNorm2d(v),
+                           nn.ReLU(inplace=True)]
+                c = v
+        self.features = nn.Sequential(*layers)
+        self.classifier = nn.Sequential(
+            nn.Dropout(), nn.Linear(512, 512), nn.ReLU(True),
+            nn.Dropout(), nn.Linear(512, 512), nn.ReLU(True), nn.Linear(512, 10))
+        for mod in self.modules():
+            if isinstance(mod, nn.Conv2d):
+                fan = mod.kernel_size[0] * mod.kernel_size[1] * mod.out_channels
+                mod.weight.data.normal_(0, math.sqrt(2.0 / fan))
+                mod.bias.data.zero_()
+
+
+VGG_BN_CHANNELS = tuple(v for v in VGG_CFG if v != "M")
+
+
+class BNState:
+    """The BatchNorm2d buffers of vgg11_bn (running_mean, running_var per layer, one
+    num_batches_tracked counter for all of them) and the module mode (train / eval)."""
+
+    def __init__(self, dtype=torch.float32):
+        self.training = True
+        self.bufs = [(torch.zeros(c, dtype=dtype), torch.ones(c, dtype=dtype))
+                     for c in VGG_BN_CHANNELS]
+        self.num_batches_tracked = 0
+
+    def flat(self):
+        """[rm_0, rv_0, rm_1, rv_1, ...] (the engine's running-buffer layout) as float64 numpy."""
+        return torch.cat([torch.cat([rm, rv]) for rm, rv in self.bufs]).double().numpy()
+
+    def load_flat(self, a, dtype=torch.float32):
+        a = torch.as_tensor(np.asarray(a)).to(dtype)
+        off = 0
+        for j, c in enumerate(VGG_BN_CHANNELS):
+            self.bufs[j] = (a[off:off + c].clone(), a[off + c:off + 2 * c].clone())
+            off += 2 * c
+
+
 def forward(params, x, noise):
     """models.py:27-47 with dropout = x * noise (noise None -> eval mode / dropout off)."""
     (w1, b1, w2, b2, w3, b3, w4, b4, w5, b5, w6, b6, l1w, l1b, l2w, l2b, l3w, l3b) = params
@@ -123,6 +179,33 @@ def vgg_forward(params, x, noise):
     return F.linear(h, l3w, l3b)
 
 
+def vgg_bn_forward(params, x, noise, bn=None):
+    """models.py:73-77 for vgg11_bn: conv3x3 -> BatchNorm2d -> ReLU (models.py:88-89), pools and
+    the classifier as vgg_forward.  bn: BNState (train mode: batch statistics of x, running
+    buffers updated in place, counter += 1; eval mode: normalise with the running buffers);
+    None = train mode without running buffers (gradient-only probes)."""
+    convs = params[:32]
+    l1w, l1b, l2w, l2b, l3w, l3b = params[32:]
+    d = (lambda h, i: h) if noise is None else (lambda h, i: h * noise[i])
+    training = bn is None or bn.training
+    h, j = x, 0
+    for v in VGG_CFG:
+        if v == "M":
+            h = F.max_pool2d(h, 2, 2)
+        else:
+            cw, cb, gw, gb = convs[4 * j:4 * j + 4]
+            h = F.conv2d(h, cw, cb, padding=1)
+            rm, rv = bn.bufs[j] if bn is not None else (None, None)
+            h = F.relu(F.batch_norm(h, rm, rv, gw, gb, training, 0.1, 1e-5))
+            j += 1
+    if bn is not None and training:
+        bn.num_batches_tracked += 1
+    h = h.reshape(x.shape[0], -1)
+    h = F.relu(F.linear(d(h, 0), l1w, l1b))
+    h = F.relu(F.linear(d(h, 1), l2w, l2b))
+    return F.linear(h, l3w, l3b)
+
+
 class _Net:
     """One models.py network: module (parameter set + init), forward, and its dropout sites in
     call order as (Philox site, p, per-sample shape)."""
@@ -143,7 +226,9 @@ NETS = {
     "PerformantNet1": _Net(PerformantNet1Ref, forward,
                            tuple(zip(O.SITE_DROPOUT, O.DROPOUT_P, DROPOUT_SHAPES))),
     "vgg11": _Net(VGG11Ref, vgg_forward, VGG_DROPOUT),
+    "vgg11_bn": _Net(VGG11BNRef, vgg_bn_forward, VGG_DROPOUT),
 }
+HAS_BN = {"vgg11_bn"}
 
 
 def init_params(seed=0, model="PerformantNet1"):
@@ -208,6 +293,7 @@ class OracleSim:
         self.max_throttle = max_throttle
         self.model = model
         self.net = NETS[model]
+        self.bn = BNState(dtype) if model in HAS_BN else None
         imgs, labels = pool if pool is not None else O.make_pool(seed)
         self.imgs, self.labels = imgs, labels
         self.lists = O.class_lists(labels)
@@ -233,9 +319,18 @@ class OracleSim:
         dt = dtype or self.dtype
         return torch.from_numpy(x).to(dt), torch.from_numpy(y)
 
-    def grad_of(self, theta_np, items, dtype=None):
-        """Sum over `items` [(t, i, k)] of per-worker mean-CE gradients at theta (in order)."""
+    def grad_of(self, theta_np, items, dtype=None, bn=None):
+        """Sum over `items` [(t, i, k)] of per-worker mean-CE gradients at theta (in order).
+        BatchNorm models: bn = a BNState to run the forwards against (train mode, buffers
+        updated), False = batch statistics only, None = the simulation's own buffers (when dtype
+        is the simulation's)."""
         dt = dtype or self.dtype
+        if self.bn is not None and bn is None:
+            bn = self.bn if dt == self.dtype else False
+        fwd = self.net.forward
+        if self.bn is not None:
+            st = bn if bn else None
+            fwd = lambda p, x, noise: vgg_bn_forward(p, x, noise, st)   # noqa: E731
         params = [torch.tensor(a, dtype=dt, requires_grad=True)
                   for a in split_flat(theta_np.astype(np.float64 if dt == torch.float64
                                                       else np.float32), self.model)]
@@ -244,7 +339,7 @@ class OracleSim:
             x, y = self.batch(t, i, k, dt)
             noise = dropout_noise(self.seed, t, i, x.shape[0], dt, self.model) \
                 if self.dropout else None
-            losses.append(float(fwd_bkwd(params, x, y, noise, self.net.forward)))
+            losses.append(float(fwd_bkwd(params, x, y, noise, fwd)))
         g = torch.cat([p.grad.reshape(-1) for p in params]).numpy()
         return g, losses
 
@@ -315,15 +410,23 @@ def O_init(seed):
     return init_params(seed)
 
 
-def predict(theta_np, imgs_u8, batch=500, model="PerformantNet1"):
+def predict(theta_np, imgs_u8, batch=500, model="PerformantNet1", bn=None):
     """util.py:31-45 forward in eval mode (no dropout): argmax of the logits per image (torch.max
     -> first maximum), fp32 torch CPU.  imgs_u8: [n, 3, 32, 32] uint8 pool images."""
     params = [torch.from_numpy(a) for a in split_flat(theta_np.astype(np.float32), model)]
     lut = O.normalize_lut()
     fwd = NETS[model].forward
+    if model in HAS_BN:              # eval mode: the running buffers (bn: BNState or flat array)
+        st = bn if isinstance(bn, BNState) else BNState()
+        if not isinstance(bn, BNState) and bn is not None:
+            st.load_flat(bn)
+        was, st.training = st.training, False
+        fwd = lambda p, x, noise: vgg_bn_forward(p, x, noise, st)   # noqa: E731
     out = []
     with torch.no_grad():
         for s in range(0, len(imgs_u8), batch):
             x = torch.from_numpy(lut[imgs_u8[s:s + batch]])
             out.append(torch.max(fwd(params, x, None), 1)[1].numpy())
+    if model in HAS_BN:
+        st.training = was
     return np.concatenate(out).astype(np.int32)

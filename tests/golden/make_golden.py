@@ -4,7 +4,7 @@ Run:  python tests/golden/make_golden.py   (needs /root/reference; never runs on
 
 What is executed from the reference (read-only, imported/exec'd, never copied):
   * FL/agents.py  Central / Worker / Agg          (real classes)
-  * FL/models.py  PerformantNet1, vgg11           (real modules, their own init)
+  * FL/models.py  PerformantNet1, vgg11, vgg11_bn (real modules, their own init)
   * main.py:23-25 rule()                          (exec'd from the parsed AST)
   * main.py:126-203 the training loop `for t in tqdm(range(n_epochs)):` (exec'd from the AST)
 with stubs for the I/O the container cannot provide (main.py:8,15,70-73,141 -- torchvision,
@@ -273,7 +273,7 @@ def tensor_stats(ts):
 
 
 def train_run(n, delay, throttle, n_epochs, seed=0, dtype=torch.float32, dropout=True,
-              pool=None, model_fn=PerformantNet1, sites=O.SITE_DROPOUT):
+              pool=None, model_fn=PerformantNet1, sites=O.SITE_DROPOUT, keep=None):
     imgs, labels = pool
     lists = O.class_lists(labels)
     lut = O.normalize_lut()
@@ -362,6 +362,8 @@ def train_run(n, delay, throttle, n_epochs, seed=0, dtype=torch.float32, dropout
         F.dropout = real_dropout
         torch.nn.functional.dropout = real_dropout
     losses = np.array([v for (tag, v, t) in writer.scalars if tag == "Avg. Loss"], np.float64)
+    if keep is not None:
+        keep["model"] = model
     return theta0, losses, agg_log, theta_log
 
 
@@ -473,10 +475,83 @@ def make_vgg_fixtures(pool):
     print("vgg fixtures: loss", out["f32_loss"], out["f64_loss"], "train", losses)
 
 
+def _bn_buffers(model):
+    """running_mean, running_var of every BatchNorm2d in order, concatenated per layer
+    [rm_0, rv_0, rm_1, rv_1, ...] (float64), and the layers' num_batches_tracked."""
+    flat, nbt = [], []
+    for mod in model.modules():
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            flat += [mod.running_mean.double(), mod.running_var.double()]
+            nbt.append(int(mod.num_batches_tracked))
+    return torch.cat(flat).numpy(), np.asarray(nbt, np.int64)
+
+
+def make_vgg_bn_fixtures(pool):
+    """vgg11_bn (models.py:106-108), the reference's own module: init sha; one worker-step
+    through the reference Worker.fwd_bkwd in train mode (f32 and f64: gradient stats + samples,
+    the BatchNorm running buffers after the call); a 3-epoch run of the verbatim loop
+    main.py:126-203 with the model swapped for vgg11_bn (losses, per-epoch parameter stats, the
+    final running buffers) and the final model's eval-mode logits on 64 test images (util.py:31-45
+    after central.model.eval(), main.py:190)."""
+    from FL.models import vgg11_bn  # noqa: E402  (reference)
+    imgs, labels = pool
+    lists = O.class_lists(labels)
+    lut = O.normalize_lut()
+    out = {}
+    for dt, tag in ((torch.float32, "f32"), (torch.float64, "f64")):
+        torch.manual_seed(0)
+        model = vgg11_bn()
+        if dt == torch.float32:
+            theta0 = torch.cat([p.detach().reshape(-1) for p in model.parameters()]).numpy()
+            out["theta0_sha"] = np.frombuffer(bytes.fromhex(_sha(theta0)), np.uint8)
+        else:
+            model = model.double()
+        model.train()
+        idx = O.batch_indices(0, 0, 0, 0, 4, lists)
+        x = torch.from_numpy(lut[imgs[idx]]).to(dt)
+        y = torch.from_numpy(labels[idx])
+        real = F.dropout
+        calls = [0]
+
+        def spec(input, p=0.5, training=True, inplace=False):
+            site = O.SITE_VGG_DROPOUT[calls[0]]
+            calls[0] += 1
+            keep = O.dropout_keep(0, 0, 0, site, p, input.numel())
+            return input * torch.from_numpy(keep).reshape(input.shape).to(input.dtype).div_(1 - p)
+
+        torch.nn.functional.dropout = spec
+        try:
+            w = Worker(torch.nn.CrossEntropyLoss())
+            w.model = model
+            grads, lossval = w.fwd_bkwd(x, y)
+        finally:
+            torch.nn.functional.dropout = real
+        assert calls[0] == 2
+        out[f"{tag}_loss"] = np.asarray(lossval, np.float64)
+        out[f"{tag}_stats"], out[f"{tag}_samp"] = tensor_stats(grads)
+        out[f"{tag}_running"], _ = _bn_buffers(model)
+    keep = {}
+    theta0, losses, agg_log, theta_log = train_run(3, 2, True, 3, pool=pool, model_fn=vgg11_bn,
+                                                   sites=O.SITE_VGG_DROPOUT, keep=keep)
+    model = keep["model"]
+    out["train_losses"] = losses
+    for t, th in enumerate(theta_log):
+        out[f"train_theta{t}_stats"] = th[0]
+    out["train_theta_stats"], out["train_theta_samp"] = tensor_stats(list(model.parameters()))
+    out["train_running"], out["train_nbt"] = _bn_buffers(model)
+    timgs, _ = O.make_test_pool(0)
+    model.eval()
+    with torch.no_grad():
+        out["eval_logits"] = model(torch.from_numpy(lut[timgs[:64]])).double().numpy()
+    np.savez_compressed(os.path.join(HERE, "vgg_bn.npz"), **out)
+    print("vgg_bn fixtures: loss", out["f32_loss"], out["f64_loss"], "train", losses,
+          "nbt", out["train_nbt"])
+
+
 def main():
-    what = sys.argv[1:] or ["schedule", "cascade", "adam", "train", "grad", "vgg"]
+    what = sys.argv[1:] or ["schedule", "cascade", "adam", "train", "grad", "vgg", "vgg_bn"]
     pool = None
-    if "train" in what or "grad" in what or "vgg" in what:
+    if "train" in what or "grad" in what or "vgg" in what or "vgg_bn" in what:
         pool = O.make_pool(0)
     if "schedule" in what:
         make_schedule_fixtures()
@@ -490,6 +565,8 @@ def main():
         make_train_fixtures(pool)
     if "vgg" in what:
         make_vgg_fixtures(pool)
+    if "vgg_bn" in what:
+        make_vgg_bn_fixtures(pool)
     meta = dict(torch=torch.__version__, threads=torch.get_num_threads(),
                 cpu_capability=torch.backends.cpu.get_cpu_capability(),
                 numpy=np.__version__, pool_sha=_sha(pool[0]) if pool is not None else None,

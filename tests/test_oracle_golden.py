@@ -203,3 +203,65 @@ def test_vgg11_oracle_trajectory(golden):
         np.testing.assert_allclose(
             [float((a.astype(np.float64) ** 2).sum()) for a in MR.split_flat(sim.theta, "vgg11")],
             g[f"train_theta{t}_stats"][:, 1], rtol=1e-3)
+
+
+def test_vgg11_bn_oracle_matches_reference(golden):
+    """vgg11_bn (models.py:106-108): the oracle's VGG11BNRef / vgg_bn_forward against the
+    reference's own module -- identical init, one worker-step gradient through Worker.fwd_bkwd in
+    train mode (batch statistics of the worker's 128 samples), and the BatchNorm running buffers
+    that call leaves behind (momentum 0.1, unbiased variance)."""
+    g = golden.vgg_bn
+    imgs, labels = O.make_pool(0)
+    sim = MR.OracleSim(4, delay=2, pool=(imgs, labels), model="vgg11_bn")
+    assert _sha(sim.theta) == g["theta0_sha"].tobytes()
+    assert sim.theta.size == 9756426
+    grad, losses = sim.grad_of(sim.theta, [(0, 0, 0)])
+    assert abs(losses[0] - float(g["f32_loss"])) < 1e-6
+    assert sim.bn.num_batches_tracked == 1
+    np.testing.assert_allclose(sim.bn.flat(), g["f32_running"], rtol=1e-5, atol=1e-7)
+    # conv biases before a BatchNorm get a gradient that is zero up to rounding: compare with
+    # an absolute tolerance at the scale of the other entries
+    np.testing.assert_allclose(_sampled(grad, "vgg11_bn"), g["f32_samp"], rtol=1e-3, atol=1e-7)
+    bn64 = MR.BNState(torch.float64)
+    g64, l64 = sim.grad_of(sim.theta, [(0, 0, 0)], dtype=torch.float64, bn=bn64)
+    assert abs(l64[0] - float(g["f64_loss"])) < 1e-12
+    np.testing.assert_allclose(_sampled(g64, "vgg11_bn"), g["f64_samp"], rtol=1e-9, atol=1e-13)
+    np.testing.assert_allclose(bn64.flat(), g["f64_running"], rtol=1e-12, atol=1e-15)
+
+
+def _check_running(got, ref, rm_atol=2e-4, rv_rtol=1e-5):
+    """running_var within rv_rtol; running_mean within rm_atol absolute.  A conv bias in front of
+    a BatchNorm cancels in the normalisation, so its gradient is rounding noise of a zero sum;
+    Adam turns that noise into +-lr steps, and the bias enters running_mean directly.  After a
+    few epochs two correct implementations differ there by O(lr * epochs * momentum)."""
+    off = 0
+    for c in MR.VGG_BN_CHANNELS:
+        np.testing.assert_allclose(got[off:off + c], ref[off:off + c], rtol=0, atol=rm_atol)
+        np.testing.assert_allclose(got[off + c:off + 2 * c], ref[off + c:off + 2 * c],
+                                   rtol=rv_rtol, atol=1e-7)
+        off += 2 * c
+
+
+def test_vgg11_bn_oracle_trajectory_and_eval(golden):
+    """3 epochs of the reference's verbatim loop with vgg11_bn (n=3, d=2, throttle): losses,
+    parameter norms, the running buffers after every computing worker's forward (in worker
+    order), num_batches_tracked, and the eval-mode logits of the final model (util.py:31-45)."""
+    g = golden.vgg_bn
+    imgs, labels = O.make_pool(0)
+    sim = MR.OracleSim(3, delay=2, throttle=True, pool=(imgs, labels), model="vgg11_bn")
+    for t, ref in enumerate(g["train_losses"]):
+        loss = sim.epoch()
+        assert abs(loss - ref) <= 1e-5, (t, loss, ref)
+        np.testing.assert_allclose(
+            [float((a.astype(np.float64) ** 2).sum())
+             for a in MR.split_flat(sim.theta, "vgg11_bn")][2::4],     # BatchNorm weights
+            g[f"train_theta{t}_stats"][2::4, 1], rtol=1e-4)
+    assert sim.bn.num_batches_tracked == int(g["train_nbt"][0])
+    _check_running(sim.bn.flat(), g["train_running"])
+    timgs, _ = O.make_test_pool(0)
+    params = [torch.from_numpy(a) for a in MR.split_flat(sim.theta, "vgg11_bn")]
+    sim.bn.training = False
+    with torch.no_grad():
+        logits = MR.vgg_bn_forward(params, torch.from_numpy(O.normalize_lut()[timgs[:64]]), None,
+                                   sim.bn)
+    np.testing.assert_allclose(logits.double().numpy(), g["eval_logits"], rtol=1e-3, atol=1e-4)
