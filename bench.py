@@ -62,9 +62,10 @@ def parse():
                     help="reference: one slow worker (n-1) with --delay; heterogeneous: configs[3] "
                          "spec (10%% slow workers, geometric delays up to 1000)")
     ap.add_argument("--chunk", type=int, default=32, help="workers per worker-batched launch")
-    ap.add_argument("--model", choices=["PerformantNet1", "vgg11"], default="PerformantNet1",
-                    help="PerformantNet1 (main.py:97, the metric's model) or vgg11 (configs[4]: "
-                         "--model vgg11 --n_workers 4096 --delay 1000)")
+    ap.add_argument("--model", choices=["PerformantNet1", "vgg11", "vgg11_bn"],
+                    default="PerformantNet1",
+                    help="PerformantNet1 (main.py:97, the metric's model), vgg11 (configs[4]: "
+                         "--model vgg11 --n_workers 4096 --delay 1000) or vgg11_bn")
     ap.add_argument("--cpu-sample", type=int, default=160,
                     help="worker-steps in the CPU sample (~10-30 s of host work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -13,8 +13,11 @@ Same classes, signatures and aliasing semantics; the arithmetic runs in libflsim
                                with the optimizer's lr/betas/eps); parameters live in one flat
                                device buffer, model.parameters() are views of it
 
-Requirements (raise otherwise): the model is FL.models.PerformantNet1 or FL.models.vgg11() on a
-HIP device, the optimizer is torch.optim.Adam without weight decay / amsgrad / maximize, batches
+vgg11_bn(): the module's BatchNorm running_mean / running_var alias the engine's device buffer;
+every train-mode fwd_bkwd call advances them (and num_batches_tracked) as nn.BatchNorm2d does.
+
+Requirements (raise otherwise): the model is FL.models.PerformantNet1, vgg11() or vgg11_bn() on
+a HIP device (vgg11_bn: train mode, 128-sample batches = one BatchNorm batch per call), the optimizer is torch.optim.Adam without weight decay / amsgrad / maximize, batches
 are multiples of 128 samples.  There is no CPU fallback.
 """
 from __future__ import annotations
@@ -49,7 +52,12 @@ class _ModelContext:
             p.data = view                       # parameters alias the flat buffer
         self.m = torch.zeros_like(self.theta)
         self.v = torch.zeros_like(self.theta)
+        self.model = model
         self.engine = self.engine_cls(dev, chunk_workers=1)
+        self.bn_stats = None
+        if self.engine.STATS_PER_WORKER:
+            self._alias_buffers(model)
+            self.bn_stats = torch.zeros(self.engine.STATS_PER_WORKER, device=dev)
         self.seed = seed
         self.t = 0               # epoch counter (dropout RNG key)
         self.G = None            # flat gradient buffer of the current epoch (p.grad views)
@@ -57,10 +65,28 @@ class _ModelContext:
         self.step = 0
         self.loss_buf = torch.zeros(64, device=dev)
 
+    def _alias_buffers(self, model):
+        """BatchNorm running buffers become views of the engine's device buffer (loaded from the
+        module first, e.g. after main.py:99 load_state_dict)."""
+        bns = [mod for mod in model.modules() if isinstance(mod, torch.nn.BatchNorm2d)]
+        views = self.engine.running_views()
+        assert len(bns) == len(views)
+        for mod, (_, rm, rv) in zip(bns, views):
+            rm.copy_(mod.running_mean.detach().reshape(-1))
+            rv.copy_(mod.running_var.detach().reshape(-1))
+            mod.running_mean.data = rm
+            mod.running_var.data = rv
+        self.engine.num_batches_tracked = int(bns[0].num_batches_tracked)
+        self.bns = bns
+
     def ensure_capacity(self, n_samples):
         cw = n_samples // 128
         if cw > self.engine.chunk_workers:
+            old = self.engine
             self.engine = self.engine_cls(self.device, chunk_workers=cw)
+            if old.STATS_PER_WORKER:        # the running buffers stay where the module sees them
+                self.engine.running = old.running
+                self.engine.num_batches_tracked = old.num_batches_tracked
             self.packed = False
         if cw > self.loss_buf.numel():
             self.loss_buf = torch.zeros(cw, device=self.device)
@@ -186,8 +212,18 @@ class Worker:
         recs = [(ctx.t, self.index, 0)] * (n // 128)
         wt = worker_table(recs, ctx.device)
         lb = ctx.loss_buf[:n // 128]
+        kw = {}
+        if ctx.bn_stats is not None:
+            if not self.model.training or n != 128:
+                raise NotImplementedError("vgg11_bn: the HIP engine runs BatchNorm in train mode "
+                                          "on 128-sample batches (main.py:43-44, 132)")
+            kw = {"stats_out": ctx.bn_stats}
         eng.run_input(theta, inp.to(ctx.device, torch.float32), outp.to(ctx.device), wt,
-                      ctx.seed, self.model.training, lb)
+                      ctx.seed, self.model.training, lb, **kw)
+        if ctx.bn_stats is not None:             # nn.BatchNorm2d's running update, this call
+            eng.update_running(ctx.bn_stats, 1)
+            for mod in ctx.bns:
+                mod.num_batches_tracked.fill_(eng.num_batches_tracked)
         eng.end_epoch(ctx.G)                     # running sum of the epoch's gradients
         grads = split_views(ctx.G[:ctx.P], ctx.shapes)
         for p, gv in zip(self.model.parameters(), grads):

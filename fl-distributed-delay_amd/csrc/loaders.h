@@ -244,6 +244,21 @@ struct Im2colKM {
 // ---------------------------------------------------------------------------------------------
 // Epilogues
 // ---------------------------------------------------------------------------------------------
+// conv forward without activation: Y[m][n] = acc + bias[n]  (vgg11_bn: the BatchNorm input)
+struct EpiBias {
+    static constexpr bool ASUM = false;
+    float* Y;
+    const float* bias;
+    int M, N;
+    __device__ void apply4(int m, int n, int z, f32x4 v) const {
+        if (n >= N) return;
+        const float b = bias[n];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (m + r < M) Y[(long)(m + r) * N + n] = v[r] + b;
+    }
+};
+
 // conv forward: Y[m][n] = relu(acc + bias[n])  (NHWC, row length N)
 struct EpiBiasRelu {
     static constexpr bool ASUM = false;

@@ -13,7 +13,13 @@
 // Each conv + ReLU (+ pool) is one fused MFMA launch (pooled layers: GEMM rows in pool-window
 // order, argmax kept for the backward); the classifier's first Dropout is fused into conv8's pool
 // epilogue.  Activations NHWC fp32.
-#include "net_kernels.h"
+//
+// vgg11_bn (models.py:106-108: Conv2d -> BatchNorm2d -> ReLU per conv, models.py:88-89) shares
+// every launch above except the conv epilogue: the conv writes z = conv + bias, the per-worker
+// batch statistics of z are reduced (bn_kernels.h), and one streaming pass applies the
+// normalisation + ReLU (+ pool / dropout).  The backward turns the masked gradient of each
+// BatchNorm output into dz in place before the conv's weight / data gradients.
+#include "bn_kernels.h"
 
 namespace flsim {
 
@@ -35,12 +41,18 @@ constexpr int VFEAT = 512;   // classifier width
 constexpr int VZL = 16;      // classifier weight-gradient splits
 constexpr int VZH = 32;      // head weight-gradient splits
 
+// vgg11_bn: per-call statistics of the 8 BatchNorms, [mean | unbiased var] per layer
+// (the running-buffer layout: running_mean, running_var of features.1, .5, .9, ... in order)
+constexpr int BN_RUN_OFF[8] = {0, 128, 384, 896, 1408, 2432, 3456, 4480};
+constexpr int BN_NSTAT = 5504;
+
 // flat parameter offsets in named_parameters order: features.{0,3,6,8,11,13,16,18}.{weight,bias},
-// classifier.{1,4,6}.{weight,bias}
+// classifier.{1,4,6}.{weight,bias}; vgg11_bn: conv {weight, bias} then BatchNorm {weight, bias}
+// per layer (features.{0,1}, {4,5}, {8,9}, {11,12}, {15,16}, {18,19}, {22,23}, {25,26})
 struct VOff {
-    long w[8], b[8], l1w, l1b, l2w, l2b, l3w, l3b, total;
+    long w[8], b[8], g[8], be[8], l1w, l1b, l2w, l2b, l3w, l3b, total;
 };
-static VOff voff() {
+static VOff voff(bool bn = false) {
     VOff o;
     long p = 0;
     for (int l = 0; l < 8; ++l) {
@@ -48,6 +60,13 @@ static VOff voff() {
         p += (long)VG[l].CO * VG[l].CI * 9;
         o.b[l] = p;
         p += VG[l].CO;
+        o.g[l] = o.be[l] = -1;
+        if (bn) {
+            o.g[l] = p;
+            p += VG[l].CO;
+            o.be[l] = p;
+            p += VG[l].CO;
+        }
     }
     o.l1w = p; p += (long)VFEAT * VFEAT;
     o.l1b = p; p += VFEAT;
@@ -66,11 +85,12 @@ struct VGrad {
     float* sw[8];   // [ZW][CO][KP]
     float* sb[8];   // [ZW][CO]
     float *l1w, *l1b, *l2w, *l2b, *l3w, *l3b;
+    float* bnacc[8];   // vgg11_bn: epoch sums of the BatchNorm [weight | bias] gradients
     float* slab_begin;
     long slab_floats, total_floats;
 };
 
-static VGrad vgs_layout(float* base) {
+static VGrad vgs_layout(float* base, bool bn = false) {
     VGrad g;
     long o = 0;
     auto take = [&](long n) {
@@ -94,6 +114,7 @@ static VGrad vgs_layout(float* base) {
     g.l2b = take((long)VZL * VFEAT);
     g.l3w = take((long)VZH * 10 * VFEAT);
     g.l3b = take((long)VZH * 10);
+    for (int l = 0; l < 8; ++l) g.bnacc[l] = bn ? take(2L * VG[l].CO) : nullptr;
     g.slab_floats = o - slab0;
     g.total_floats = o;
     return g;
@@ -107,10 +128,12 @@ struct VWS {
     float *ga, *gb, *gy, *loss_s, *dlog;
     int32_t* y;
     uint8_t *i1, *i2, *i4, *i6, *i8;
+    // vgg11_bn: z = conv + bias per layer, per-(worker, channel) mean / invstd, scratch
+    float *z[8], *bmean[8], *binv[8], *pa, *pb, *cm, *ck, *dg, *db;
     long bytes;
 };
 
-static VWS vws_layout(char* base, int S) {
+static VWS vws_layout(char* base, int S, bool bn = false) {
     VWS w;
     long o = 0;
     auto take = [&](long bytes) {
@@ -145,46 +168,127 @@ static VWS vws_layout(char* base, int S) {
     w.i4 = tb(4 * 4 * 256);
     w.i6 = tb(2 * 2 * 512);
     w.i8 = tb(VFEAT);
+    for (int l = 0; l < 8; ++l) w.z[l] = w.bmean[l] = w.binv[l] = nullptr;
+    w.pa = w.pb = w.cm = w.ck = w.dg = w.db = nullptr;
+    if (bn) {
+        const int W = S / SAMPLES_PER_WORKER;
+        for (int l = 0; l < 8; ++l) {
+            w.z[l] = tf((long)VG[l].H * VG[l].H * VG[l].CO);
+            w.bmean[l] = (float*)take(4L * (W > 0 ? W : 1) * VG[l].CO);
+            w.binv[l] = (float*)take(4L * (W > 0 ? W : 1) * VG[l].CO);
+        }
+        w.pa = tf(256);     // W * NS * C = 256 * S floats at most (bn_kernels.h)
+        w.pb = tf(256);
+        w.cm = (float*)take(4L * (W > 0 ? W : 1) * 512);
+        w.ck = (float*)take(4L * (W > 0 ? W : 1) * 512);
+        w.dg = (float*)take(4L * (W > 0 ? W : 1) * 512);
+        w.db = (float*)take(4L * (W > 0 ? W : 1) * 512);
+    }
     w.bytes = o;
     return w;
 }
 
-static int vpack(const VGrad& g, const float* th, hipStream_t st) {
-    const VOff o = voff();
+static int vpack(const VGrad& g, const float* th, const VOff& o, hipStream_t st) {
     for (int l = 0; l < 8; ++l)
         RC(pack_conv(th + o.w[l], g.wf[l], g.wd[l], VG[l].CO, VG[l].CI, VG[l].CIP, VG[l].KP, st));
     return 0;
 }
 
+// vgg11_bn forward mode: train (batch statistics of every worker's 128 samples; per-call
+// statistics for the running buffers into stats[worker][BN_NSTAT] unless null) or eval (the
+// per-channel coefficients of the running buffers, vbn_eval_coef)
+struct VBN {
+    const VWS* w;
+    int train;
+    float* stats;
+};
+
+// conv (z = conv + bias) -> BatchNorm -> ReLU (-> 2x2 max-pool (-> dropout)) of layer l
+template <int H, int CIP, int CO, int FM, int FN, int WM, int WN, bool POOL>
+static int vbn_conv(const VBN& bn, int l, const float* X, int S, const VGrad& g, const float* th,
+                    const VOff& o, float* out, uint8_t* idx, const WorkerRec* workers,
+                    uint64_t seed, uint32_t site, int dropout, hipStream_t st, int kid,
+                    int kreal) {
+    const VWS& w = *bn.w;
+    RC((conv_like<H, H, CIP, 1, FM, FN, WM, WN>(X, S, g.wf[l], CO, VG[l].KP,
+        EpiBias{w.z[l], th + o.b[l], S * H * H, CO}, st, kid, kreal)));
+    if (bn.train)
+        RC((bn_forward_stats<H, CO>(w.z[l], S, w.bmean[l], w.binv[l], w.pa, w.pb, bn.stats,
+                                    BN_RUN_OFF[l], BN_NSTAT, st)));
+    if constexpr (POOL)
+        return bn_apply_pool<H, CO>(w.z[l], S, w.bmean[l], w.binv[l], th + o.g[l], th + o.be[l],
+                                    bn.train, out, idx, workers, seed, site, THR_P50, SCALE_P50,
+                                    dropout, st);
+    else
+        return bn_apply<H, CO>(w.z[l], S, w.bmean[l], w.binv[l], th + o.g[l], th + o.be[l],
+                               bn.train, out, st);
+}
+
+// eval mode: mean / invstd of every BatchNorm from the running buffers
+static int vbn_eval_coef(const VWS& w, const float* running, hipStream_t st) {
+    for (int l = 0; l < 8; ++l) {
+        const int C = VG[l].CO;
+        hipLaunchKernelGGL(k_bn_eval_coef, dim3(ceil_div(C, 256)), dim3(256), 0, st,
+                           running + BN_RUN_OFF[l], running + BN_RUN_OFF[l] + C, C, w.bmean[l],
+                           w.binv[l]);
+        FLSIM_LAUNCH_CHECK();
+    }
+    return 0;
+}
+
 // models.py:73-77 (features, flatten, classifier) up to the last ReLU; the head follows
-static int vforward(const VGrad& g, const VWS& w, const float* th, int S, const WorkerRec* workers,
-                    uint64_t seed, int dropout, hipStream_t st) {
-    const VOff o = voff();
-    // conv1 + ReLU + pool (features.0-2)
-    RC((conv_pool_fwd<32, 32, 4, 64, 1, 2, 4, 4, 1, false>(w.x0, S, g.wf[0], 48, w.d1, w.i1,
-        th + o.b[0], workers, seed, 0, 0, 1.f, 0, st, K_VF1, 27)));
-    // conv2 + ReLU + pool (features.3-5)
-    RC((conv_pool_fwd<16, 16, 64, 128, 1, 4, 4, 2, 2, false>(w.d1, S, g.wf[1], 576, w.d2, w.i2,
-        th + o.b[1], workers, seed, 0, 0, 1.f, 0, st, K_VF2, 576)));
-    // conv3 + ReLU (features.6-7)
-    RC((conv_like<8, 8, 128, 1, 4, 4, 2, 2>(w.d2, S, g.wf[2], 256, 1152,
-        EpiBiasRelu{w.a3, th + o.b[2], S * 64, 256}, st, K_VF3, 1152)));
-    // conv4 + ReLU + pool (features.8-10)
-    RC((conv_pool_fwd<8, 8, 256, 256, 1, 4, 4, 2, 2, false>(w.a3, S, g.wf[3], 2304, w.d4, w.i4,
-        th + o.b[3], workers, seed, 0, 0, 1.f, 0, st, K_VF4, 2304)));
-    // conv5 + ReLU (features.11-12)
-    RC((conv_like<4, 4, 256, 1, 4, 4, 2, 2>(w.d4, S, g.wf[4], 512, 2304,
-        EpiBiasRelu{w.a5, th + o.b[4], S * 16, 512}, st, K_VF5, 2304)));
-    // conv6 + ReLU + pool (features.13-15)
-    RC((conv_pool_fwd<4, 4, 512, 512, 1, 4, 4, 2, 2, false>(w.a5, S, g.wf[5], 4608, w.d6, w.i6,
-        th + o.b[5], workers, seed, 0, 0, 1.f, 0, st, K_VF6, 4608)));
-    // conv7 + ReLU (features.16-17)
-    RC((conv_like<2, 2, 512, 1, 4, 4, 2, 2>(w.d6, S, g.wf[6], 512, 4608,
-        EpiBiasRelu{w.a7, th + o.b[6], S * 4, 512}, st, K_VF7, 4608)));
-    // conv8 + ReLU + pool (features.18-20) + classifier Dropout (models.py:58): the 1x1 pooled map
-    // is the flattened feature vector
-    RC((conv_pool_fwd<2, 2, 512, 512, 1, 4, 4, 2, 2, false>(w.a7, S, g.wf[7], 4608, w.f0, w.i8,
-        th + o.b[7], workers, seed, SITE_VDROP1, THR_P50, SCALE_P50, dropout, st, K_VF8, 4608)));
+template <bool BN>
+static int vforward(const VGrad& g, const VWS& w, const float* th, const VOff& o, int S,
+                    const WorkerRec* workers, uint64_t seed, int dropout, const VBN* bn,
+                    hipStream_t st) {
+    if constexpr (BN) {
+        // features.{0-3}, {4-7}, {8-10}, {11-14}, {15-17}, {18-21}, {22-24}, {25-28}
+        RC((vbn_conv<32, 4, 64, 2, 4, 4, 1, true>(*bn, 0, w.x0, S, g, th, o, w.d1, w.i1, workers,
+                                                  seed, 0, 0, st, K_VF1, 27)));
+        RC((vbn_conv<16, 64, 128, 4, 4, 2, 2, true>(*bn, 1, w.d1, S, g, th, o, w.d2, w.i2,
+                                                    workers, seed, 0, 0, st, K_VF2, 576)));
+        RC((vbn_conv<8, 128, 256, 4, 4, 2, 2, false>(*bn, 2, w.d2, S, g, th, o, w.a3, nullptr,
+                                                     workers, seed, 0, 0, st, K_VF3, 1152)));
+        RC((vbn_conv<8, 256, 256, 4, 4, 2, 2, true>(*bn, 3, w.a3, S, g, th, o, w.d4, w.i4,
+                                                    workers, seed, 0, 0, st, K_VF4, 2304)));
+        RC((vbn_conv<4, 256, 512, 4, 4, 2, 2, false>(*bn, 4, w.d4, S, g, th, o, w.a5, nullptr,
+                                                     workers, seed, 0, 0, st, K_VF5, 2304)));
+        RC((vbn_conv<4, 512, 512, 4, 4, 2, 2, true>(*bn, 5, w.a5, S, g, th, o, w.d6, w.i6,
+                                                    workers, seed, 0, 0, st, K_VF6, 4608)));
+        RC((vbn_conv<2, 512, 512, 4, 4, 2, 2, false>(*bn, 6, w.d6, S, g, th, o, w.a7, nullptr,
+                                                     workers, seed, 0, 0, st, K_VF7, 4608)));
+        // + classifier Dropout (models.py:58) on the flattened 1x1 pooled map
+        RC((vbn_conv<2, 512, 512, 4, 4, 2, 2, true>(*bn, 7, w.a7, S, g, th, o, w.f0, w.i8,
+                                                    workers, seed, SITE_VDROP1, dropout, st,
+                                                    K_VF8, 4608)));
+    } else {
+        // conv1 + ReLU + pool (features.0-2)
+        RC((conv_pool_fwd<32, 32, 4, 64, 1, 2, 4, 4, 1, false>(w.x0, S, g.wf[0], 48, w.d1, w.i1,
+            th + o.b[0], workers, seed, 0, 0, 1.f, 0, st, K_VF1, 27)));
+        // conv2 + ReLU + pool (features.3-5)
+        RC((conv_pool_fwd<16, 16, 64, 128, 1, 4, 4, 2, 2, false>(w.d1, S, g.wf[1], 576, w.d2,
+            w.i2, th + o.b[1], workers, seed, 0, 0, 1.f, 0, st, K_VF2, 576)));
+        // conv3 + ReLU (features.6-7)
+        RC((conv_like<8, 8, 128, 1, 4, 4, 2, 2>(w.d2, S, g.wf[2], 256, 1152,
+            EpiBiasRelu{w.a3, th + o.b[2], S * 64, 256}, st, K_VF3, 1152)));
+        // conv4 + ReLU + pool (features.8-10)
+        RC((conv_pool_fwd<8, 8, 256, 256, 1, 4, 4, 2, 2, false>(w.a3, S, g.wf[3], 2304, w.d4,
+            w.i4, th + o.b[3], workers, seed, 0, 0, 1.f, 0, st, K_VF4, 2304)));
+        // conv5 + ReLU (features.11-12)
+        RC((conv_like<4, 4, 256, 1, 4, 4, 2, 2>(w.d4, S, g.wf[4], 512, 2304,
+            EpiBiasRelu{w.a5, th + o.b[4], S * 16, 512}, st, K_VF5, 2304)));
+        // conv6 + ReLU + pool (features.13-15)
+        RC((conv_pool_fwd<4, 4, 512, 512, 1, 4, 4, 2, 2, false>(w.a5, S, g.wf[5], 4608, w.d6,
+            w.i6, th + o.b[5], workers, seed, 0, 0, 1.f, 0, st, K_VF6, 4608)));
+        // conv7 + ReLU (features.16-17)
+        RC((conv_like<2, 2, 512, 1, 4, 4, 2, 2>(w.d6, S, g.wf[6], 512, 4608,
+            EpiBiasRelu{w.a7, th + o.b[6], S * 4, 512}, st, K_VF7, 4608)));
+        // conv8 + ReLU + pool (features.18-20) + classifier Dropout (models.py:58): the 1x1
+        // pooled map is the flattened feature vector
+        RC((conv_pool_fwd<2, 2, 512, 512, 1, 4, 4, 2, 2, false>(w.a7, S, g.wf[7], 4608, w.f0,
+            w.i8, th + o.b[7], workers, seed, SITE_VDROP1, THR_P50, SCALE_P50, dropout, st,
+            K_VF8, 4608)));
+    }
     // Linear + ReLU + Dropout (models.py:59-61)
     RC((linear_fwd<4, 4, 2, 2>(w.f0, th + o.l1w, w.part, S, VFEAT, VFEAT, 1, st, K_VL1F)));
     RC(linear_finish(w.part, 1, th + o.l1b, w.e1, S, VFEAT, workers, seed, SITE_VDROP2, THR_P50,
@@ -195,10 +299,20 @@ static int vforward(const VGrad& g, const VWS& w, const float* th, int S, const 
     return 0;
 }
 
+// vgg11_bn: gradient wrt BatchNorm l's output (mask applied) -> dz in place
+template <bool BN, int H, int C>
+static int vbn_back(const VGrad& g, const VWS& w, const float* th, const VOff& o, int l,
+                    float* dy, int S, hipStream_t st) {
+    if constexpr (BN)
+        return bn_backward<H, C>(dy, w.z[l], S, w.bmean[l], w.binv[l], th + o.g[l], w.pa, w.pb,
+                                 w.cm, w.ck, w.dg, w.db, g.bnacc[l], st);
+    return 0;
+}
+
 // backward from the head's dlog / dh2 (gradient wrt linear2's pre-activation)
-static int vbackward(const VGrad& g, const VWS& w, const float* th, int S, int dropout,
-                     hipStream_t st) {
-    const VOff o = voff();
+template <bool BN>
+static int vbackward(const VGrad& g, const VWS& w, const float* th, const VOff& o, int S,
+                     int dropout, hipStream_t st) {
     const float s50 = dropout ? SCALE_P50 : 1.f;
     // Linear(512,10) weight / bias
     RC(head_wgrad<VFEAT>(w.dlog, w.e2, g.l3w, g.l3b, S, VZH, st));
@@ -212,107 +326,111 @@ static int vbackward(const VGrad& g, const VWS& w, const float* th, int S, int d
     RC((linear_dgrad<4, 4, 2, 2>(w.dh1, th + o.l1w, w.gy, w.f0, s50, S, VFEAT, VFEAT, st,
                                  K_VL1D)));
     RC((pool_scatter<2, 2, 512, false>(w.gy, w.i8, w.ga, S, st)));
+    RC((vbn_back<BN, 2, 512>(g, w, th, o, 7, w.ga, S, st)));
     // conv8: wgrad (input a7), dgrad -> dz7 = . * (a7 > 0)
     RC((conv_wgrad<2, 2, 512, 1, 4, 4, 2, 2>(w.ga, w.a7, S, 512, 4608, g.sw[7], g.sb[7], VG[7].ZW,
                                             st, K_VWG8, 4608)));
     RC((conv_like<2, 2, 512, 1, 4, 4, 2, 2>(w.ga, S, g.wd[7], 512, 4608,
         EpiMask<true>{w.gb, w.a7, S * 4, 512}, st, K_VDG8, 4608)));
+    RC((vbn_back<BN, 2, 512>(g, w, th, o, 6, w.gb, S, st)));
     // conv7: wgrad (input d6), dgrad -> gradient wrt d6 (d6 > 0), pool scatter -> dz6
     RC((conv_wgrad<2, 2, 512, 1, 4, 4, 2, 2>(w.gb, w.d6, S, 512, 4608, g.sw[6], g.sb[6], VG[6].ZW,
                                             st, K_VWG7, 4608)));
     RC((conv_like<2, 2, 512, 1, 4, 4, 2, 2>(w.gb, S, g.wd[6], 512, 4608,
         EpiDropMask{w.gy, w.d6, 1.f, S * 4, 512}, st, K_VDG7, 4608)));
     RC((pool_scatter<4, 4, 512, false>(w.gy, w.i6, w.ga, S, st)));
+    RC((vbn_back<BN, 4, 512>(g, w, th, o, 5, w.ga, S, st)));
     // conv6: wgrad (input a5), dgrad -> dz5 = . * (a5 > 0)
     RC((conv_wgrad<4, 4, 512, 1, 4, 4, 2, 2>(w.ga, w.a5, S, 512, 4608, g.sw[5], g.sb[5], VG[5].ZW,
                                             st, K_VWG6, 4608)));
     RC((conv_like<4, 4, 512, 1, 4, 4, 2, 2>(w.ga, S, g.wd[5], 512, 4608,
         EpiMask<true>{w.gb, w.a5, S * 16, 512}, st, K_VDG6, 4608)));
+    RC((vbn_back<BN, 4, 512>(g, w, th, o, 4, w.gb, S, st)));
     // conv5: wgrad (input d4), dgrad -> gradient wrt d4, pool scatter -> dz4
     RC((conv_wgrad<4, 4, 256, 1, 4, 4, 2, 2>(w.gb, w.d4, S, 512, 2304, g.sw[4], g.sb[4], VG[4].ZW,
                                             st, K_VWG5, 2304)));
     RC((conv_like<4, 4, 512, 1, 4, 4, 2, 2>(w.gb, S, g.wd[4], 256, 4608,
         EpiDropMask{w.gy, w.d4, 1.f, S * 16, 256}, st, K_VDG5, 4608)));
     RC((pool_scatter<8, 8, 256, false>(w.gy, w.i4, w.ga, S, st)));
+    RC((vbn_back<BN, 8, 256>(g, w, th, o, 3, w.ga, S, st)));
     // conv4: wgrad (input a3), dgrad -> dz3 = . * (a3 > 0)
     RC((conv_wgrad<8, 8, 256, 1, 4, 4, 2, 2>(w.ga, w.a3, S, 256, 2304, g.sw[3], g.sb[3], VG[3].ZW,
                                             st, K_VWG4, 2304)));
     RC((conv_like<8, 8, 256, 1, 4, 4, 2, 2>(w.ga, S, g.wd[3], 256, 2304,
         EpiMask<true>{w.gb, w.a3, S * 64, 256}, st, K_VDG4, 2304)));
+    RC((vbn_back<BN, 8, 256>(g, w, th, o, 2, w.gb, S, st)));
     // conv3: wgrad (input d2), dgrad -> gradient wrt d2, pool scatter -> dz2
     RC((conv_wgrad<8, 8, 128, 1, 4, 4, 2, 2>(w.gb, w.d2, S, 256, 1152, g.sw[2], g.sb[2], VG[2].ZW,
                                             st, K_VWG3, 1152)));
     RC((conv_like<8, 8, 256, 1, 4, 4, 2, 2>(w.gb, S, g.wd[2], 128, 2304,
         EpiDropMask{w.gy, w.d2, 1.f, S * 64, 128}, st, K_VDG3, 2304)));
     RC((pool_scatter<16, 16, 128, false>(w.gy, w.i2, w.ga, S, st)));
+    RC((vbn_back<BN, 16, 128>(g, w, th, o, 1, w.ga, S, st)));
     // conv2: wgrad (input d1), dgrad -> gradient wrt d1, pool scatter -> dz1
     RC((conv_wgrad<16, 16, 64, 1, 4, 4, 2, 2>(w.ga, w.d1, S, 128, 576, g.sw[1], g.sb[1], VG[1].ZW,
                                              st, K_VWG2, 576)));
     RC((conv_like<16, 16, 128, 1, 2, 4, 4, 1>(w.ga, S, g.wd[1], 64, 1152,
         EpiDropMask{w.gy, w.d1, 1.f, S * 256, 64}, st, K_VDG2, 1152)));
     RC((pool_scatter<32, 32, 64, false>(w.gy, w.i1, w.ga, S, st)));
+    RC((vbn_back<BN, 32, 64>(g, w, th, o, 0, w.ga, S, st)));
     // conv1: wgrad (input x0)
     RC((conv_wgrad<32, 32, 4, 1, 4, 3, 1, 1>(w.ga, w.x0, S, 64, 48, g.sw[0], g.sb[0], VG[0].ZW, st,
                                             K_VWG1, 27)));
     return 0;
 }
 
+template <bool BN>
 static int vrun_chunk(void* gradstate, const VWS& w, const float* theta, const WorkerRec* workers,
                       int n_chunk_workers, uint64_t seed, int dropout, int backward_pass,
-                      float* worker_loss, hipStream_t stream) {
+                      float* worker_loss, float* bn_stats, hipStream_t stream) {
     const int S = n_chunk_workers * SAMPLES_PER_WORKER;
-    const VOff o = voff();
-    VGrad g = vgs_layout((float*)gradstate);
-    RC(vforward(g, w, theta, S, workers, seed, dropout, stream));
+    const VOff o = voff(BN);
+    VGrad g = vgs_layout((float*)gradstate, BN);
+    const VBN bn{&w, 1, bn_stats};
+    RC(vforward<BN>(g, w, theta, o, S, workers, seed, dropout, &bn, stream));
     // Linear(512,10) + CrossEntropyLoss (models.py:64, main.py:107); no dropout after the ReLU
     RC(head_and_loss<VFEAT>(w.e2, theta + o.l3w, theta + o.l3b, w.y, w.loss_s, w.dlog, w.dh2, S,
                             backward_pass, 1.f, worker_loss, stream));
-    if (backward_pass) RC(vbackward(g, w, theta, S, dropout, stream));
+    if (backward_pass) RC(vbackward<BN>(g, w, theta, o, S, dropout, stream));
     return 0;
 }
 
-}  // namespace flsim
-
-using namespace flsim;
-
-// =============================================================================================
-// C-ABI (declared in include/flsim.h): the flsim_pn1_* contract for vgg11()
-// =============================================================================================
-extern "C" {
-
-long flsim_vgg11_param_count(void) { return voff().total; }
-
-long flsim_vgg11_gradstate_bytes(void) { return vgs_layout(nullptr).total_floats * 4; }
-
-long flsim_vgg11_workspace_bytes(int max_samples) { return vws_layout(nullptr, max_samples).bytes; }
-
-int flsim_vgg11_workspace_offset(int which, int samples, long* offset_bytes) {
+// ---- the C-ABI bodies, shared by vgg11 (BN = false) and vgg11_bn ----------------------------
+template <bool BN>
+static int vgg_workspace_offset(int which, int samples, long* offset_bytes) {
     char* const fake = reinterpret_cast<char*>(4096);   // layout only; never dereferenced
-    VWS w = vws_layout(fake, samples);
+    VWS w = vws_layout(fake, samples, BN);
     const void* p[] = {w.x0, w.d1, w.d2, w.a3, w.d4, w.a5, w.d6, w.a7, w.f0, w.e1, w.e2, w.dh1,
                        w.dh2, w.ga, w.gb, w.gy, w.loss_s, w.dlog, w.y, w.i1, w.i2, w.i4, w.i6,
-                       w.i8};
+                       w.i8,
+                       w.z[0], w.z[1], w.z[2], w.z[3], w.z[4], w.z[5], w.z[6], w.z[7],
+                       w.bmean[0], w.bmean[1], w.bmean[2], w.bmean[3], w.bmean[4], w.bmean[5],
+                       w.bmean[6], w.bmean[7],
+                       w.binv[0], w.binv[1], w.binv[2], w.binv[3], w.binv[4], w.binv[5],
+                       w.binv[6], w.binv[7]};
+    const int n = BN ? (int)(sizeof(p) / sizeof(p[0])) : 24;
     FLSIM_REQUIRE(offset_bytes, "null pointer");
-    FLSIM_REQUIRE(which >= 0 && which < (int)(sizeof(p) / sizeof(p[0])), "bad workspace id %d",
-                  which);
+    FLSIM_REQUIRE(which >= 0 && which < n, "bad workspace id %d", which);
     *offset_bytes = (long)((const char*)p[which] - fake);
     return 0;
 }
 
-int flsim_vgg11_begin_epoch(void* gradstate, const float* theta, hipStream_t stream) {
+template <bool BN>
+static int vgg_begin_epoch(void* gradstate, const float* theta, hipStream_t stream) {
     FLSIM_REQUIRE(gradstate && theta, "null pointer");
-    VGrad g = vgs_layout((float*)gradstate);
-    RC(vpack(g, theta, stream));
+    VGrad g = vgs_layout((float*)gradstate, BN);
+    RC(vpack(g, theta, voff(BN), stream));
     FLSIM_CHECK_HIP(hipMemsetAsync(g.slab_begin, 0, g.slab_floats * 4, stream));
     return 0;
 }
 
-int flsim_vgg11_fwd_bwd_chunk(void* gradstate, void* workspace, int max_samples,
-                              const float* theta, const uint8_t* pool, const int32_t* labels,
-                              const int32_t* list_a, int len_a, const int32_t* list_b, int len_b,
-                              const float* lut, const WorkerRec* workers, int n_chunk_workers,
-                              int n_workers_total, uint64_t seed, int dropout, int backward_pass,
-                              float* worker_loss, hipStream_t stream) {
+template <bool BN>
+static int vgg_fwd_bwd_chunk(void* gradstate, void* workspace, int max_samples,
+                             const float* theta, const uint8_t* pool, const int32_t* labels,
+                             const int32_t* list_a, int len_a, const int32_t* list_b, int len_b,
+                             const float* lut, const WorkerRec* workers, int n_chunk_workers,
+                             int n_workers_total, uint64_t seed, int dropout, int backward_pass,
+                             float* worker_loss, float* bn_stats, hipStream_t stream) {
     FLSIM_REQUIRE(gradstate && workspace && theta && pool && labels && list_a && list_b && lut &&
                   workers && worker_loss, "null pointer");
     FLSIM_REQUIRE(n_chunk_workers > 0, "empty chunk");
@@ -320,18 +438,20 @@ int flsim_vgg11_fwd_bwd_chunk(void* gradstate, void* workspace, int max_samples,
     FLSIM_REQUIRE(S <= max_samples, "chunk of %d samples exceeds workspace (%d)", S, max_samples);
     FLSIM_REQUIRE(S <= 16384, "chunk of %d samples exceeds the 32-bit index budget", S);
     FLSIM_REQUIRE(len_a > 0 && len_b > 0, "empty class list");
-    VWS w = vws_layout((char*)workspace, max_samples);
+    VWS w = vws_layout((char*)workspace, max_samples, BN);
     hipLaunchKernelGGL(k_fill_batch, dim3(S), dim3(256), 0, stream, pool, labels, list_a, len_a,
                        list_b, len_b, workers, n_workers_total, seed, lut, w.x0, w.y);
     FLSIM_LAUNCH_CHECK();
-    return vrun_chunk(gradstate, w, theta, workers, n_chunk_workers, seed, dropout, backward_pass,
-                      worker_loss, stream);
+    return vrun_chunk<BN>(gradstate, w, theta, workers, n_chunk_workers, seed, dropout,
+                          backward_pass, worker_loss, bn_stats, stream);
 }
 
-int flsim_vgg11_fwd_bwd_input(void* gradstate, void* workspace, int max_samples,
-                              const float* theta, const float* x, const int64_t* y, int n_samples,
-                              const WorkerRec* workers, uint64_t seed, int dropout,
-                              int backward_pass, float* worker_loss, hipStream_t stream) {
+template <bool BN>
+static int vgg_fwd_bwd_input(void* gradstate, void* workspace, int max_samples,
+                             const float* theta, const float* x, const int64_t* y, int n_samples,
+                             const WorkerRec* workers, uint64_t seed, int dropout,
+                             int backward_pass, float* worker_loss, float* bn_stats,
+                             hipStream_t stream) {
     FLSIM_REQUIRE(gradstate && workspace && theta && x && y && workers && worker_loss,
                   "null pointer");
     FLSIM_REQUIRE(n_samples > 0 && n_samples % SAMPLES_PER_WORKER == 0,
@@ -341,32 +461,37 @@ int flsim_vgg11_fwd_bwd_input(void* gradstate, void* workspace, int max_samples,
                   max_samples);
     FLSIM_REQUIRE(n_samples <= 16384, "batch of %d samples exceeds the 32-bit index budget",
                   n_samples);
-    VWS w = vws_layout((char*)workspace, max_samples);
+    VWS w = vws_layout((char*)workspace, max_samples, BN);
     hipLaunchKernelGGL(k_load_input, dim3(n_samples), dim3(256), 0, stream, x, y, w.x0, w.y);
     FLSIM_LAUNCH_CHECK();
-    return vrun_chunk(gradstate, w, theta, workers, n_samples / SAMPLES_PER_WORKER, seed, dropout,
-                      backward_pass, worker_loss, stream);
+    return vrun_chunk<BN>(gradstate, w, theta, workers, n_samples / SAMPLES_PER_WORKER, seed,
+                          dropout, backward_pass, worker_loss, bn_stats, stream);
 }
 
-// Evaluation (util.py:31-45 after central.model.eval(), main.py:190: dropout off)
-int flsim_vgg11_eval_pool(void* gradstate, void* workspace, int max_samples, const float* theta,
-                          const uint8_t* pool, int first, int n_images, const float* lut,
-                          int32_t* pred, hipStream_t stream) {
+// Evaluation (util.py:31-45 after central.model.eval(), main.py:190: dropout off; vgg11_bn:
+// BatchNorm with the running buffers)
+template <bool BN>
+static int vgg_eval_pool(void* gradstate, void* workspace, int max_samples, const float* theta,
+                         const uint8_t* pool, int first, int n_images, const float* lut,
+                         const float* running, int32_t* pred, hipStream_t stream) {
     FLSIM_REQUIRE(gradstate && workspace && theta && pool && lut && pred, "null pointer");
+    FLSIM_REQUIRE(!BN || running, "null running buffers");
     FLSIM_REQUIRE(n_images > 0 && first >= 0, "bad image range");
     FLSIM_REQUIRE(max_samples >= SAMPLES_PER_WORKER && max_samples % SAMPLES_PER_WORKER == 0,
                   "max_samples must be a positive multiple of %d", SAMPLES_PER_WORKER);
-    const VOff o = voff();
-    VGrad g = vgs_layout((float*)gradstate);
-    VWS w = vws_layout((char*)workspace, max_samples);
-    RC(vpack(g, theta, stream));
+    const VOff o = voff(BN);
+    VGrad g = vgs_layout((float*)gradstate, BN);
+    VWS w = vws_layout((char*)workspace, max_samples, BN);
+    RC(vpack(g, theta, o, stream));
+    const VBN bn{&w, 0, nullptr};
+    if (BN) RC(vbn_eval_coef(w, running, stream));
     for (int c0 = 0; c0 < n_images; c0 += max_samples) {
         const int n = n_images - c0 < max_samples ? n_images - c0 : max_samples;
         const int S = ceil_div(n, SAMPLES_PER_WORKER) * SAMPLES_PER_WORKER;
         hipLaunchKernelGGL(k_fill_seq, dim3(S), dim3(256), 0, stream, pool, first + c0, n, lut,
                            w.x0, w.y);
         FLSIM_LAUNCH_CHECK();
-        RC(vforward(g, w, theta, S, nullptr, 0, 0, stream));
+        RC(vforward<BN>(g, w, theta, o, S, nullptr, 0, 0, &bn, stream));
         RC(head_predict<VFEAT>(w.e2, theta + o.l3w, theta + o.l3b, w.y, w.loss_s, S, pred + c0, n,
                                stream));
     }
@@ -374,15 +499,20 @@ int flsim_vgg11_eval_pool(void* gradstate, void* workspace, int max_samples, con
 }
 
 // S_t (torch named_parameters layout) = sum of the epoch's slabs (fixed order)
-int flsim_vgg11_end_epoch(void* gradstate, float* grad_out, hipStream_t stream) {
+template <bool BN>
+static int vgg_end_epoch(void* gradstate, float* grad_out, hipStream_t stream) {
     FLSIM_REQUIRE(gradstate && grad_out, "null pointer");
-    const VOff o = voff();
-    VGrad g = vgs_layout((float*)gradstate);
+    const VOff o = voff(BN);
+    VGrad g = vgs_layout((float*)gradstate, BN);
     for (int l = 0; l < 8; ++l) {
         const VConv& c = VG[l];
         RC(fin_sum(g.sw[l], c.ZW, (long)c.CO * c.KP, grad_out + o.w[l], stream, c.CO, c.CI, c.CIP,
                    c.KP));
         RC(fin_sum(g.sb[l], c.ZW, c.CO, grad_out + o.b[l], stream));
+        if (BN) {
+            RC(fin_sum(g.bnacc[l], 1, c.CO, grad_out + o.g[l], stream));
+            RC(fin_sum(g.bnacc[l] + c.CO, 1, c.CO, grad_out + o.be[l], stream));
+        }
     }
     RC(fin_sum(g.l1w, VZL, (long)VFEAT * VFEAT, grad_out + o.l1w, stream));
     RC(fin_sum(g.l1b, VZL, VFEAT, grad_out + o.l1b, stream));
@@ -390,6 +520,128 @@ int flsim_vgg11_end_epoch(void* gradstate, float* grad_out, hipStream_t stream) 
     RC(fin_sum(g.l2b, VZL, VFEAT, grad_out + o.l2b, stream));
     RC(fin_sum(g.l3w, VZH, 10L * VFEAT, grad_out + o.l3w, stream));
     RC(fin_sum(g.l3b, VZH, 10, grad_out + o.l3b, stream));
+    return 0;
+}
+
+}  // namespace flsim
+
+using namespace flsim;
+
+// =============================================================================================
+// C-ABI (declared in include/flsim.h): the flsim_pn1_* contract for vgg11() and vgg11_bn()
+// =============================================================================================
+extern "C" {
+
+long flsim_vgg11_param_count(void) { return voff(false).total; }
+
+long flsim_vgg11_gradstate_bytes(void) { return vgs_layout(nullptr, false).total_floats * 4; }
+
+long flsim_vgg11_workspace_bytes(int max_samples) {
+    return vws_layout(nullptr, max_samples, false).bytes;
+}
+
+int flsim_vgg11_workspace_offset(int which, int samples, long* offset_bytes) {
+    return vgg_workspace_offset<false>(which, samples, offset_bytes);
+}
+
+int flsim_vgg11_begin_epoch(void* gradstate, const float* theta, hipStream_t stream) {
+    return vgg_begin_epoch<false>(gradstate, theta, stream);
+}
+
+int flsim_vgg11_fwd_bwd_chunk(void* gradstate, void* workspace, int max_samples,
+                              const float* theta, const uint8_t* pool, const int32_t* labels,
+                              const int32_t* list_a, int len_a, const int32_t* list_b, int len_b,
+                              const float* lut, const WorkerRec* workers, int n_chunk_workers,
+                              int n_workers_total, uint64_t seed, int dropout, int backward_pass,
+                              float* worker_loss, hipStream_t stream) {
+    return vgg_fwd_bwd_chunk<false>(gradstate, workspace, max_samples, theta, pool, labels, list_a,
+                                    len_a, list_b, len_b, lut, workers, n_chunk_workers,
+                                    n_workers_total, seed, dropout, backward_pass, worker_loss,
+                                    nullptr, stream);
+}
+
+int flsim_vgg11_fwd_bwd_input(void* gradstate, void* workspace, int max_samples,
+                              const float* theta, const float* x, const int64_t* y, int n_samples,
+                              const WorkerRec* workers, uint64_t seed, int dropout,
+                              int backward_pass, float* worker_loss, hipStream_t stream) {
+    return vgg_fwd_bwd_input<false>(gradstate, workspace, max_samples, theta, x, y, n_samples,
+                                    workers, seed, dropout, backward_pass, worker_loss, nullptr,
+                                    stream);
+}
+
+int flsim_vgg11_eval_pool(void* gradstate, void* workspace, int max_samples, const float* theta,
+                          const uint8_t* pool, int first, int n_images, const float* lut,
+                          int32_t* pred, hipStream_t stream) {
+    return vgg_eval_pool<false>(gradstate, workspace, max_samples, theta, pool, first, n_images,
+                                lut, nullptr, pred, stream);
+}
+
+int flsim_vgg11_end_epoch(void* gradstate, float* grad_out, hipStream_t stream) {
+    return vgg_end_epoch<false>(gradstate, grad_out, stream);
+}
+
+// ---- vgg11_bn -------------------------------------------------------------------------------
+long flsim_vgg11_bn_param_count(void) { return voff(true).total; }
+
+long flsim_vgg11_bn_gradstate_bytes(void) { return vgs_layout(nullptr, true).total_floats * 4; }
+
+long flsim_vgg11_bn_workspace_bytes(int max_samples) {
+    return vws_layout(nullptr, max_samples, true).bytes;
+}
+
+int flsim_vgg11_bn_workspace_offset(int which, int samples, long* offset_bytes) {
+    return vgg_workspace_offset<true>(which, samples, offset_bytes);
+}
+
+int flsim_vgg11_bn_stats_per_worker(void) { return BN_NSTAT; }
+
+int flsim_vgg11_bn_begin_epoch(void* gradstate, const float* theta, hipStream_t stream) {
+    return vgg_begin_epoch<true>(gradstate, theta, stream);
+}
+
+int flsim_vgg11_bn_fwd_bwd_chunk(void* gradstate, void* workspace, int max_samples,
+                                 const float* theta, const uint8_t* pool, const int32_t* labels,
+                                 const int32_t* list_a, int len_a, const int32_t* list_b,
+                                 int len_b, const float* lut, const WorkerRec* workers,
+                                 int n_chunk_workers, int n_workers_total, uint64_t seed,
+                                 int dropout, int backward_pass, float* worker_loss,
+                                 float* bn_stats, hipStream_t stream) {
+    return vgg_fwd_bwd_chunk<true>(gradstate, workspace, max_samples, theta, pool, labels, list_a,
+                                   len_a, list_b, len_b, lut, workers, n_chunk_workers,
+                                   n_workers_total, seed, dropout, backward_pass, worker_loss,
+                                   bn_stats, stream);
+}
+
+int flsim_vgg11_bn_fwd_bwd_input(void* gradstate, void* workspace, int max_samples,
+                                 const float* theta, const float* x, const int64_t* y,
+                                 int n_samples, const WorkerRec* workers, uint64_t seed,
+                                 int dropout, int backward_pass, float* worker_loss,
+                                 float* bn_stats, hipStream_t stream) {
+    return vgg_fwd_bwd_input<true>(gradstate, workspace, max_samples, theta, x, y, n_samples,
+                                   workers, seed, dropout, backward_pass, worker_loss, bn_stats,
+                                   stream);
+}
+
+int flsim_vgg11_bn_eval_pool(void* gradstate, void* workspace, int max_samples,
+                             const float* theta, const uint8_t* pool, int first, int n_images,
+                             const float* lut, const float* running, int32_t* pred,
+                             hipStream_t stream) {
+    return vgg_eval_pool<true>(gradstate, workspace, max_samples, theta, pool, first, n_images,
+                               lut, running, pred, stream);
+}
+
+int flsim_vgg11_bn_end_epoch(void* gradstate, float* grad_out, hipStream_t stream) {
+    return vgg_end_epoch<true>(gradstate, grad_out, stream);
+}
+
+int flsim_vgg11_bn_update_running(float* running, const float* bn_stats, int n_workers,
+                                  hipStream_t stream) {
+    FLSIM_REQUIRE(running && (bn_stats || n_workers == 0), "null pointer");
+    FLSIM_REQUIRE(n_workers >= 0, "negative worker count");
+    if (n_workers == 0) return 0;
+    hipLaunchKernelGGL(k_bn_running, dim3(ceil_div(BN_NSTAT, 256)), dim3(256), 0, stream, running,
+                       bn_stats, n_workers, BN_NSTAT);
+    FLSIM_LAUNCH_CHECK();
     return 0;
 }
 

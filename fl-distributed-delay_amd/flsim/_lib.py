@@ -21,7 +21,11 @@ EXPORTS = [
     "flsim_pn1_eval_pool", "flsim_vgg11_param_count", "flsim_vgg11_gradstate_bytes",
     "flsim_vgg11_workspace_bytes", "flsim_vgg11_workspace_offset", "flsim_vgg11_begin_epoch",
     "flsim_vgg11_fwd_bwd_chunk", "flsim_vgg11_fwd_bwd_input", "flsim_vgg11_end_epoch",
-    "flsim_vgg11_eval_pool",
+    "flsim_vgg11_eval_pool", "flsim_vgg11_bn_param_count", "flsim_vgg11_bn_gradstate_bytes",
+    "flsim_vgg11_bn_workspace_bytes", "flsim_vgg11_bn_workspace_offset",
+    "flsim_vgg11_bn_stats_per_worker", "flsim_vgg11_bn_begin_epoch",
+    "flsim_vgg11_bn_fwd_bwd_chunk", "flsim_vgg11_bn_fwd_bwd_input", "flsim_vgg11_bn_end_epoch",
+    "flsim_vgg11_bn_eval_pool", "flsim_vgg11_bn_update_running",
     "flsim_aggregate_adam", "flsim_aggregate_adam_seq", "flsim_probe_enable", "flsim_probe_read", "flsim_probe_disable",
     "flsim_probe_kernel_count", "flsim_probe_kernel_name",
 ]
@@ -54,7 +58,9 @@ def lib():
     L.flsim_sched_destroy.argtypes = [vp]
     L.flsim_sched_epoch.argtypes = [vp] * 6
     L.flsim_sched_state.argtypes = [vp, vp]
-    for net in ("pn1", "vgg11"):          # the same per-network contract (include/flsim.h)
+    for net in ("pn1", "vgg11", "vgg11_bn"):      # one per-network contract (include/flsim.h)
+        bn = [vp] if net == "vgg11_bn" else []    # + bn_stats (chunk) / running (eval)
+
         def f(name):
             return getattr(L, f"flsim_{net}_{name}")
         f("param_count").restype = ctypes.c_long
@@ -65,13 +71,14 @@ def lib():
         f("begin_epoch").argtypes = [vp, vp, vp]
         f("fwd_bwd_chunk").argtypes = [
             vp, vp, ctypes.c_int, vp, vp, vp, vp, ctypes.c_int, vp, ctypes.c_int, vp, vp,
-            ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, vp, vp]
+            ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, vp] + bn + [vp]
         f("fwd_bwd_input").argtypes = [
             vp, vp, ctypes.c_int, vp, vp, vp, ctypes.c_int, vp, ctypes.c_uint64, ctypes.c_int,
-            ctypes.c_int, vp, vp]
+            ctypes.c_int, vp] + bn + [vp]
         f("end_epoch").argtypes = [vp, vp, vp]
         f("eval_pool").argtypes = [vp, vp, ctypes.c_int, vp, vp, ctypes.c_int, ctypes.c_int,
-                                   vp, vp, vp]
+                                   vp] + bn + [vp, vp]
+    L.flsim_vgg11_bn_update_running.argtypes = [vp, vp, ctypes.c_int, vp]
     L.flsim_aggregate_adam.argtypes = [
         vp, ctypes.c_int, vp, ctypes.c_int, vp, vp, vp, ctypes.c_long, vp, ctypes.c_int,
         ctypes.c_long, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp]

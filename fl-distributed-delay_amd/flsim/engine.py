@@ -7,7 +7,8 @@
 
 PN1Engine runs models.py:PerformantNet1 (the model main.py:97 builds) through flsim_pn1_*;
 VGG11Engine runs models.py:vgg11() (models.py:50-103, configs[4]'s larger CNN) through
-flsim_vgg11_*.  Both entry-point families share one contract (include/flsim.h).
+flsim_vgg11_*; VGG11BNEngine runs vgg11_bn() (models.py:106-108) through flsim_vgg11_bn_* and
+keeps its BatchNorm running buffers.  Both entry-point families share one contract (include/flsim.h).
 """
 from __future__ import annotations
 
@@ -45,6 +46,19 @@ VGG11_SHAPES = [
     ("classifier.4.weight", (512, 512)), ("classifier.4.bias", (512,)),
     ("classifier.6.weight", (10, 512)), ("classifier.6.bias", (10,)),
 ]
+# named_parameters() order of models.py:vgg11_bn() (make_layers(cfg 'A', batch_norm=True):
+# Conv2d, BatchNorm2d, ReLU per conv, models.py:88-89) and its BatchNorm buffers
+_BN_IDX = (0, 4, 8, 11, 15, 18, 22, 25)      # conv module index in features; BatchNorm = +1
+VGG11_BN_SHAPES = []
+for _j, (_, _shp) in enumerate(VGG11_SHAPES[:16:2]):
+    _co = _shp[0]
+    VGG11_BN_SHAPES += [(f"features.{_BN_IDX[_j]}.weight", _shp),
+                        (f"features.{_BN_IDX[_j]}.bias", (_co,)),
+                        (f"features.{_BN_IDX[_j] + 1}.weight", (_co,)),
+                        (f"features.{_BN_IDX[_j] + 1}.bias", (_co,))]
+VGG11_BN_SHAPES += VGG11_SHAPES[16:]
+VGG11_BN_BUFFERS = [(f"features.{i + 1}", int(shp[0]))
+                    for i, (_, shp) in zip(_BN_IDX, VGG11_SHAPES[:16:2])]
 PN1_SIZES = [int(np.prod(s)) for _, s in PN1_SHAPES]
 VGG11_SIZES = [int(np.prod(s)) for _, s in VGG11_SHAPES]
 SAMPLES_PER_WORKER = 128
@@ -71,6 +85,7 @@ class NetEngine:
     MODEL = None
     SHAPES = None
     FLOP_PER_WORKER_STEP = None     # algorithmic fwd + dgrad + wgrad FLOPs of 128 samples
+    STATS_PER_WORKER = 0            # per-call statistics the model's buffers need (BatchNorm)
 
     def __init__(self, device, chunk_workers=32):
         self.device = torch.device(device)
@@ -91,32 +106,53 @@ class NetEngine:
     def begin_epoch(self, theta):
         check(self._fn("begin_epoch")(ptr(self.gradstate), ptr(theta), stream_ptr()))
 
+    def _stats_arg(self, stats_out):
+        """The extra bn_stats argument of a BatchNorm model's entry points (none otherwise)."""
+        if not self.STATS_PER_WORKER:
+            return ()
+        return (ptr(stats_out) if stats_out is not None else None,)
+
     def run_chunk(self, theta, pool, workers_dev, n_chunk, n_workers_total, seed, dropout,
-                  loss_out, backward=True):
+                  loss_out, backward=True, stats_out=None):
+        """stats_out (BatchNorm models): device float[n_chunk][STATS_PER_WORKER] for the
+        per-call statistics that update_running() folds into the running buffers."""
         check(self._fn("fwd_bwd_chunk")(
             ptr(self.gradstate), ptr(self.workspace), self.max_samples, ptr(theta),
             ptr(pool.imgs), ptr(pool.labels), ptr(pool.list_a), int(pool.list_a.numel()),
             ptr(pool.list_b), int(pool.list_b.numel()), ptr(pool.lut), ptr(workers_dev),
             int(n_chunk), int(n_workers_total), ctypes.c_uint64(seed), int(bool(dropout)),
-            int(bool(backward)), ptr(loss_out), stream_ptr()))
+            int(bool(backward)), ptr(loss_out), *self._stats_arg(stats_out), stream_ptr()))
 
-    def run_input(self, theta, x, y, workers_dev, seed, dropout, loss_out, backward=True):
+    def run_input(self, theta, x, y, workers_dev, seed, dropout, loss_out, backward=True,
+                  stats_out=None):
         x = x.contiguous()
         y = y.to(torch.int64).contiguous()
         check(self._fn("fwd_bwd_input")(
             ptr(self.gradstate), ptr(self.workspace), self.max_samples, ptr(theta), ptr(x), ptr(y),
             int(x.shape[0]), ptr(workers_dev), ctypes.c_uint64(seed), int(bool(dropout)),
-            int(bool(backward)), ptr(loss_out), stream_ptr()))
+            int(bool(backward)), ptr(loss_out), *self._stats_arg(stats_out), stream_ptr()))
 
     def evaluate(self, theta, pool, first=0, n_images=None):
         """Predictions (argmax of the logits, dropout off) for pool images [first, first + n):
         util.print_test_accuracy's forward (util.py:31-45).  Returns a device int32 tensor."""
         n = int(pool.imgs.shape[0]) - first if n_images is None else int(n_images)
         pred = torch.empty(n, dtype=torch.int32, device=self.device)
+        extra = (ptr(self.running),) if self.STATS_PER_WORKER else ()
         check(self._fn("eval_pool")(
             ptr(self.gradstate), ptr(self.workspace), self.max_samples, ptr(theta), ptr(pool.imgs),
-            int(first), n, ptr(pool.lut), ptr(pred), stream_ptr()))
+            int(first), n, ptr(pool.lut), *extra, ptr(pred), stream_ptr()))
         return pred
+
+    # -- model buffers (BatchNorm running statistics; none for the other models) ----------------
+    def update_running(self, stats, n_workers):
+        """nn.BatchNorm2d's per-call running update for n_workers calls in worker order."""
+
+    def buffer_state(self):
+        """The model's buffers as state_dict entries (OrderedDict order of models.py)."""
+        return []
+
+    def load_buffers(self, state):
+        """Restore buffer_state() output (names -> tensors)."""
 
     def end_epoch(self, grad_out):
         check(self._fn("end_epoch")(ptr(self.gradstate), ptr(grad_out), stream_ptr()))
@@ -156,7 +192,60 @@ class VGG11Engine(NetEngine):
                  "i1 i2 i4 i6 i8").split()
 
 
-ENGINES = {"PerformantNet1": PN1Engine, "vgg11": VGG11Engine}
+class VGG11BNEngine(NetEngine):
+    """models.py:106-108 vgg11_bn() through flsim_vgg11_bn_*.  Holds the model's BatchNorm
+    buffers: `running` = [running_mean | running_var] per layer on the device (zeros / ones at
+    construction, nn.BatchNorm2d's init) and the num_batches_tracked counter (the same for every
+    layer: each fwd_bkwd call updates all of them)."""
+    PREFIX = "vgg11_bn"
+    MODEL = "vgg11_bn"
+    SHAPES = VGG11_BN_SHAPES
+    FLOP_PER_WORKER_STEP = 117_276_672_000          # the GEMMs of vgg11 (BatchNorm is streaming)
+    STATS_PER_WORKER = 5504
+    WORKSPACE = ("x0 d1 d2 a3 d4 a5 d6 a7 f0 e1 e2 dh1 dh2 ga gb gy loss_s dlog y "
+                 "i1 i2 i4 i6 i8 " + " ".join(f"z{j}" for j in range(8)) + " " +
+                 " ".join(f"bmean{j}" for j in range(8)) + " " +
+                 " ".join(f"binv{j}" for j in range(8))).split()
+
+    def __init__(self, device, chunk_workers=32):
+        super().__init__(device, chunk_workers)
+        assert int(lib().flsim_vgg11_bn_stats_per_worker()) == self.STATS_PER_WORKER
+        self.running = torch.cat([torch.cat([torch.zeros(c), torch.ones(c)])
+                                  for _, c in VGG11_BN_BUFFERS]).to(self.device)
+        self.num_batches_tracked = 0
+
+    def update_running(self, stats, n_workers):
+        n = int(n_workers)
+        if n:
+            check(lib().flsim_vgg11_bn_update_running(ptr(self.running), ptr(stats), n,
+                                                      stream_ptr()))
+        self.num_batches_tracked += n
+
+    def running_views(self):
+        """[(name, running_mean view, running_var view)] per BatchNorm layer."""
+        out, off = [], 0
+        for name, c in VGG11_BN_BUFFERS:
+            out.append((name, self.running[off:off + c], self.running[off + c:off + 2 * c]))
+            off += 2 * c
+        return out
+
+    def buffer_state(self):
+        out = []
+        for name, rm, rv in self.running_views():
+            out += [(f"{name}.running_mean", rm.detach().cpu().clone()),
+                    (f"{name}.running_var", rv.detach().cpu().clone()),
+                    (f"{name}.num_batches_tracked",
+                     torch.tensor(self.num_batches_tracked, dtype=torch.int64))]
+        return out
+
+    def load_buffers(self, state):
+        for name, rm, rv in self.running_views():
+            rm.copy_(state[f"{name}.running_mean"].to(self.device))
+            rv.copy_(state[f"{name}.running_var"].to(self.device))
+        self.num_batches_tracked = int(state[f"{VGG11_BN_BUFFERS[0][0]}.num_batches_tracked"])
+
+
+ENGINES = {"PerformantNet1": PN1Engine, "vgg11": VGG11Engine, "vgg11_bn": VGG11BNEngine}
 
 
 def engine_class(model):
@@ -171,7 +260,8 @@ def engine_for_parameters(names):
     for cls in ENGINES.values():
         if names == [n for n, _ in cls.SHAPES]:
             return cls
-    raise NotImplementedError("the HIP engine implements FL.models.PerformantNet1 and vgg11")
+    raise NotImplementedError("the HIP engine implements FL.models.PerformantNet1, vgg11 and "
+                              "vgg11_bn")
 
 
 def aggregate_adam(S, c, stale, theta, m, v, step, sizes, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):

@@ -7,7 +7,9 @@ Per epoch t (one "server step"):
      (torch.distributed; one process per GPU), and each rank runs its block as worker-batched
      chunks of `chunk_workers` x 128 samples through the HIP forward/backward; all of them use
      theta_t, so their gradients simply add (agents.py:35) -- S_t;
-  3. world > 1: ONE all-reduce (RCCL) of [S_t partial | per-worker losses];
+  3. world > 1: ONE all-reduce (RCCL) of [S_t partial | per-worker losses | per-worker BatchNorm
+     statistics (vgg11_bn)]; BatchNorm running buffers advance over every computing worker's
+     call in worker order;
   4. a slow worker that computed stores S_t in its FIFO (main.py:156,161: the entry is an alias
      of the epoch's .grad tensors, so under torch >= 2 it holds S_t); popped entries (main.py:162)
      are the stale gradients S_{t-d};
@@ -79,8 +81,11 @@ class FLSimulation:
         self.m = torch.zeros_like(self.theta)
         self.v = torch.zeros_like(self.theta)
         self.step = 0
-        # [S_t | losses of the computing workers]; one all-reduce per epoch when world > 1
-        self.comm = torch.zeros(self.Ppad + padded(self.n), device=self.device)
+        # [S_t | losses of the computing workers | their per-call BatchNorm statistics (vgg11_bn)]
+        # -- one all-reduce per epoch when world > 1 (each rank fills only its workers' rows)
+        self.nstat = int(getattr(self.engine, "STATS_PER_WORKER", 0))
+        self.stats_off = self.Ppad + padded(self.n)
+        self.comm = torch.zeros(self.stats_off + self.n * self.nstat, device=self.device)
         self.stale_store = {}     # epoch -> [slot tensor, refcount]
         self.free_slots = []
         self.trace = []
@@ -163,16 +168,24 @@ class FLSimulation:
         eng = self.engine
         S = self.comm[:self.P]
         losses = self.comm[self.Ppad:self.Ppad + len(active)]
+        stats = self.comm[self.stats_off:self.stats_off + len(active) * self.nstat].view(
+            len(active), self.nstat)
         if self.world > 1:
             losses.zero_()
+            stats.zero_()
         eng.begin_epoch(self.theta)
         wt = self._worker_table(t, active[lo:hi], ks)      # one async upload per epoch
         for c0, c1 in self.chunks(lo, hi):
+            kw = {"stats_out": stats[c0:c1]} if self.nstat else {}
             eng.run_chunk(self.theta, self.pool, wt[c0 - lo:c1 - lo], c1 - c0, self.n, self.seed,
-                          self.dropout, losses[c0:c1])
+                          self.dropout, losses[c0:c1], **kw)
         eng.end_epoch(S)
         if self.world > 1:
-            torch.distributed.all_reduce(self.comm[:self.Ppad + len(active)], group=self.group)
+            end = self.stats_off + len(active) * self.nstat if self.nstat else \
+                self.Ppad + len(active)
+            torch.distributed.all_reduce(self.comm[:end], group=self.group)
+        if self.nstat:   # BatchNorm running buffers: every computing worker's call, in order
+            eng.update_running(stats, len(active))
         if plan.pushed and self.semantics == "reference":
             n_push = int(sum(1 for i in range(self.n) if self.delays[i] != 0 and plan.computes[i]))
             slot = self._slot()
@@ -251,12 +264,21 @@ class FLSimulation:
         return acc, per
 
     def model_state_dict(self):
-        """models.py PerformantNet1 state_dict (torch.save-compatible with the reference's
-        main.py:98-100 / :192-194 load_state_dict / save)."""
+        """The models.py module's state_dict (torch.save-compatible with the reference's
+        main.py:98-100 / :192-194 load_state_dict / save); BatchNorm buffers follow their
+        module's parameters, as nn.Module.state_dict orders them."""
         from collections import OrderedDict
         shapes = self.engine.SHAPES
-        return OrderedDict((name, v.detach().cpu().clone())
-                           for (name, _), v in zip(shapes, split_views(self.theta, shapes)))
+        bufs = self.engine.buffer_state()
+        out = OrderedDict()
+        for (name, _), v in zip(shapes, split_views(self.theta, shapes)):
+            out[name] = v.detach().cpu().clone()
+            mod = name.rsplit(".", 1)[0]
+            if name.endswith(".bias"):
+                for bname, b in bufs:
+                    if bname.rsplit(".", 1)[0] == mod:
+                        out[bname] = b
+        return out
 
     # -- checkpoint / resume ----------------------------------------------------------------------
     def checkpoint(self):
@@ -275,6 +297,7 @@ class FLSimulation:
             "stale": {int(src): (slot[:self.P].detach().cpu(), int(rc))
                       for src, (slot, rc) in self.stale_store.items()},
             "loss_log": [float(x) for x in self.losses()],
+            "buffers": dict(getattr(self.engine, "buffer_state", list)()),
         }
 
     def save_checkpoint(self, path):
@@ -311,6 +334,8 @@ class FLSimulation:
             slot[:self.P].copy_(vals.to(self.device))
             self.stale_store[int(src)] = [slot, int(rc)]
         self.loss_log = list(ck["loss_log"])
+        if ck.get("buffers"):
+            self.engine.load_buffers(ck["buffers"])
 
     def executed_worker_steps(self, plan):
         return int(plan.computes.sum())

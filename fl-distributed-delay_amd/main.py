@@ -45,8 +45,9 @@ def parse(argv=None):
                    help='stale entry = S_{t-d} (torch>=2 aliasing) or zeros (torch 1.x)')
     p.add_argument('--no-dropout', action='store_true')
     p.add_argument('--chunk', type=int, default=32, help='workers per worker-batched launch')
-    p.add_argument('--model', default='PerformantNet1', choices=['PerformantNet1', 'vgg11'],
-                   help='models.py network (main.py:97 builds PerformantNet1; vgg11 = configs[4])')
+    p.add_argument('--model', default='PerformantNet1', choices=['PerformantNet1', 'vgg11', 'vgg11_bn'],
+                   help='models.py network (main.py:97 builds PerformantNet1; vgg11 = configs[4]; '
+                        'vgg11_bn = models.py:106-108)')
     p.add_argument('--log', type=str, default=None,
                    help="JSONL scalar log ('Avg. Loss', 'Avg. Test Accuracy', 'Class 9 ...')")
     p.add_argument('--data_dir', type=str, default=None,
@@ -74,11 +75,13 @@ def main(argv=None):
     rank = torch.distributed.get_rank() if world > 1 else 0
     from flsim.sim import FLSimulation, default_theta
     theta0 = default_theta(args.seed, args.model)
+    buffers = None
     if args.model_file is not None:                       # main.py:98-100
         from FL import models
         m = getattr(models, args.model)()
         m.load_state_dict(torch.load(args.model_file, map_location="cpu", weights_only=True))
         theta0 = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+        buffers = dict(m.named_buffers())                 # vgg11_bn running statistics
     if rank == 0:
         print(dev)
     pool = test_pool = None
@@ -89,6 +92,8 @@ def main(argv=None):
                        lr=args.learning_rate, seed=args.seed, semantics=args.semantics,
                        dropout=not args.no_dropout, chunk_workers=args.chunk, device=dev,
                        theta0=theta0, pool=pool, test_pool=test_pool, model=args.model)
+    if buffers:
+        sim.engine.load_buffers(buffers)
     if args.resume:
         sim.restore(args.resume)
     log = open(args.log, "a" if args.resume else "w") if (args.log and rank == 0) else None

@@ -114,6 +114,46 @@ int flsim_vgg11_eval_pool(void* gradstate, void* workspace, int max_samples, con
                           int32_t* pred, flsim_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * VGG-11 with BatchNorm (models.py:106-108 vgg11_bn(): Conv2d -> BatchNorm2d -> ReLU per conv,
+ * models.py:88-89): replaces Worker.fwd_bkwd (agents.py:32-40) when the central model is
+ * vgg11_bn().  Same contract as flsim_vgg11_*; parameters flat in vgg11_bn().named_parameters()
+ * order (conv weight, conv bias, BatchNorm weight, BatchNorm bias per layer), P = 9,756,426.
+ * Train mode: every simulated worker's 128 samples are one BatchNorm batch (one fwd_bkwd call);
+ * bn_stats (device float[n_chunk_workers][flsim_vgg11_bn_stats_per_worker()] or nullptr)
+ * receives each worker's per-layer [batch mean | unbiased batch variance], the inputs of the
+ * running-buffer update nn.BatchNorm2d does on every call.  The running buffers are a device
+ * float[5504]: [running_mean | running_var] of features.1, .5, .9, .12, .16, .19, .23, .26.
+ * ------------------------------------------------------------------------------------------- */
+long flsim_vgg11_bn_param_count(void);
+long flsim_vgg11_bn_gradstate_bytes(void);
+long flsim_vgg11_bn_workspace_bytes(int max_samples);
+int flsim_vgg11_bn_workspace_offset(int which, int samples, long* offset_bytes);
+int flsim_vgg11_bn_stats_per_worker(void);
+int flsim_vgg11_bn_begin_epoch(void* gradstate, const float* theta, flsim_stream_t stream);
+int flsim_vgg11_bn_fwd_bwd_chunk(void* gradstate, void* workspace, int max_samples,
+                                 const float* theta, const uint8_t* pool, const int32_t* labels,
+                                 const int32_t* list_a, int len_a, const int32_t* list_b,
+                                 int len_b, const float* lut, const WorkerRec* workers,
+                                 int n_chunk_workers, int n_workers_total, uint64_t seed,
+                                 int dropout, int backward_pass, float* worker_loss,
+                                 float* bn_stats, flsim_stream_t stream);
+int flsim_vgg11_bn_fwd_bwd_input(void* gradstate, void* workspace, int max_samples,
+                                 const float* theta, const float* x, const int64_t* y,
+                                 int n_samples, const WorkerRec* workers, uint64_t seed,
+                                 int dropout, int backward_pass, float* worker_loss,
+                                 float* bn_stats, flsim_stream_t stream);
+int flsim_vgg11_bn_end_epoch(void* gradstate, float* grad_out, flsim_stream_t stream);
+/* util.py:31-45 in eval mode: BatchNorm normalises with the running buffers `running`. */
+int flsim_vgg11_bn_eval_pool(void* gradstate, void* workspace, int max_samples,
+                             const float* theta, const uint8_t* pool, int first, int n_images,
+                             const float* lut, const float* running, int32_t* pred,
+                             flsim_stream_t stream);
+/* nn.BatchNorm2d's running update (momentum 0.1) for n_workers calls in worker order:
+ * r = 0.1 * stat + 0.9 * r per call, stat from bn_stats[w] (w = 0 .. n_workers-1). */
+int flsim_vgg11_bn_update_running(float* running, const float* bn_stats, int n_workers,
+                                  flsim_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
  * Fused server step: replaces Agg.rule = rule() (main.py:23-25, agents.py:43-45: per-tensor
  * torch.stack(weight_ups).mean(0)) + Central.update_model (agents.py:9-21: Adam step,
  * main.py:106).  weight_ups = c copies of S (the aliased fast entries) followed by n_stale stale
