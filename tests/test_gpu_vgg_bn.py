@@ -201,7 +201,6 @@ def test_vgg_bn_simulation_matches_oracle_trajectory(pool):
     losses within the fp32 tolerance, running buffers advanced over every computing worker."""
     from flsim.sim import FLSimulation
     from oracle import model_ref as MR
-    from test_oracle_golden import _check_running
     n, d, ep = 3, 2, 4
     osim = MR.OracleSim(n, delay=d, throttle=True, pool=pool, model=M)
     gsim = FLSimulation(n, delay=d, throttle=True, device=DEV, chunk_workers=2, pool=pool, model=M)
@@ -214,8 +213,19 @@ def test_vgg_bn_simulation_matches_oracle_trajectory(pool):
         assert [i for (_, i, _) in tr_o["items"]] == list(np.nonzero(plan.computes)[0])
         assert [s for (k, s) in tr_o["appended"] if k == "stale"] == [s for (_, s) in plan.stale]
         assert abs(lg - lo) <= (1e-4, 2e-3, 5e-3, 1e-2)[t], (t, lg, lo)
+        if t == 0:      # every call of epoch 0 ran on theta_0: the buffers agree tightly
+            np.testing.assert_allclose(gsim.engine.running.double().cpu().numpy(),
+                                       osim.bn.flat(), rtol=1e-5, atol=1e-6)
     assert gsim.engine.num_batches_tracked == osim.bn.num_batches_tracked
-    _check_running(gsim.engine.running.double().cpu().numpy(), osim.bn.flat(), rv_rtol=1e-4)
+    # after several epochs the buffers follow two (legitimately) different trajectories --
+    # statistical agreement only (Adam's first steps move every weight by ~lr whatever the
+    # gradient's size, i.e. ~5 % of a VGG conv weight's init std, in the direction of sign(g)): the
+    # conv biases (noise-driven, +-lr per Adam step, see _check_running) enter running_mean
+    # directly, and the weights differ at the trajectory tolerance.  The per-call update itself
+    # is checked at 1e-5 (single-step and facade tests, tests/test_oracle_golden).
+    # calibration: the oracle's own fp32 vs fp64-gradient runs differ by rel-L2 5e-8 / 8e-5 /
+    # 4.4e-3 / 1.0e-2 in the buffers after epochs 0-3 (theta: 4e-4 ... 5.3e-3); GPU: 2.2e-2
+    assert _rel_l2(gsim.engine.running.double().cpu().numpy(), osim.bn.flat()) < 5e-2
     # the state dict loads into the models.py module (main.py:98-100 / 192-194 round trip)
     from FL.models import vgg11_bn
     sd = gsim.model_state_dict()
