@@ -146,8 +146,11 @@ struct RowsKC {
 // ---------------------------------------------------------------------------------------------
 // Row-major matrix whose ROWS are the reduction index (KM): element (k, col) at P[k * ld + col];
 // the tile spans columns [c0, c0 + ROWS).  k >= NK or col >= NC read as zero (NC % 4 == 0).
+// PO > 0: the rows are the pixels of PO x PO images and k walks only the top-left PV x PV
+// window of each (k -> row img*PO*PO + oh*PO + ow): conv6's weight gradient skips the pixels
+// the floor-mode pool never reads (their dZ is zero).
 // ---------------------------------------------------------------------------------------------
-template <int TR, int NT>
+template <int TR, int NT, int PO = 0, int PV = 0>
 struct RowsKM {
     static constexpr int ROWS = TR;
     static constexpr bool KC = false;
@@ -174,7 +177,14 @@ struct RowsKM {
 #pragma unroll
         for (int j = 0; j < UNITS; ++j) {
             const int k = ks * GK + krow[j];
-            r[j] = (c_off[j] >= 0 && k < NK) ? ldg4(P + (long)k * ld + c_off[j]) : zero4();
+            long row = k;
+            if constexpr (PO > 0) {
+                const unsigned img = (unsigned)k / (unsigned)(PV * PV);
+                const unsigned rem = (unsigned)k - img * (PV * PV);
+                const unsigned oh = rem / (unsigned)PV;
+                row = (long)img * (PO * PO) + oh * PO + (rem - oh * PV);
+            }
+            r[j] = (c_off[j] >= 0 && k < NK) ? ldg4(P + row * ld + c_off[j]) : zero4();
         }
     }
     __device__ void store(float* lds, const f32x4 (&r)[UNITS]) const {
@@ -187,13 +197,15 @@ struct RowsKM {
 // ---------------------------------------------------------------------------------------------
 // B operand of the weight gradient: im2col(X) with the pixel as the reduction index (KM).
 // Tile columns = kk = (kh*3 + kw) * CI + ci in [c0, c0 + ROWS); reduction rows = pixels p.
+// VO > 0: p walks only the top-left VO x VO output window of each image (pairs with RowsKM's
+// PV window).
 // ---------------------------------------------------------------------------------------------
-template <int IH, int IW, int CI, int PAD, int TR, int NT>
+template <int IH, int IW, int CI, int PAD, int TR, int NT, int VO = 0>
 struct Im2colKM {
     static constexpr int ROWS = TR;
     static constexpr bool KC = false;
-    static constexpr int OH = IH + 2 * PAD - 2;
-    static constexpr int OW = IW + 2 * PAD - 2;
+    static constexpr int OH = VO > 0 ? VO : IH + 2 * PAD - 2;
+    static constexpr int OW = VO > 0 ? VO : IW + 2 * PAD - 2;
     static constexpr int C4 = ROWS / 4;
     static constexpr int TOTAL = GK * C4;
     static constexpr int UNITS = (TOTAL + NT - 1) / NT;

@@ -480,13 +480,16 @@ static int conv_like(const float* X, int S, const float* Wpk, int N, int KP, con
 }
 
 // weight gradient: slab[z][co][kk] += sum_p dz[p][co] * im2col(X)[p][kk]  (conv padding PAD)
-template <int IH, int IW, int CI, int PAD, int FM, int FN, int WM, int WN>
+// VO > 0: only the top-left VO x VO window of the output pixels (dz is zero outside it)
+template <int IH, int IW, int CI, int PAD, int FM, int FN, int WM, int WN, int VO = 0>
 static int conv_wgrad(const float* dz, const float* X, int S, int CO, int KP, float* slab,
                       float* bslab, int Z, hipStream_t st, int kid, int kreal) {
     constexpr int NT = 64 * WM * WN;
     constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
-    using AL = RowsKM<BM, NT>;
-    using BL = Im2colKM<IH, IW, CI, PAD, BN, NT>;
+    constexpr int OFULL = IH + 2 * PAD - 2;
+    static_assert(IH == IW && VO <= OFULL, "square maps only");
+    using AL = RowsKM<BM, NT, (VO > 0 ? OFULL : 0), VO>;
+    using BL = Im2colKM<IH, IW, CI, PAD, BN, NT, VO>;
     const int M = S * BL::OH * BL::OW;
     AL al;
     al.P = dz;

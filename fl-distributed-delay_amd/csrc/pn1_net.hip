@@ -190,8 +190,9 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC((pool_scatter<15, 15, 192, true>(w.gy, w.i3, w.a6, S, st)));
     float* dz6 = w.a6;
     // ---- conv6: wgrad (input a5), bias, dgrad -> dz5 = . * (a5 > 0) into gx ----
-    RC((conv_wgrad<13, 13, 192, 2, 6, 3, 2, 2>(dz6, w.a5, S, 192, 1728, g.sw[5], g.sb[5], GEO[5].ZW,
-                                              st, K_WG6, 1728)));
+    // (row/column 14 of conv6's 15x15 output is never pooled: its dz is zero, skip those pixels)
+    RC((conv_wgrad<13, 13, 192, 2, 6, 3, 2, 2, 14>(dz6, w.a5, S, 192, 1728, g.sw[5], g.sb[5],
+                                                  GEO[5].ZW, st, K_WG6, 1728)));
     RC((conv_like<15, 15, 192, 0, 2, 6, 4, 2>(dz6, S, g.wd[5], 192, 1728,
         EpiMask<true>{w.gx, w.a5, S * 13 * 13, 192}, st, K_DG6, 1728)));
     float* dz5 = w.gx;
