@@ -427,8 +427,84 @@ k_fin_sum(const float* __restrict__ slab, int Z, long n, int zl, float* __restri
     }
 }
 
+// Large slabs (n % 4 == 0, n >= 64K): one wave per z-lane, so each wave reads 1 KB contiguous
+// per slab, and four slabs in flight per thread (partials u = 0..3 take z = tz + (4j + u) * 4,
+// added in u order): fixed order, deterministic.  (Template only for one definition per TU.)
+template <int V>
+__global__ void __launch_bounds__(256)
+k_fin_sum_wide(const float* __restrict__ slab, int Z, long n, float* __restrict__ out, int CO,
+               int CI, int CIP, int KP) {
+    __shared__ f32x4 red[256];
+    const int tx = threadIdx.x & 63, tz = threadIdx.x >> 6;
+    const long e0 = ((long)blockIdx.x * 64 + tx) * 4;
+    f32x4 acc[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] = zero4();
+    if (e0 < n) {
+        const float* p = slab + e0;
+        int z = tz;
+        for (; z + 12 < Z; z += 16) {
+            f32x4 x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) x[u] = *reinterpret_cast<const f32x4*>(p + (long)(z + 4 * u) * n);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                acc[u].x += x[u].x;
+                acc[u].y += x[u].y;
+                acc[u].z += x[u].z;
+                acc[u].w += x[u].w;
+            }
+        }
+        for (int u = 0; z < Z; z += 4, ++u) {
+            const f32x4 x = *reinterpret_cast<const f32x4*>(p + (long)z * n);
+            acc[u].x += x.x;
+            acc[u].y += x.y;
+            acc[u].z += x.z;
+            acc[u].w += x.w;
+        }
+    }
+    f32x4 t = acc[0];
+#pragma unroll
+    for (int u = 1; u < 4; ++u) {
+        t.x += acc[u].x;
+        t.y += acc[u].y;
+        t.z += acc[u].z;
+        t.w += acc[u].w;
+    }
+    red[threadIdx.x] = t;
+    __syncthreads();
+    if (tz != 0 || e0 >= n) return;
+#pragma unroll
+    for (int j = 1; j < 4; ++j) {
+        const f32x4 y = red[j * 64 + tx];
+        t.x += y.x;
+        t.y += y.y;
+        t.z += y.z;
+        t.w += y.w;
+    }
+    const float tv[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        const long s = e0 + v;
+        if (CO > 0) {
+            const int co = (int)(s / KP);
+            const int k = (int)(s - (long)co * KP);
+            const int khkw = k / CIP, ci = k - (k / CIP) * CIP;
+            if (khkw < 9 && ci < CI) out[((long)co * CI + ci) * 9 + khkw] = tv[v];
+        } else {
+            out[s] = tv[v];
+        }
+    }
+}
+
 static int fin_sum(const float* slab, int Z, long n, float* out, hipStream_t st, int CO = 0,
                    int CI = 0, int CIP = 1, int KP = 1) {
+    if (n % 4 == 0 && n >= 65536 && Z >= 4) {
+        hipLaunchKernelGGL(k_fin_sum_wide<4>, dim3(ceil_div(n, 256L)), dim3(256), 0, st, slab, Z, n,
+                           out, CO, CI, CIP, KP);
+        FLSIM_LAUNCH_CHECK();
+        return 0;
+    }
     int zl = 1;
     while (zl < Z && zl < 16) zl *= 2;
     const int cols = 256 / zl;

@@ -234,14 +234,20 @@ int main(int argc, char** argv) {
     if (want(tag)) { conv_fwd_glds<IH, CI, PAD, FM, FN, WM, WN>(tag, X, W, b, Y2, S, CO, K, zp); \
                      conv_fwd<IH, CI, PAD, FM, FN, WM, WN>(tag, X, W, b, Y, S, CO, K); \
                      check_same(Y2, Y, (size_t)S * (IH + 2 * PAD - 2) * (IH + 2 * PAD - 2) * CO, tag); }
-    FG("fwd6 128x192", 13, 192, 2, 192, 1728, 2, 6, 4, 2)
-    FG("fwd6 128x96", 13, 192, 2, 192, 1728, 4, 3, 2, 2)
-    FG("fwd6 256x96", 13, 192, 2, 192, 1728, 4, 3, 4, 2)
-    FG("fwd4 256x96", 20, 96, 2, 96, 864, 4, 3, 4, 2)
-    FG("fwd4 128x96", 20, 96, 2, 96, 864, 4, 3, 2, 2)
-    FG("dg6 128x192", 15, 192, 0, 192, 1728, 2, 6, 4, 2)
-    FG("dg4 256x96", 22, 96, 0, 96, 864, 4, 3, 4, 2)
-    FG("fwd2 256x48", 34, 48, 2, 48, 432, 2, 3, 8, 1)
-    FG("dg2 256x48", 36, 48, 0, 48, 432, 2, 3, 8, 1)
+    // weight-gradient tile sweep (conv2: CO 48, 9*CI 432; conv3: CO 96, 9*CI 432)
+    G("wg2 48x144 z2048 (current)", 34, 48, 48, 2048, 432, 3, 3, 1, 3)
+    G("wg2 48x144 z4096", 34, 48, 48, 4096, 432, 3, 3, 1, 3)
+    G("wg2 48x144 z1024", 34, 48, 48, 1024, 432, 3, 3, 1, 3)
+    G("wg2 48x432 z2048", 34, 48, 48, 2048, 432, 3, 9, 1, 3)
+    G("wg2 48x432 z4096", 34, 48, 48, 4096, 432, 3, 9, 1, 3)
+    G("wg2 48x144 w3m z2048", 34, 48, 48, 2048, 432, 1, 9, 3, 1)
+    G("wg2 48x144 1w z2048", 34, 48, 48, 2048, 432, 3, 9, 1, 1)
+    G("wg2 48x48 1w z4096", 34, 48, 48, 4096, 432, 3, 3, 1, 1)
+    G("wg3 96x96 z1024 (current)", 18, 48, 96, 1024, 432, 3, 3, 2, 2)
+    G("wg3 96x96 z2048", 18, 48, 96, 2048, 432, 3, 3, 2, 2)
+    G("wg3 96x144 z1024", 18, 48, 96, 1024, 432, 3, 3, 2, 3)
+    G("wg3 96x432 z1024", 18, 48, 96, 1024, 432, 3, 9, 2, 3)
+    G("wg3 96x144 3w z1024", 18, 48, 96, 1024, 432, 6, 3, 1, 3)
+    G("wg3 96x48 z2048", 18, 48, 96, 2048, 432, 3, 3, 2, 1)
     return 0;
 }
