@@ -93,6 +93,28 @@ static void conv_wgrad(const char* tag, const float* dz, const float* X, float* 
 }
 
 
+// conv6-style weight gradient over the top-left VO x VO output window (product: conv_wgrad VO)
+template <int IH, int CI, int FM, int FN, int WM, int WN, int VO>
+static void conv_wgrad_vo(const char* tag, const float* dz, const float* X, float* slab,
+                          float* bslab, int S, int CO, int Z, int kreal) {
+    constexpr int NT = 64 * WM * WN, BM = 16 * FM * WM, BN = 16 * FN * WN;
+    constexpr int OFULL = IH + 2;
+    using AL = RowsKM<BM, NT, OFULL, VO>;
+    using BL = Im2colKM<IH, IH, CI, 2, BN, NT, VO>;
+    const int M = S * VO * VO;
+    const int KP = (9 * CI + 15) / 16 * 16;
+    AL al;
+    al.P = dz;
+    al.ld = CO;
+    al.NK = M;
+    al.NC = CO;
+    BL bl;
+    bl.X = X;
+    bl.M = M;
+    EpiSlabAcc epi{slab, CO, KP, (long)CO * KP, bslab};
+    time_gemm<FM, FN, WM, WN>(tag, al, bl, epi, CO, KP, ceil_div(M, GK), Z, 2.0 * M * CO * kreal);
+}
+
 template <int FM, int FN, int WM, int WN, int KSUB, int PRIO, int MINW, int MODE = 0, class AL, class BL, class EPI>
 static double time_gemm_v(const char* tag, const AL& al, const BL& bl, const EPI& epi, int M, int N,
                           int ksteps, int Z, double flops) {
@@ -234,20 +256,18 @@ int main(int argc, char** argv) {
     if (want(tag)) { conv_fwd_glds<IH, CI, PAD, FM, FN, WM, WN>(tag, X, W, b, Y2, S, CO, K, zp); \
                      conv_fwd<IH, CI, PAD, FM, FN, WM, WN>(tag, X, W, b, Y, S, CO, K); \
                      check_same(Y2, Y, (size_t)S * (IH + 2 * PAD - 2) * (IH + 2 * PAD - 2) * CO, tag); }
-    // weight-gradient tile sweep (conv2: CO 48, 9*CI 432; conv3: CO 96, 9*CI 432)
-    G("wg2 48x144 z2048 (current)", 34, 48, 48, 2048, 432, 3, 3, 1, 3)
-    G("wg2 48x144 z4096", 34, 48, 48, 4096, 432, 3, 3, 1, 3)
-    G("wg2 48x144 z1024", 34, 48, 48, 1024, 432, 3, 3, 1, 3)
-    G("wg2 48x432 z2048", 34, 48, 48, 2048, 432, 3, 9, 1, 3)
-    G("wg2 48x432 z4096", 34, 48, 48, 4096, 432, 3, 9, 1, 3)
-    G("wg2 48x144 w3m z2048", 34, 48, 48, 2048, 432, 1, 9, 3, 1)
-    G("wg2 48x144 1w z2048", 34, 48, 48, 2048, 432, 3, 9, 1, 1)
-    G("wg2 48x48 1w z4096", 34, 48, 48, 4096, 432, 3, 3, 1, 1)
-    G("wg3 96x96 z1024 (current)", 18, 48, 96, 1024, 432, 3, 3, 2, 2)
-    G("wg3 96x96 z2048", 18, 48, 96, 2048, 432, 3, 3, 2, 2)
-    G("wg3 96x144 z1024", 18, 48, 96, 1024, 432, 3, 3, 2, 3)
-    G("wg3 96x432 z1024", 18, 48, 96, 1024, 432, 3, 9, 2, 3)
-    G("wg3 96x144 3w z1024", 18, 48, 96, 1024, 432, 6, 3, 1, 3)
-    G("wg3 96x48 z2048", 18, 48, 96, 2048, 432, 3, 3, 2, 1)
+#define G14(tag, Z, FM, FN, WM, WN) \
+    if (want(tag)) conv_wgrad_vo<13, 192, FM, FN, WM, WN, 14>(tag, Y, X, slab, bsl, S, 192, Z, 1728);
+    // conv6 weight gradient (14x14 window): tile sweep
+    G14("wg6 192x96 4w z128 (current)", 128, 6, 3, 2, 2)
+    G14("wg6 192x96 4w z64", 64, 6, 3, 2, 2)
+    G14("wg6 192x96 4w z256", 256, 6, 3, 2, 2)
+    G14("wg6 192x96 8w 48x48", 128, 3, 3, 4, 2)
+    G14("wg6 192x96 4w 48x96", 128, 3, 6, 4, 1)
+    G14("wg6 192x96 6w 64x48", 128, 4, 3, 3, 2)
+    G14("wg6 192x48 2w", 128, 6, 3, 2, 1)
+    G14("wg6 96x96 4w", 128, 3, 3, 2, 2)
+    G14("wg6 192x192 8w 96x48", 128, 6, 3, 2, 4)
+    G14("wg6 192x144 6w", 128, 6, 3, 2, 3)
     return 0;
 }
