@@ -70,6 +70,9 @@ def parse():
                     help="worker-steps in the CPU sample (~10-30 s of host work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI). gloo is for "
+                         "rehearsing the N > 1 path with several ranks on one GPU (slow collective)")
     return ap.parse_args()
 
 
@@ -112,10 +115,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         raise SystemExit(f"--gpus {args.gpus} != WORLD_SIZE {world}")
+    if args.backend == "gloo":   # rehearsal: ranks may share the box's GPU(s)
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        torch.distributed.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=dev)
+        else:
+            torch.distributed.init_process_group("gloo")
     from flsim._lib import KernelProbe
     from flsim.sim import FLSimulation
 
@@ -205,7 +213,7 @@ def main():
                                    f"128 samples/worker-step, Adam lr 1e-3",
                        "executed_worker_steps": ws, "chunk_workers": args.chunk,
                        "parallelism": f"workers sharded over {world} GPU(s), "
-                                      f"{'1 RCCL all-reduce/step' if world > 1 else 'no collective'}"},
+                                      f"{'1 RCCL all-reduce/step' if world > 1 and args.backend == 'nccl' else '1 gloo all-reduce/step (rehearsal)' if world > 1 else 'no collective'}"},
             "mfma_efficiency_whole_step": round(value * flop_per_ws / 1e12 /
                                                 (MFMA_F32_PEAK_TFLOPS * world), 4),
             "roofline": roofline,
