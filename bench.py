@@ -68,6 +68,9 @@ def parse():
                          "--model vgg11 --n_workers 4096 --delay 1000) or vgg11_bn")
     ap.add_argument("--cpu-sample", type=int, default=160,
                     help="worker-steps in the CPU sample (~10-30 s of host work)")
+    ap.add_argument("--model_file", type=str, default=None,
+                    help="warm start (main.py:98-100): a models.py state_dict, e.g. configs[1]'s "
+                         "warm_start.pt from tools/make_warm_start.py")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
@@ -125,15 +128,20 @@ def main():
         else:
             torch.distributed.init_process_group("gloo")
     from flsim._lib import KernelProbe
-    from flsim.sim import FLSimulation
+    from flsim.sim import FLSimulation, load_model_file
 
+    theta0 = buffers = None
+    if args.model_file:
+        theta0, buffers = load_model_file(args.model_file, args.model)
     throttle = not args.no_throttle
     delays = None
     if args.delays == "heterogeneous":
         from flsim.schedule import heterogeneous_delays
         delays = heterogeneous_delays(args.n_workers)
     sim = FLSimulation(args.n_workers, delay=args.delay, delays=delays, throttle=throttle,
-                       chunk_workers=args.chunk, device=dev, model=args.model)
+                       chunk_workers=args.chunk, device=dev, model=args.model, theta0=theta0)
+    if buffers:
+        sim.engine.load_buffers(buffers)
     flop_per_ws = sim.engine.FLOP_PER_WORKER_STEP
     for _ in range(args.warmup):
         sim.epoch(sync_loss=False)
@@ -204,8 +212,10 @@ def main():
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f32",
-            "data": f"synthetic: seeded CIFAR-shaped u8 pool in HBM, models.py-init "
-                    f"{args.model} (no network for CIFAR10)",
+            "data": f"synthetic: seeded CIFAR-shaped u8 pool in HBM, "
+                    + (f"{args.model} warm-started from {os.path.basename(args.model_file)}"
+                       if args.model_file else f"models.py-init {args.model}")
+                    + " (no network for CIFAR10)",
             "config": {"workload": f"FL server epochs, n_workers={args.n_workers}, "
                                    + (f"delay={args.delay}" if delays is None else
                                       "heterogeneous delays (configs[3] spec)")

@@ -37,6 +37,19 @@ def default_theta(seed=0, model="PerformantNet1"):
     return torch.cat([p.detach().reshape(-1) for p in m.parameters()])
 
 
+def load_model_file(path, model="PerformantNet1"):
+    """--model_file (main.py:49-50,98-100): `model.load_state_dict(torch.load(path))` on the
+    models.py module, then the flat theta0 in named_parameters order and the module's buffers
+    (vgg11_bn running statistics; empty for the others).  The file is a plain state_dict, so it
+    is read with weights_only=True; a missing or mismatched key raises load_state_dict's
+    RuntimeError exactly as the reference would."""
+    from FL import models
+    m = getattr(models, model)()
+    m.load_state_dict(torch.load(path, map_location="cpu", weights_only=True))
+    theta0 = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+    return theta0, dict(m.named_buffers())
+
+
 class FLSimulation:
     def __init__(self, n_workers, delay=100, delays=None, throttle=False, lr=1e-3, seed=0,
                  semantics="reference", dropout=True, chunk_workers=32, device=None, theta0=None,

@@ -73,15 +73,11 @@ def main(argv=None):
     if world > 1:
         torch.distributed.init_process_group("nccl", device_id=dev)
     rank = torch.distributed.get_rank() if world > 1 else 0
-    from flsim.sim import FLSimulation, default_theta
+    from flsim.sim import FLSimulation, default_theta, load_model_file
     theta0 = default_theta(args.seed, args.model)
     buffers = None
     if args.model_file is not None:                       # main.py:98-100
-        from FL import models
-        m = getattr(models, args.model)()
-        m.load_state_dict(torch.load(args.model_file, map_location="cpu", weights_only=True))
-        theta0 = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
-        buffers = dict(m.named_buffers())                 # vgg11_bn running statistics
+        theta0, buffers = load_model_file(args.model_file, args.model)
     if rank == 0:
         print(dev)
     pool = test_pool = None

@@ -220,6 +220,32 @@ def test_simulation_matches_oracle_trajectory(pool, thr):
     assert drift_gpu <= 6 * drift_cpu + 1e-3, (drift_gpu, drift_cpu)
 
 
+def test_warm_start_model_file_trajectory(pool, tmp_path):
+    """configs[1]'s --model_file warm start: a pre-trained state_dict (written by the engine's
+    model_state_dict, as tools/make_warm_start.py does) loaded through load_model_file starts
+    the GPU run and the oracle at the same theta; same trace, losses within the trajectory
+    tolerance."""
+    from flsim.sim import FLSimulation, load_model_file
+    from oracle import model_ref as MR
+    pre = FLSimulation(4, delay=2, throttle=True, seed=1, device=DEV, chunk_workers=2, pool=pool)
+    for _ in range(3):
+        pre.epoch()
+    path = str(tmp_path / "warm_start.pt")
+    torch.save(pre.model_state_dict(), path)
+    theta0, _ = load_model_file(path)
+    assert torch.equal(theta0, pre.theta.cpu()[:theta0.numel()])
+    n, d = 4, 2
+    osim = MR.OracleSim(n, delay=d, throttle=True, pool=pool, theta0=theta0.numpy())
+    gsim = FLSimulation(n, delay=d, throttle=True, device=DEV, chunk_workers=2, pool=pool,
+                        theta0=theta0)
+    for t in range(4):
+        lo = osim.epoch()
+        lg = gsim.epoch()
+        assert [i for (_, i, _) in osim.trace[-1]["items"]] == \
+            list(np.nonzero(gsim.trace[-1].computes)[0])
+        assert abs(lg - lo) <= (1e-4 if t == 0 else 1e-3), (t, lg, lo)
+
+
 def test_reference_api_facade_loop(pool):
     """The reference's own loop structure (main.py:126-188) written against the drop-in FL.agents
     API (Worker.fwd_bkwd / Agg(rule) / Central.update_model), fed the spec's batches, against

@@ -75,3 +75,30 @@ def test_test_split_spec_matches_oracle():
     tr, _ = O.make_pool(3, size=2000)
     assert not np.array_equal(a, tr)         # independent noise from the train split
     assert np.bincount(la, minlength=10).tolist() == [200] * 10
+
+
+@pytest.mark.parametrize("model", ["PerformantNet1", "vgg11_bn"])
+def test_model_file_warm_start_loads_state_dict(tmp_path, model):
+    """--model_file (main.py:98-100): a torch.save'd models.py state_dict becomes theta0 in
+    named_parameters order plus the module buffers; a wrong key set fails like load_state_dict."""
+    from FL import models
+    from flsim.sim import load_model_file
+    torch.manual_seed(3)
+    m = getattr(models, model)()
+    with torch.no_grad():
+        for b in m.buffers():
+            if b.is_floating_point():
+                b.uniform_(0.5, 1.5)
+    path = str(tmp_path / "warm_start.pt")
+    torch.save(m.state_dict(), path)
+    theta0, bufs = load_model_file(path, model)
+    want = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+    assert torch.equal(theta0, want)
+    assert set(bufs) == {k for k, _ in m.named_buffers()}
+    for k, b in m.named_buffers():
+        assert torch.equal(bufs[k], b)
+    sd = m.state_dict()
+    sd.pop(next(iter(sd)))
+    torch.save(sd, path)
+    with pytest.raises(RuntimeError):
+        load_model_file(path, model)
