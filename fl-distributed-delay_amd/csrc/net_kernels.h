@@ -131,11 +131,61 @@ k_pool_scatter(const float* __restrict__ gy, const uint8_t* __restrict__ idx,
     }
 }
 
+// NCHW gy (the pool feeding linear1 through torch's C,H,W flatten): one block per sample.  The
+// sample's gy plane set (C * PH * PW floats, contiguous) is read into LDS with coalesced float4
+// loads, then the (window, 4 channels) threads pick their four channels from LDS, so neither
+// side of the transpose makes strided global accesses.
+template <int H, int W, int C>
+__global__ void __launch_bounds__(256)
+k_pool_scatter_nchw(const float* __restrict__ gy, const uint8_t* __restrict__ idx,
+                    float* __restrict__ dz) {
+    constexpr int PH = H / 2, PW = W / 2, PP = PH * PW;
+    constexpr int CH = (H + 1) / 2, CW = (W + 1) / 2;
+    constexpr int C4 = C / 4;
+    static_assert((C * PP) % 4 == 0, "float4 staging");
+    __shared__ __attribute__((aligned(16))) float sg[C * PP];
+    const int n = blockIdx.x;
+    const f32x4* src = reinterpret_cast<const f32x4*>(gy + (long)n * C * PP);
+    for (int i = threadIdx.x; i < C * PP / 4; i += 256)
+        reinterpret_cast<f32x4*>(sg)[i] = src[i];
+    __syncthreads();
+    for (int e = threadIdx.x; e < CH * CW * C4; e += 256) {
+        const int c = 4 * (e % C4);
+        const int cell = e / C4;
+        const int cw = cell % CW, ch = cell / CW;
+        f32x4 g = f32x4{0.f, 0.f, 0.f, 0.f};
+        uint32_t id = 0xffffffffu;
+        if (ch < PH && cw < PW) {
+            id = *reinterpret_cast<const uint32_t*>(idx + (((long)n * PH + ch) * PW + cw) * C + c);
+            const float* b = sg + c * PP + ch * PW + cw;
+            g.x = b[0];
+            g.y = b[PP];
+            g.z = b[2 * PP];
+            g.w = b[3 * PP];
+        }
+#pragma unroll
+        for (int pos = 0; pos < 4; ++pos) {
+            const int h = 2 * ch + (pos >> 1), w = 2 * cw + (pos & 1);
+            if (h >= H || w >= W) continue;
+            f32x4 v;
+            v.x = ((id & 0xff) == (uint32_t)pos) ? g.x : 0.f;
+            v.y = (((id >> 8) & 0xff) == (uint32_t)pos) ? g.y : 0.f;
+            v.z = (((id >> 16) & 0xff) == (uint32_t)pos) ? g.z : 0.f;
+            v.w = ((id >> 24) == (uint32_t)pos) ? g.w : 0.f;
+            *reinterpret_cast<f32x4*>(dz + (((long)n * H + h) * W + w) * C + c) = v;
+        }
+    }
+}
+
 template <int H, int W, int C, bool NCHW_G>
 static int pool_scatter(const float* gy, const uint8_t* idx, float* dz, int S, hipStream_t st) {
-    const long total = (long)S * ((H + 1) / 2) * ((W + 1) / 2) * (C / 4);
-    hipLaunchKernelGGL((k_pool_scatter<H, W, C, NCHW_G>), dim3(ceil_div(total, 256)), dim3(256), 0,
-                       st, gy, idx, dz, total);
+    if constexpr (NCHW_G) {
+        hipLaunchKernelGGL((k_pool_scatter_nchw<H, W, C>), dim3(S), dim3(256), 0, st, gy, idx, dz);
+    } else {
+        const long total = (long)S * ((H + 1) / 2) * ((W + 1) / 2) * (C / 4);
+        hipLaunchKernelGGL((k_pool_scatter<H, W, C, false>), dim3(ceil_div(total, 256)), dim3(256),
+                           0, st, gy, idx, dz, total);
+    }
     FLSIM_LAUNCH_CHECK();
     return 0;
 }
