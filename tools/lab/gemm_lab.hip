@@ -269,5 +269,17 @@ int main(int argc, char** argv) {
     G14("wg6 96x96 4w", 128, 3, 3, 2, 2)
     G14("wg6 192x192 8w 96x48", 128, 6, 3, 2, 4)
     G14("wg6 192x144 6w", 128, 6, 3, 2, 3)
+    // conv2 / conv3 weight gradients: deeper LDS stages (KSUB), issue priority, occupancy hint
+    G("wgv2 base 48x144 z2048", 34, 48, 48, 2048, 432, 3, 3, 1, 3)
+    GV("wgv2 ks2", 34, 48, 48, 2048, 432, 3, 3, 1, 3, 2, 0, 1)
+    GV("wgv2 ks2 prio", 34, 48, 48, 2048, 432, 3, 3, 1, 3, 2, 1, 1)
+    GV("wgv2 ks1 prio", 34, 48, 48, 2048, 432, 3, 3, 1, 3, 1, 1, 1)
+    GV("wgv2 ks4", 34, 48, 48, 2048, 432, 3, 3, 1, 3, 4, 0, 1)
+    GV("wgv2 ks2 z1024", 34, 48, 48, 1024, 432, 3, 3, 1, 3, 2, 0, 1)
+    GV("wgv2 ks2 6w 96x144", 34, 48, 48, 2048, 432, 3, 3, 2, 3, 2, 0, 1)
+    G("wgv3 base 96x96 z1024", 18, 48, 96, 1024, 432, 3, 3, 2, 2)
+    GV("wgv3 ks2", 18, 48, 96, 1024, 432, 3, 3, 2, 2, 2, 0, 1)
+    GV("wgv3 ks2 prio", 18, 48, 96, 1024, 432, 3, 3, 2, 2, 2, 1, 1)
+    GV("wgv3 ks4", 18, 48, 96, 1024, 432, 3, 3, 2, 2, 4, 0, 1)
     return 0;
 }
