@@ -61,7 +61,9 @@ def parse():
     ap.add_argument("--delays", choices=["reference", "heterogeneous"], default="reference",
                     help="reference: one slow worker (n-1) with --delay; heterogeneous: configs[3] "
                          "spec (10%% slow workers, geometric delays up to 1000)")
-    ap.add_argument("--chunk", type=int, default=32, help="workers per worker-batched launch")
+    ap.add_argument("--chunk", type=int, default=128,
+                    help="workers per worker-batched launch (128 = 16,384 samples, the largest the "
+                         "32-bit index budget allows; fastest for every model, profiles/r01e)")
     ap.add_argument("--model", choices=["PerformantNet1", "vgg11", "vgg11_bn"],
                     default="PerformantNet1",
                     help="PerformantNet1 (main.py:97, the metric's model), vgg11 (configs[4]: "

@@ -52,7 +52,7 @@ def load_model_file(path, model="PerformantNet1"):
 
 class FLSimulation:
     def __init__(self, n_workers, delay=100, delays=None, throttle=False, lr=1e-3, seed=0,
-                 semantics="reference", dropout=True, chunk_workers=32, device=None, theta0=None,
+                 semantics="reference", dropout=True, chunk_workers=128, device=None, theta0=None,
                  group=None, max_throttle=32, pool=None, betas=(0.9, 0.999), eps=1e-8,
                  engine=None, device_pool=None, test_pool=None, model="PerformantNet1"):
         if semantics not in SEMANTICS:
@@ -80,8 +80,9 @@ class FLSimulation:
             torch.device("cuda", torch.cuda.current_device())
         # engine / device_pool are injectable only so tests can drive the sharding and
         # collective logic with a CPU stand-in (gloo); the product path always builds PN1Engine
+        # a chunk never needs more workers than the run has (the workspace scales with it)
         self.engine = engine if engine is not None else \
-            engine_class(model)(self.device, chunk_workers)
+            engine_class(model)(self.device, min(int(chunk_workers), self.n))
         self.pool = device_pool if device_pool is not None else \
             DevicePool(self.device, self.seed, pool)
         self.sched = Schedule(self.n, self.delays, self.throttle, max_throttle)

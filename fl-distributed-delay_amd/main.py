@@ -44,7 +44,8 @@ def parse(argv=None):
     p.add_argument('--semantics', default='reference', choices=['reference', 'torch1'],
                    help='stale entry = S_{t-d} (torch>=2 aliasing) or zeros (torch 1.x)')
     p.add_argument('--no-dropout', action='store_true')
-    p.add_argument('--chunk', type=int, default=32, help='workers per worker-batched launch')
+    p.add_argument('--chunk', type=int, default=128,
+                   help='workers per worker-batched launch (max 128 = 16,384 samples)')
     p.add_argument('--model', default='PerformantNet1', choices=['PerformantNet1', 'vgg11', 'vgg11_bn'],
                    help='models.py network (main.py:97 builds PerformantNet1; vgg11 = configs[4]; '
                         'vgg11_bn = models.py:106-108)')

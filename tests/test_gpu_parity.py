@@ -518,3 +518,33 @@ def test_heterogeneous_delays_trajectory(pool):
         assert [s for (kd, s) in tr_o["appended"] if kd == "stale"] == [s for (_, s) in plan.stale]
         if not np.isnan(lo):
             assert abs(lg - lo) <= (1e-4 if t == 0 else 1e-3), (t, lg, lo)
+
+
+def test_max_chunk_matches_small_chunks(pool):
+    """The largest worker-batched launch (128 workers = 16,384 samples, the 32-bit index budget)
+    against 4 launches of 32 from the same theta and batches: the forward does not depend on the
+    chunking, so every worker's loss is bit-identical; S_t differs only by the split-K slab
+    order (rel-L2 <= 1e-5 per tensor)."""
+    from flsim.engine import PN1_SHAPES
+    from flsim.sim import FLSimulation
+    n = 129                                   # epoch 1: the 128 fast workers, no tick
+    a = FLSimulation(n, delay=50, throttle=False, device=DEV, chunk_workers=32, pool=pool)
+    b = FLSimulation(n, delay=50, throttle=False, device=DEV, chunk_workers=128, pool=pool)
+    a.epoch()
+    b.epoch()
+    for x, y in ((b.theta, a.theta), (b.m, a.m), (b.v, a.v)):
+        x.copy_(y)
+    assert b.chunks(0, 128) == [(0, 128)]
+    la, lb = a.epoch(), b.epoch()
+    assert int(a.trace[-1].computes.sum()) == 128
+    assert la == lb
+    wa = a.comm[a.Ppad:a.Ppad + 128].cpu().numpy()
+    wb = b.comm[b.Ppad:b.Ppad + 128].cpu().numpy()
+    assert np.array_equal(wa.view(np.uint32), wb.view(np.uint32))
+    sa = a.comm[:a.P].cpu().numpy().astype(np.float64)
+    sb = b.comm[:b.P].cpu().numpy().astype(np.float64)
+    off = 0
+    for (name, _), size in zip(PN1_SHAPES, _sizes()):
+        r = _rel_l2(sb[off:off + size], sa[off:off + size])
+        assert r <= 1e-5, (name, r)
+        off += size
