@@ -350,10 +350,32 @@ extern "C" {
 
 // tensor_sizes: numel of each parameter tensor in named_parameters order (the cascade's column
 // rule is per tensor).  stale[i] == nullptr means a zero entry (torch-1.x stale semantics).
+static int aggregate_adam_impl(const float* S, int c, const float* const* stale, int n_stale,
+                               int divisor, float* p, float* m, float* v, long P,
+                               const long* tensor_sizes, int n_tensors, long step, double lr,
+                               double beta1, double beta2, double eps, hipStream_t stream);
+
 int flsim_aggregate_adam(const float* S, int c, const float* const* stale, int n_stale,
                          float* p, float* m, float* v, long P, const long* tensor_sizes,
                          int n_tensors, long step, double lr, double beta1, double beta2,
                          double eps, hipStream_t stream) {
+    return aggregate_adam_impl(S, c, stale, n_stale, c + n_stale, p, m, v, P, tensor_sizes,
+                               n_tensors, step, lr, beta1, beta2, eps, stream);
+}
+
+// independent-entry semantics: S already holds the sum of the k distinct entries
+int flsim_aggregate_adam_sum(const float* S, int k, float* p, float* m, float* v, long P,
+                             const long* tensor_sizes, int n_tensors, long step, double lr,
+                             double beta1, double beta2, double eps, hipStream_t stream) {
+    FLSIM_REQUIRE(k > 0, "empty weight_ups (reference: IndexError in rule, main.py:25)");
+    return aggregate_adam_impl(S, 1, nullptr, 0, k, p, m, v, P, tensor_sizes, n_tensors, step, lr,
+                               beta1, beta2, eps, stream);
+}
+
+static int aggregate_adam_impl(const float* S, int c, const float* const* stale, int n_stale,
+                               int divisor, float* p, float* m, float* v, long P,
+                               const long* tensor_sizes, int n_tensors, long step, double lr,
+                               double beta1, double beta2, double eps, hipStream_t stream) {
     FLSIM_REQUIRE(S && p && m && v && tensor_sizes, "null pointer");
     FLSIM_REQUIRE(c >= 0 && n_stale >= 0 && n_stale <= MAX_STALE, "bad entry counts c=%d ns=%d", c,
                   n_stale);
@@ -382,9 +404,10 @@ int flsim_aggregate_adam(const float* S, int c, const float* const* stale, int n
         cq = cq < 0 ? 0 : (cq > sz ? sz : cq);
         A.rs[q] = make_casc(cq, sz, 4 * cq + q - c);
     }
-    A.fk = (float)k;
+    FLSIM_REQUIRE(divisor > 0 && divisor < (1 << 24), "divisor %d out of range", divisor);
+    A.fk = (float)divisor;                         // rule(): mean = sum / k
     {
-        volatile float one = 1.f, fk = (float)k;   // RN(1/k) in fp32, not via double
+        volatile float one = 1.f, fk = (float)divisor;   // RN(1/k) in fp32, not via double
         A.rk = one / fk;
     }
     const double bc1 = 1.0 - pow(beta1, (double)step);

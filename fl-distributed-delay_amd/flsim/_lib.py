@@ -26,7 +26,8 @@ EXPORTS = [
     "flsim_vgg11_bn_stats_per_worker", "flsim_vgg11_bn_begin_epoch",
     "flsim_vgg11_bn_fwd_bwd_chunk", "flsim_vgg11_bn_fwd_bwd_input", "flsim_vgg11_bn_end_epoch",
     "flsim_vgg11_bn_eval_pool", "flsim_vgg11_bn_update_running",
-    "flsim_aggregate_adam", "flsim_aggregate_adam_seq", "flsim_probe_enable", "flsim_probe_read", "flsim_probe_disable",
+    "flsim_aggregate_adam", "flsim_aggregate_adam_seq", "flsim_aggregate_adam_sum",
+    "flsim_probe_enable", "flsim_probe_read", "flsim_probe_disable",
     "flsim_probe_kernel_count", "flsim_probe_kernel_name",
 ]
 
@@ -81,6 +82,9 @@ def lib():
     L.flsim_vgg11_bn_update_running.argtypes = [vp, vp, ctypes.c_int, vp]
     L.flsim_aggregate_adam.argtypes = [
         vp, ctypes.c_int, vp, ctypes.c_int, vp, vp, vp, ctypes.c_long, vp, ctypes.c_int,
+        ctypes.c_long, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp]
+    L.flsim_aggregate_adam_sum.argtypes = [
+        vp, ctypes.c_int, vp, vp, vp, ctypes.c_long, vp, ctypes.c_int,
         ctypes.c_long, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp]
     L.flsim_aggregate_adam_seq.argtypes = [
         vp, ctypes.c_int, vp, ctypes.c_int, vp, ctypes.c_int, vp, vp, vp, ctypes.c_long, vp,

@@ -170,6 +170,9 @@ class NetEngine:
         """stale: list of device tensors (or None = zero entry)."""
         aggregate_adam(S, c, stale, theta, m, v, step, self.SIZES, lr, betas, eps)
 
+    def aggregate_adam_sum(self, S, k, theta, m, v, step, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
+        aggregate_adam_sum(S, k, theta, m, v, step, self.SIZES, lr, betas, eps)
+
     def aggregate_adam_seq(self, S, k, events, arrays, theta, m, v, step, lr=1e-3,
                            betas=(0.9, 0.999), eps=1e-8):
         aggregate_adam_seq(S, k, events, arrays, theta, m, v, step, self.SIZES, lr, betas, eps)
@@ -273,6 +276,15 @@ def aggregate_adam(S, c, stale, theta, m, v, step, sizes, lr=1e-3, betas=(0.9, 0
     csz = (ctypes.c_long * len(sizes))(*[int(n) for n in sizes])
     check(lib().flsim_aggregate_adam(
         ptr(S), int(c), arr, ns, ptr(theta), ptr(m), ptr(v), sum(int(n) for n in sizes), csz, len(sizes),
+        int(step), float(lr), float(betas[0]), float(betas[1]), float(eps), stream_ptr()))
+
+
+def aggregate_adam_sum(S, k, theta, m, v, step, sizes, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
+    """Independent-entry semantics: S = the sum of the k distinct weight_ups entries; mean = S / k
+    then the same Adam step (flsim_aggregate_adam_sum)."""
+    csz = (ctypes.c_long * len(sizes))(*[int(n) for n in sizes])
+    check(lib().flsim_aggregate_adam_sum(
+        ptr(S), int(k), ptr(theta), ptr(m), ptr(v), sum(int(n) for n in sizes), csz, len(sizes),
         int(step), float(lr), float(betas[0]), float(betas[1]), float(eps), stream_ptr()))
 
 

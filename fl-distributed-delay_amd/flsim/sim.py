@@ -25,7 +25,7 @@ from .data import DevicePool, make_test_pool
 from .engine import PN1_SIZES, engine_class, padded, split_views
 from .schedule import Schedule, reference_delays
 
-SEMANTICS = ("reference", "torch1")
+SEMANTICS = ("reference", "torch1", "independent")
 
 
 def default_theta(seed=0, model="PerformantNet1"):
@@ -98,6 +98,8 @@ class FLSimulation:
         # [S_t | losses of the computing workers | their per-call BatchNorm statistics (vgg11_bn)]
         # -- one all-reduce per epoch when world > 1 (each rank fills only its workers' rows)
         self.nstat = int(getattr(self.engine, "STATS_PER_WORKER", 0))
+        if self.nstat and semantics == "independent":
+            raise NotImplementedError("independent entries with BatchNorm models")
         self.stats_off = self.Ppad + padded(self.n)
         self.comm = torch.zeros(self.stats_off + self.n * self.nstat, device=self.device)
         self.stale_store = {}     # epoch -> [slot tensor, refcount]
@@ -177,6 +179,8 @@ class FLSimulation:
         if t >= 1 and self.delay_arg == 0 and self.delays[self.n - 1] == 0:
             raise ZeroDivisionError("integer division or modulo by zero")   # main.py:158
         ks = self.rs.randint(0, self.n, size=self.n)
+        if self.semantics == "independent":
+            return self._epoch_independent(plan, ks, sync_loss)
         active = np.nonzero(plan.computes)[0]
         lo, hi = self.shard(active)
         eng = self.engine
@@ -245,6 +249,59 @@ class FLSimulation:
         self.loss_log.append((losses.detach().clone(), fast_pos))
         return None
 
+    def _epoch_independent(self, plan, ks, sync_loss):
+        """Independent-entry semantics: every weight_ups entry is a distinct
+        per-worker gradient and a slow worker's FIFO holds its own gradient.  A slow worker's
+        gradient is computed and kept by its owner rank (worker index mod world); the fast
+        workers are sharded as usual.  Each rank adds the stale gradients it owns to its partial
+        sum, so the one all-reduce combines the partial sums of all k entries; mean = sum / k,
+        then the same Adam step, replicated."""
+        t = plan.t
+        eng = self.engine
+        active = np.nonzero(plan.computes)[0]
+        slow_mask = self.delays[active] != 0
+        fast, slow = active[~slow_mask], active[slow_mask]
+        own_slow = np.asarray([i for i in slow if int(i) % self.world == self.rank], np.int64)
+        lo, hi = self.shard(fast)
+        S = self.comm[:self.P]
+        losses = self.comm[self.Ppad:self.Ppad + len(fast)]
+        if self.world > 1:
+            losses.zero_()
+        wt = self._worker_table(t, np.concatenate([own_slow, fast[lo:hi]]), ks)
+        if not hasattr(self, "_slow_loss"):
+            self._slow_loss = torch.zeros(1, device=self.device)
+        ns = len(own_slow)
+        for j, i in enumerate(own_slow):           # the slow worker's own gradient (FIFO push)
+            eng.begin_epoch(self.theta)
+            eng.run_chunk(self.theta, self.pool, wt[j:j + 1], 1, self.n, self.seed, self.dropout,
+                          self._slow_loss)
+            slot = self._slot()
+            eng.end_epoch(slot[:self.P])
+            self.stale_store[(int(i), t)] = slot
+        eng.begin_epoch(self.theta)
+        for c0, c1 in self.chunks(lo, hi):
+            eng.run_chunk(self.theta, self.pool, wt[ns + c0 - lo:ns + c1 - lo], c1 - c0, self.n,
+                          self.seed, self.dropout, losses[c0:c1])
+        eng.end_epoch(S)
+        for (i, src) in plan.stale:                 # popped entries, added by their owner rank
+            if int(i) % self.world == self.rank:
+                slot = self.stale_store.pop((int(i), int(src)))
+                S.add_(slot[:self.P])
+                self.free_slots.append(slot)
+        if self.world > 1:
+            torch.distributed.all_reduce(self.comm[:self.Ppad + len(fast)], group=self.group)
+        self.step += 1
+        eng.aggregate_adam_sum(S, len(fast) + len(plan.stale), self.theta, self.m, self.v,
+                               self.step, self.lr, self.betas, self.eps)
+        self.trace.append(plan)
+        if sync_loss:
+            lv = losses.detach().cpu().numpy()
+            val = float(np.mean(lv.astype(np.float32))) if len(lv) else float("nan")
+            self.loss_log.append(val)
+            return val
+        self.loss_log.append((losses.detach().clone(), np.arange(len(fast))))
+        return None
+
     def losses(self):
         out = []
         for e in self.loss_log:
@@ -299,6 +356,8 @@ class FLSimulation:
         """Everything needed to continue bit-for-bit: theta, Adam m/v/step, the epoch counter,
         the FIFO'd stale gradients still referenced, the loss log.  The schedule and the numpy
         k-draws are deterministic scans and are replayed on restore."""
+        if self.semantics == "independent":
+            raise NotImplementedError("checkpoint of the independent-entry semantics")
         return {
             "format": "flsim-checkpoint-1",
             "config": {"n": self.n, "delays": torch.from_numpy(self.delays.copy()),

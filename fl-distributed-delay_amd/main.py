@@ -41,8 +41,9 @@ def parse(argv=None):
     p.add_argument('--throttle', action='store_true', help='gradient throttling')
     # build flags
     p.add_argument('--seed', type=int, default=0)
-    p.add_argument('--semantics', default='reference', choices=['reference', 'torch1'],
-                   help='stale entry = S_{t-d} (torch>=2 aliasing) or zeros (torch 1.x)')
+    p.add_argument('--semantics', default='reference', choices=['reference', 'torch1', 'independent'],
+                   help='stale entry = S_{t-d} (torch>=2 aliasing), zeros (torch 1.x) or the slow '
+                        "worker's own gradient with distinct per-worker entries (independent)")
     p.add_argument('--no-dropout', action='store_true')
     p.add_argument('--chunk', type=int, default=128,
                    help='workers per worker-batched launch (max 128 = 16,384 samples)')

@@ -165,6 +165,14 @@ int flsim_aggregate_adam(const float* S, int c, const float* const* stale, int n
                          int n_tensors, long step, double lr, double beta1, double beta2,
                          double eps, flsim_stream_t stream);
 
+/* Independent-entry semantics (every weight_ups entry a distinct per-worker
+ * gradient, the stale one the slow worker's own gradient from step t - d): S = the sum of the k
+ * entries (the fast workers' gradients plus the popped stale gradients, already combined across
+ * ranks by the one all-reduce), then mean = S / k (fp32) and the same Adam step. */
+int flsim_aggregate_adam_sum(const float* S, int k, float* p, float* m, float* v, long P,
+                             const long* tensor_sizes, int n_tensors, long step, double lr,
+                             double beta1, double beta2, double eps, flsim_stream_t stream);
+
 /* General entry order (the heterogeneous-delay extension of main.py:150-166, SURVEY 8 a1: every
  * worker with a delay is a slow worker with its own FIFO; weight_ups is appended in worker-index
  * order, so popped entries sit among the S_t copies).  k entries; events = device int32

@@ -276,7 +276,9 @@ def fwd_bkwd(params, x, y, noise, fwd=forward):
 
 
 class OracleSim:
-    """main.py:126-188 restated on CPU, reference (torch>=2 aliasing) or torch1 semantics."""
+    """main.py:126-188 restated on CPU, reference (torch>=2 aliasing), torch1 (stale = zeros) or
+    independent semantics (every weight_ups entry a distinct per-worker gradient; a slow worker's
+    FIFO holds its own gradient; rule() is the same per-tensor stack-mean, main.py:23-25)."""
 
     def __init__(self, n, delay=None, delays=None, throttle=False, seed=0, dtype=torch.float32,
                  semantics="reference", dropout=True, pool=None, lr=1e-3, theta0=None,
@@ -348,6 +350,8 @@ class OracleSim:
         t, n = self.t, self.n
         ks = self.rs.randint(0, n, size=n)
         items, fast_losses_idx, appended = [], [], []
+        ent_src = []                  # independent: ("item", j) or ("own", worker, source epoch)
+        pushed_own = {}               # independent: (worker, t) -> item index
         for i in range(n):
             if self.delays[i] != 0:
                 self.gone = False
@@ -356,16 +360,20 @@ class OracleSim:
                 if t == 0:
                     items.append((t, i, int(ks[i])))
                     self.fifo[i].append(t)
+                    pushed_own[(i, t)] = len(items) - 1
                 elif t % d == 0:
                     items.append((t, i, int(ks[i])))
                     self.fifo[i].append(t)
+                    pushed_own[(i, t)] = len(items) - 1
                     popped = self.fifo[i].pop(0)
                 if popped is not None:
                     appended.append(("stale", popped))
+                    ent_src.append(("own", i, popped))
                     self.gone = True
             else:
                 if self.window <= 0:
                     fast_losses_idx.append(len(items))
+                    ent_src.append(("item", len(items)))
                     items.append((t, i, int(ks[i])))
                     appended.append(("fast", t))
                     if self.throttle:
@@ -376,6 +384,17 @@ class OracleSim:
                 self.window -= 1
         if not appended:
             raise IndexError("list index out of range")   # rule(): ups_list[0] (main.py:25)
+        if self.semantics == "independent":
+            per = [self.grad_of(self.theta, [it]) for it in items]
+            gi = [g.astype(np.float32) for g, _ in per]
+            losses = [ls[0] for _, ls in per]
+            if not hasattr(self, "own"):
+                self.own = {}
+            for key, j in pushed_own.items():
+                self.own[key] = gi[j]
+            entries = [gi[e[1]] if e[0] == "item" else self.own.pop((e[1], e[2])) for e in ent_src]
+            S = np.sum(np.stack(gi), 0).astype(np.float32) if gi else None
+            return self._finish(t, entries, S, losses, fast_losses_idx, items, appended)
         S, losses = self.grad_of(self.theta, items)
         S = S.astype(np.float32)
         entries = []
@@ -390,7 +409,11 @@ class OracleSim:
             self.ring[t] = S
         live = {src for q in self.fifo.values() for src in q}     # entries a FIFO still holds
         self.ring = {src: a for src, a in self.ring.items() if src in live}
-        g = np.empty_like(S)
+        return self._finish(t, entries, S, losses, fast_losses_idx, items, appended)
+
+    def _finish(self, t, entries, S, losses, fast_losses_idx, items, appended):
+        """rule() over the weight_ups entries + Adam + loss logging (main.py:184-188)."""
+        g = np.empty_like(entries[0])
         off = 0
         for _, shp in _shapes(self.model):                # rule() is per parameter tensor
             nel = int(np.prod(shp))

@@ -46,6 +46,9 @@ class StandInEngine:
                 tot = tot + s[:P]
         theta -= lr * tot / (c + len(stale))
 
+    def aggregate_adam_sum(self, S, k, theta, m, v, step, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
+        theta -= lr * S / k
+
     def aggregate_adam_seq(self, S, k, events, arrays, theta, m, v, step, lr=1e-3,
                            betas=(0.9, 0.999), eps=1e-8):
         tot = S * (k - len(events))
@@ -55,7 +58,7 @@ class StandInEngine:
         theta -= lr * tot / k
 
 
-def _run(rank, world, n, d, thr, epochs, out, port, delays=None):
+def _run(rank, world, n, d, thr, epochs, out, port, delays=None, semantics="reference"):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, os.path.dirname(here))
@@ -65,7 +68,7 @@ def _run(rank, world, n, d, thr, epochs, out, port, delays=None):
         os.environ["MASTER_PORT"] = str(port)
         dist.init_process_group("gloo", rank=rank, world_size=world)
     from flsim.sim import FLSimulation
-    sim = FLSimulation(n, delay=d, delays=delays, throttle=thr, device="cpu",
+    sim = FLSimulation(n, delay=d, delays=delays, throttle=thr, device="cpu", semantics=semantics,
                        engine=StandInEngine(), device_pool=object(), theta0=torch.zeros(P))
     losses = [sim.epoch() for _ in range(epochs)]
     res = dict(theta=sim.theta.numpy().copy(), losses=losses,
@@ -89,6 +92,31 @@ def test_two_rank_sharding_matches_single(thr, delays):
     port = 29500 + (os.getpid() % 1000) + (7 if delays else 0) + (3 if thr else 0)
     procs = [ctx.Process(target=_run, args=(r, 2, n, d, thr, epochs, out, port, delays))
              for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+        assert p.exitcode == 0
+    for r in range(2):
+        assert out[r]["trace"] == single[0]["trace"]
+        np.testing.assert_allclose(out[r]["losses"], single[0]["losses"], rtol=0, atol=1e-6)
+        np.testing.assert_allclose(out[r]["theta"], single[0]["theta"], rtol=1e-5, atol=1e-7)
+    assert np.array_equal(out[0]["theta"], out[1]["theta"])
+
+
+@pytest.mark.parametrize("delays", [None, [0, 2, 0, 0, 3, 0, 0, 2, 0, 0, 0]])
+def test_two_rank_independent_entries_match_single(delays):
+    """Independent-entry semantics: each slow worker's own gradient stays on its owner rank
+    (index mod world) and is added to that rank's partial sum before the one all-reduce."""
+    n, d, epochs = 11, 3, 8
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
+    single = mgr.dict()
+    _run(0, 1, n, d, True, epochs, single, 0, delays, "independent")
+    out = mgr.dict()
+    port = 29500 + (os.getpid() % 1000) + 13 + (5 if delays else 0)
+    procs = [ctx.Process(target=_run, args=(r, 2, n, d, True, epochs, out, port, delays,
+                                            "independent")) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:

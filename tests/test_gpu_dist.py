@@ -20,7 +20,7 @@ from conftest import has_gpu
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not has_gpu(), reason="needs an MI355X")]
 
 
-def _sim_run(model, n, d, epochs, world, rank, port, out):
+def _sim_run(model, n, d, epochs, world, rank, port, out, semantics="reference"):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, os.path.dirname(here))
@@ -33,7 +33,7 @@ def _sim_run(model, n, d, epochs, world, rank, port, out):
     from oracle import oracle as O
     from flsim.sim import FLSimulation
     sim = FLSimulation(n, delay=d, throttle=True, device="cuda:0", chunk_workers=2,
-                       pool=O.make_pool(0), model=model)
+                       pool=O.make_pool(0), model=model, semantics=semantics)
     losses = [sim.epoch()]
     run0 = sim.engine.running.cpu().numpy().copy() if hasattr(sim.engine, "running") else None
     losses += [sim.epoch() for _ in range(epochs - 1)]
@@ -47,17 +47,20 @@ def _sim_run(model, n, d, epochs, world, rank, port, out):
     out[rank] = res
 
 
-def _child(rank, world, model, n, d, epochs, port, out):
-    _sim_run(model, n, d, epochs, world, rank, port, out)
+def _child(rank, world, model, n, d, epochs, port, out, semantics="reference"):
+    _sim_run(model, n, d, epochs, world, rank, port, out, semantics)
 
 
-@pytest.mark.parametrize("model,n,d,epochs", [("PerformantNet1", 7, 2, 4), ("vgg11_bn", 5, 2, 3)])
-def test_two_rank_sharding_on_gpu(model, n, d, epochs):
+@pytest.mark.parametrize("model,n,d,epochs,semantics", [
+    ("PerformantNet1", 7, 2, 4, "reference"), ("vgg11_bn", 5, 2, 3, "reference"),
+    # the slow worker's own gradients stay on its owner rank (6 mod 2 = rank 0)
+    ("PerformantNet1", 7, 2, 5, "independent")])
+def test_two_rank_sharding_on_gpu(model, n, d, epochs, semantics):
     ctx = mp.get_context("spawn")
     with ctx.Manager() as mgr:
         out = mgr.dict()
         port = 29500 + os.getpid() % 1000
-        procs = [ctx.Process(target=_child, args=(r, 2, model, n, d, epochs, port, out))
+        procs = [ctx.Process(target=_child, args=(r, 2, model, n, d, epochs, port, out, semantics))
                  for r in range(2)]
         for p in procs:
             p.start()
@@ -66,7 +69,8 @@ def test_two_rank_sharding_on_gpu(model, n, d, epochs):
         assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
         two = [dict(out[0]), dict(out[1])]
         single = mgr.dict()
-        p1 = ctx.Process(target=_child, args=(0, 1, model, n, d, epochs, port + 1, single))
+        p1 = ctx.Process(target=_child, args=(0, 1, model, n, d, epochs, port + 1, single,
+                                              semantics))
         p1.start()
         p1.join(240)
         assert p1.exitcode == 0

@@ -548,3 +548,30 @@ def test_max_chunk_matches_small_chunks(pool):
         r = _rel_l2(sb[off:off + size], sa[off:off + size])
         assert r <= 1e-5, (name, r)
         off += size
+
+
+@pytest.mark.parametrize("thr", [False, True])
+def test_independent_entries_trajectory(pool, thr):
+    """Independent-entry semantics (distinct per-worker weight_ups entries; the slow worker's
+    FIFO holds its own gradient) against the oracle's per-worker restatement: same trace, losses
+    within the trajectory tolerance, parameter drift bounded by the CPU's own fp32 drift."""
+    from flsim.sim import FLSimulation
+    from oracle import model_ref as MR
+    n, d, ep = 4, 2, 5
+    osim = MR.OracleSim(n, delay=d, throttle=thr, pool=pool, semantics="independent")
+    gsim = FLSimulation(n, delay=d, throttle=thr, device=DEV, chunk_workers=2, pool=pool,
+                        semantics="independent")
+    for t in range(ep):
+        lo = osim.epoch()
+        lg = gsim.epoch()
+        assert [i for (_, i, _) in osim.trace[-1]["items"]] == \
+            list(np.nonzero(gsim.trace[-1].computes)[0])
+        assert abs(lg - lo) <= (1e-4 if t == 0 else 1e-3), (t, lg, lo)
+    o64 = MR.OracleSim(n, delay=d, throttle=thr, pool=pool, dtype=torch.float64,
+                       semantics="independent")
+    for t in range(ep):
+        o64.epoch()
+    th = gsim.theta.cpu().numpy().astype(np.float64)
+    drift_gpu = _rel_l2(th, o64.theta.astype(np.float64))
+    drift_cpu = _rel_l2(osim.theta.astype(np.float64), o64.theta.astype(np.float64))
+    assert drift_gpu <= 6 * drift_cpu + 1e-3, (drift_gpu, drift_cpu)
