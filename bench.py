@@ -70,6 +70,10 @@ def parse():
                          "--model vgg11 --n_workers 4096 --delay 1000) or vgg11_bn")
     ap.add_argument("--cpu-sample", type=int, default=160,
                     help="worker-steps in the CPU sample (~10-30 s of host work)")
+    ap.add_argument("--semantics", choices=["reference", "torch1", "independent"],
+                    default="reference",
+                    help="weight_ups entries: aliased S_t (the reference under torch 2.x), zero "
+                         "stale entries (torch 1.x) or distinct per-worker gradients")
     ap.add_argument("--model_file", type=str, default=None,
                     help="warm start (main.py:98-100): a models.py state_dict, e.g. configs[1]'s "
                          "warm_start.pt from tools/make_warm_start.py")
@@ -141,7 +145,8 @@ def main():
         from flsim.schedule import heterogeneous_delays
         delays = heterogeneous_delays(args.n_workers)
     sim = FLSimulation(args.n_workers, delay=args.delay, delays=delays, throttle=throttle,
-                       chunk_workers=args.chunk, device=dev, model=args.model, theta0=theta0)
+                       chunk_workers=args.chunk, device=dev, model=args.model, theta0=theta0,
+                       semantics=args.semantics)
     if buffers:
         sim.engine.load_buffers(buffers)
     flop_per_ws = sim.engine.FLOP_PER_WORKER_STEP
@@ -222,7 +227,9 @@ def main():
                                    + (f"delay={args.delay}" if delays is None else
                                       "heterogeneous delays (configs[3] spec)")
                                    + f", throttle={throttle}, {args.model}, "
-                                   f"128 samples/worker-step, Adam lr 1e-3",
+                                   + (f"{args.semantics} entries, "
+                                      if args.semantics != "reference" else "")
+                                   + "128 samples/worker-step, Adam lr 1e-3",
                        "executed_worker_steps": ws, "chunk_workers": args.chunk,
                        "parallelism": f"workers sharded over {world} GPU(s), "
                                       f"{'1 RCCL all-reduce/step' if world > 1 and args.backend == 'nccl' else '1 gloo all-reduce/step (rehearsal)' if world > 1 else 'no collective'}"},
