@@ -40,9 +40,11 @@ struct ConvGeo {
 // ZW (pixel splits of the weight gradient) sized so each wgrad launch has thousands of blocks:
 // several rounds of resident blocks on 256 CUs.  Tile shapes per layer were picked with
 // tools/lab/gemm_lab.hip on MI355X (4-wave wgrad tiles: a 6-wave block loads two SIMDs twice).
+// Splits re-swept at the 128-worker chunk (profiles/r01f/lab_wgrad_splits_s16384.txt): twice the
+// 4096-sample choice for conv2..6, 1-3 % faster each; the per-epoch slab sum reads 1.7 GB.
 static const ConvGeo GEO[6] = {
-    {3, 4, 48, 32, 48, 8192},    {48, 48, 48, 34, 432, 2048},   {48, 48, 96, 18, 432, 1024},
-    {96, 96, 96, 20, 864, 512},  {96, 96, 192, 11, 864, 256},  {192, 192, 192, 13, 1728, 128},
+    {3, 4, 48, 32, 48, 8192},    {48, 48, 48, 34, 432, 4096},   {48, 48, 96, 18, 432, 2048},
+    {96, 96, 96, 20, 864, 1024}, {96, 96, 192, 11, 864, 512},  {192, 192, 192, 13, 1728, 256},
 };
 static const long P_OFF[18] = {0,       1296,    1344,    22080,   22128,   63600,
                                63696,   146640,  146736,  312624,  312816,  644592,

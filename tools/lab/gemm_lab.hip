@@ -230,7 +230,7 @@ static void check_same(const float* Y, const float* Yref, size_t n, const char* 
 }
 
 int main(int argc, char** argv) {
-    const int S = 4096;
+    const int S = getenv("FLSIM_LAB_S") ? atoi(getenv("FLSIM_LAB_S")) : 4096;   // samples per chunk
     const size_t big = (size_t)S * 36 * 36 * 48;   // largest activation
     float* X = dalloc(big, 1.f);
     float* Y = dalloc(big, 0.f);
@@ -281,5 +281,22 @@ int main(int argc, char** argv) {
     GV("wgv3 ks2", 18, 48, 96, 1024, 432, 3, 3, 2, 2, 2, 0, 1)
     GV("wgv3 ks2 prio", 18, 48, 96, 1024, 432, 3, 3, 2, 2, 2, 1, 1)
     GV("wgv3 ks4", 18, 48, 96, 1024, 432, 3, 3, 2, 2, 4, 0, 1)
+    // split counts at the 128-worker chunk (FLSIM_LAB_S=16384): ZW is fixed per layer, so the
+    // K range per block grew 4x with the chunk
+    G("zs wg2 z2048", 34, 48, 48, 2048, 432, 3, 3, 1, 3)
+    G("zs wg2 z4096", 34, 48, 48, 4096, 432, 3, 3, 1, 3)
+    G("zs wg2 z8192", 34, 48, 48, 8192, 432, 3, 3, 1, 3)
+    G("zs wg3 z1024", 18, 48, 96, 1024, 432, 3, 3, 2, 2)
+    G("zs wg3 z2048", 18, 48, 96, 2048, 432, 3, 3, 2, 2)
+    G("zs wg3 z4096", 18, 48, 96, 4096, 432, 3, 3, 2, 2)
+    G("zs wg4 z512", 20, 96, 96, 512, 864, 3, 3, 2, 2)
+    G("zs wg4 z1024", 20, 96, 96, 1024, 864, 3, 3, 2, 2)
+    G("zs wg4 z2048", 20, 96, 96, 2048, 864, 3, 3, 2, 2)
+    G("zs wg5 z256", 11, 96, 192, 256, 864, 6, 3, 2, 2)
+    G("zs wg5 z512", 11, 96, 192, 512, 864, 6, 3, 2, 2)
+    G("zs wg5 z1024", 11, 96, 192, 1024, 864, 6, 3, 2, 2)
+    G14("zs wg6 z128", 128, 6, 3, 2, 2)
+    G14("zs wg6 z256", 256, 6, 3, 2, 2)
+    G14("zs wg6 z512", 512, 6, 3, 2, 2)
     return 0;
 }
