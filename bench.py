@@ -208,6 +208,12 @@ def main():
                    alg_bytes_per_launch=int(byts / cnt),
                    traffic=traffic["bytes_per_launch"] if traffic else None,
                    traffic_source=traffic["source"] if traffic else None)
+        if traffic and traffic.get("trace_avg_ns"):
+            # the same launch timed by the rocprofv3 kernel trace of that profile (no event
+            # packets around it): context for `achieved`, which stays the live measurement
+            rus = traffic["trace_avg_ns"] / 1e3
+            agg.update(rocprof_avg_launch_us=round(rus, 2),
+                       rocprof_frac=round(byts / cnt / (rus * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4))
 
     value = ws / elapsed
     cpu = None

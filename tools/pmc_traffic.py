@@ -4,7 +4,8 @@
 
 Reads <dir>/pmc_FETCH_SIZE/run_counter_collection.csv and <dir>/pmc_WRITE_SIZE/...csv, maps the
 template kernel names to the probe names bench.py reports, and writes
-{kernel: {"bytes_per_launch": B, "fetch": F, "write": W, "launches": n, "source": ...}}.
+{kernel: {"bytes_per_launch": B, "fetch": F, "write": W, "launches": n, "source": ...,
+"trace_avg_ns": T}} (T = the kernel-trace pass's average duration, when <dir>/trace has it).
 Units and corrections follow MI355X_MICROARCH.md (HBM section): FETCH_SIZE / WRITE_SIZE are in
 KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide streaming read, so it is doubled.
 """
@@ -60,6 +61,19 @@ def main():
                       launches=len(fetch[k]),
                       source=f"rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE, "
                              f"{os.path.basename(os.path.normpath(d))}")
+    stats = os.path.join(d, "trace", "run_kernel_stats.csv")
+    if os.path.exists(stats):
+        tot = {}
+        with open(stats) as f:
+            for r in csv.DictReader(f):
+                name = probe_name(r["Name"])
+                if name is None:
+                    continue
+                c, ns = tot.get(name, (0, 0.0))
+                tot[name] = (c + int(r["Calls"]), ns + float(r["TotalDurationNs"]))
+        for k, (c, ns) in tot.items():
+            if k in res and c:
+                res[k]["trace_avg_ns"] = ns / c
     for o in outs:
         os.makedirs(os.path.dirname(os.path.abspath(o)), exist_ok=True)
         with open(o, "w") as fh:
