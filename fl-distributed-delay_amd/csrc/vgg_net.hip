@@ -32,10 +32,10 @@ struct VConv {
     int ZW;              // weight-gradient pixel splits: thousands of blocks per launch
 };
 static const VConv VG[8] = {
-    {3, 4, 64, 32, 48, 2048},      {64, 64, 128, 16, 576, 256},
-    {128, 128, 256, 8, 1152, 128}, {256, 256, 256, 8, 2304, 64},
-    {256, 256, 512, 4, 2304, 32},  {512, 512, 512, 4, 4608, 16},
-    {512, 512, 512, 2, 4608, 16},  {512, 512, 512, 2, 4608, 16},
+    {3, 4, 64, 32, 48, 2048},      {64, 64, 128, 16, 576, 512},
+    {128, 128, 256, 8, 1152, 256}, {256, 256, 256, 8, 2304, 128},
+    {256, 256, 512, 4, 2304, 64},  {512, 512, 512, 4, 4608, 32},
+    {512, 512, 512, 2, 4608, 32},  {512, 512, 512, 2, 4608, 32},
 };
 constexpr int VFEAT = 512;   // classifier width
 constexpr int VZL = 16;      // classifier weight-gradient splits
