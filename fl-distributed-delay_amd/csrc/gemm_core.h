@@ -15,6 +15,8 @@
 // MFMA j consumes element j of that 4-vector, so A and B agree on which k each slot holds.
 // C/D: col = l&15, row = 4*(l>>4) + reg.
 #pragma once
+#include <type_traits>
+
 #include "common.h"
 
 namespace flsim {
@@ -87,6 +89,14 @@ constexpr int tile_floats() {
 // Epilogue concept:  void operator()(int m, int n, float v)   (m, n global; bounds checked inside)
 //                    or apply4(m0, n, f32x4) for 4 consecutive rows of one column.
 
+// Epilogues with STAGED = true write the block's whole BM x BN tile through LDS: the tile is
+// BN = the full output row width, so its rows are one contiguous range of the output and the
+// epilogue stores it with coalesced float4 writes instead of 64-byte column pieces.
+template <class E, class = void>
+struct IsStaged : std::false_type {};
+template <class E>
+struct IsStaged<E, std::void_t<decltype(E::STAGED)>> : std::bool_constant<E::STAGED> {};
+
 template <int FM, int FN, int WAVES_M, int WAVES_N, class AL, class BL, class EPI>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N)
 gemm_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, int tiles_m,
@@ -97,7 +107,12 @@ gemm_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, int t
     static_assert(BL::ROWS == BN, "B loader rows != BN");
     constexpr int A_FL = tile_floats<AL::KC, BM>();
     constexpr int B_FL = tile_floats<BL::KC, BN>();
-    __shared__ __attribute__((aligned(16))) float lds[2 * (A_FL + B_FL)];
+    constexpr bool STAGED = IsStaged<EPI>::value;
+    constexpr int STAGE_LD = BN + 4;   // row stride 4 (mod 64) banks: the 4 row groups of a
+                                       // wave's accumulator writes land on disjoint banks
+    constexpr int LDS_FL = 2 * (A_FL + B_FL) > (STAGED ? BM * STAGE_LD : 0)
+                               ? 2 * (A_FL + B_FL) : BM * STAGE_LD;
+    __shared__ __attribute__((aligned(16))) float lds[LDS_FL];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -195,15 +210,31 @@ gemm_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, int t
     if constexpr (EPI::ASUM) {
         if (tn == 0 && tid < BM) epi.asum(m0 + tid, tz, asum);
     }
-    // epilogue: lane holds rows 4*(lane>>4)+r, col lane&15 of each 16x16 tile
+    if constexpr (STAGED) {
+        static_assert(BN == EPI::NCOL, "staged epilogue needs the full row in one block");
+        __syncthreads();
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
+        for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) {
-            const int m = m0 + wm * 16 * FM + 16 * i + 4 * (lane >> 4);
-            const int n = n0 + wn * 16 * FN + 16 * j + (lane & 15);
-            epi.apply4(m, n, tz, acc[i][j]);
-        }
+            for (int j = 0; j < FN; ++j) {
+                const int ml = wm * 16 * FM + 16 * i + 4 * (lane >> 4);
+                const int nl = wn * 16 * FN + 16 * j + (lane & 15);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) lds[(ml + r) * STAGE_LD + nl] = epi.value(nl, acc[i][j][r]);
+            }
+        __syncthreads();
+        epi.store_rows(lds, STAGE_LD, m0, BM, tid, 64 * WAVES_M * WAVES_N);
+    } else {
+        // epilogue: lane holds rows 4*(lane>>4)+r, col lane&15 of each 16x16 tile
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+                const int m = m0 + wm * 16 * FM + 16 * i + 4 * (lane >> 4);
+                const int n = n0 + wn * 16 * FN + 16 * j + (lane & 15);
+                epi.apply4(m, n, tz, acc[i][j]);
+            }
+    }
 }
 
 }  // namespace flsim

@@ -286,6 +286,29 @@ struct EpiBiasRelu {
     }
 };
 
+// bias + ReLU staged through LDS (gemm_core.h STAGED): the block covers all NC output columns,
+// so its BM rows are one contiguous piece of Y written with float4 stores
+template <int NC>
+struct EpiBiasReluRows {
+    static constexpr bool ASUM = false;
+    static constexpr bool STAGED = true;
+    static constexpr int NCOL = NC;
+    static_assert(NC % 4 == 0, "float4 rows");
+    float* Y;
+    const float* bias;
+    int M;
+    __device__ float value(int n, float v) const { return fmaxf(v + bias[n], 0.f); }
+    __device__ void store_rows(const float* tile, int ld, int m0, int bm, int tid, int nt) const {
+        const int rows = M - m0 < bm ? M - m0 : bm;
+        constexpr int N4 = NC / 4;
+        f32x4* dst = reinterpret_cast<f32x4*>(Y + (long)m0 * NC);
+        for (int q = tid; q < rows * N4; q += nt) {
+            const int r = q / N4, c = q - r * N4;
+            dst[q] = *reinterpret_cast<const f32x4*>(tile + r * ld + 4 * c);
+        }
+    }
+};
+
 // conv forward + bias + ReLU + 2x2 max-pool + dropout (models.py:30-32 / 34-36 / 38-40), rows in
 // pool-window order (Im2colKC<..., WIN>): a lane's 4 accumulator rows are one pooling window of
 // one channel.  Writes the pooled, dropped output d (NHWC, or torch flatten order for NCHW_OUT)

@@ -144,7 +144,7 @@ static int forward(const GradState& g, const WS& w, const float* theta, int S,
                    const WorkerRec* workers, uint64_t seed, int dropout, hipStream_t st) {
     // conv1, conv2 (+ReLU)  models.py:29-30
     RC((conv_like<32, 32, 4, 2, 2, 3, 4, 1>(w.x0, S, g.wf[0], 48, 48,
-        EpiBiasRelu{w.a1, theta + P_OFF[1], S * 34 * 34, 48}, st, K_FWD1, 27)));
+        EpiBiasReluRows<48>{w.a1, theta + P_OFF[1], S * 34 * 34}, st, K_FWD1, 27)));
     // conv2 + ReLU + pool1 + dropout1 (models.py:30-32), one fused launch
     RC((conv_pool_fwd<34, 34, 48, 48, 2, 2, 3, 8, 1, false>(w.a1, S, g.wf[1], 432, w.d1, w.i1,
         theta + P_OFF[3], workers, seed, SITE_DROP1, THR_P25, SCALE_P25, dropout, st, K_FWD2,
