@@ -110,8 +110,16 @@ gemm_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, int t
     constexpr bool STAGED = IsStaged<EPI>::value;
     constexpr int STAGE_LD = BN + 4;   // row stride 4 (mod 64) banks: the 4 row groups of a
                                        // wave's accumulator writes land on disjoint banks
-    constexpr int LDS_FL = 2 * (A_FL + B_FL) > (STAGED ? BM * STAGE_LD : 0)
-                               ? 2 * (A_FL + B_FL) : BM * STAGE_LD;
+    // the staged tile goes out in passes of WM_PASS wave-rows (16 FM rows each) that fit the
+    // pipeline's own LDS footprint or 32 KB, whichever is larger (conv1: one pass in 26.6 KB,
+    // 1.23 vs 1.33 ms for two; conv2 data-grad: two passes in the pipeline's 38 KB)
+    constexpr int BASE_FL = 2 * (A_FL + B_FL);
+    constexpr int STAGE_BUDGET = BASE_FL > 8192 ? BASE_FL : 8192;
+    constexpr int WROWS = 16 * FM;
+    constexpr int WM_FIT = STAGE_BUDGET / (WROWS * STAGE_LD);
+    constexpr int WM_PASS = WM_FIT < 1 ? 1 : (WM_FIT > WAVES_M ? WAVES_M : WM_FIT);
+    constexpr int LDS_FL = STAGED && WM_PASS * WROWS * STAGE_LD > BASE_FL
+                               ? WM_PASS * WROWS * STAGE_LD : BASE_FL;
     __shared__ __attribute__((aligned(16))) float lds[LDS_FL];
 
     const int tid = threadIdx.x;
@@ -212,18 +220,27 @@ gemm_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, int t
     }
     if constexpr (STAGED) {
         static_assert(BN == EPI::NCOL, "staged epilogue needs the full row in one block");
-        __syncthreads();
+        constexpr int PASSES = (WAVES_M + WM_PASS - 1) / WM_PASS;
+#pragma unroll 1
+        for (int pass = 0; pass < PASSES; ++pass) {
+            __syncthreads();
+            if (wm / WM_PASS == pass) {
 #pragma unroll
-        for (int i = 0; i < FM; ++i)
+                for (int i = 0; i < FM; ++i)
 #pragma unroll
-            for (int j = 0; j < FN; ++j) {
-                const int ml = wm * 16 * FM + 16 * i + 4 * (lane >> 4);
-                const int nl = wn * 16 * FN + 16 * j + (lane & 15);
+                    for (int j = 0; j < FN; ++j) {
+                        const int ml = (wm - pass * WM_PASS) * WROWS + 16 * i + 4 * (lane >> 4);
+                        const int nl = wn * 16 * FN + 16 * j + (lane & 15);
 #pragma unroll
-                for (int r = 0; r < 4; ++r) lds[(ml + r) * STAGE_LD + nl] = epi.value(nl, acc[i][j][r]);
+                        for (int r = 0; r < 4; ++r)
+                            lds[(ml + r) * STAGE_LD + nl] = epi.value(nl, acc[i][j][r]);
+                    }
             }
-        __syncthreads();
-        epi.store_rows(lds, STAGE_LD, m0, BM, tid, 64 * WAVES_M * WAVES_N);
+            __syncthreads();
+            const int wm_hi = (pass + 1) * WM_PASS < WAVES_M ? (pass + 1) * WM_PASS : WAVES_M;
+            epi.store_rows(lds, STAGE_LD, m0 + pass * WM_PASS * WROWS,
+                           (wm_hi - pass * WM_PASS) * WROWS, tid, 64 * WAVES_M * WAVES_N);
+        }
     } else {
         // epilogue: lane holds rows 4*(lane>>4)+r, col lane&15 of each 16x16 tile
 #pragma unroll

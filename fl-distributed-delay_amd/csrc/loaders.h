@@ -376,6 +376,37 @@ struct EpiMask {
     }
 };
 
+// EpiMask<true> staged through LDS (gemm_core.h STAGED): float4 rows of the ReLU mask source
+// and of the output
+template <int NC>
+struct EpiMaskRows {
+    static constexpr bool ASUM = false;
+    static constexpr bool STAGED = true;
+    static constexpr int NCOL = NC;
+    static_assert(NC % 4 == 0, "float4 rows");
+    float* Y;
+    const float* act;
+    int M;
+    __device__ float value(int, float v) const { return v; }
+    __device__ void store_rows(const float* tile, int ld, int m0, int bm, int tid, int nt) const {
+        const int rows = M - m0 < bm ? M - m0 : bm;
+        constexpr int N4 = NC / 4;
+        f32x4* dst = reinterpret_cast<f32x4*>(Y + (long)m0 * NC);
+        const f32x4* a4 = reinterpret_cast<const f32x4*>(act + (long)m0 * NC);
+        for (int q = tid; q < rows * N4; q += nt) {
+            const int r = q / N4, c = q - r * N4;
+            const f32x4 t = *reinterpret_cast<const f32x4*>(tile + r * ld + 4 * c);
+            const f32x4 a = a4[q];
+            f32x4 o;
+            o.x = a.x > 0.f ? t.x : 0.f;
+            o.y = a.y > 0.f ? t.y : 0.f;
+            o.z = a.z > 0.f ? t.z : 0.f;
+            o.w = a.w > 0.f ? t.w : 0.f;
+            dst[q] = o;
+        }
+    }
+};
+
 // gradient of a dropout(relu(.)) output: Y = acc * scale * (act > 0)  (act = dropped output)
 struct EpiDropMask {
     static constexpr bool ASUM = false;

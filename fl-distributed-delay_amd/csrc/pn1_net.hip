@@ -222,7 +222,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC((conv_wgrad<34, 34, 48, 2, 3, 3, 1, 3>(dz2, w.a1, S, 48, 432, g.sw[1], g.sb[1], GEO[1].ZW,
                                              st, K_WG2, 432)));
     RC((conv_like<36, 36, 48, 0, 2, 3, 8, 1>(dz2, S, g.wd[1], 48, 432,
-        EpiMask<true>{w.gx, w.a1, S * 34 * 34, 48}, st, K_DG2, 432)));
+        EpiMaskRows<48>{w.gx, w.a1, S * 34 * 34}, st, K_DG2, 432)));
     float* dz1 = w.gx;
     // ---- conv1: wgrad (input x0), bias ----
     // (3 waves of 16 rows each: 0.272 vs 0.325 ms for one 48x48 wave, profiles/r01c/lab_conv1.txt)
