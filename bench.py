@@ -68,8 +68,11 @@ def parse():
                     default="PerformantNet1",
                     help="PerformantNet1 (main.py:97, the metric's model), vgg11 (configs[4]: "
                          "--model vgg11 --n_workers 4096 --delay 1000) or vgg11_bn")
-    ap.add_argument("--cpu-sample", type=int, default=160,
-                    help="worker-steps in the CPU sample (~10-30 s of host work)")
+    ap.add_argument("--configs0-epochs", type=int, default=3,
+                    help="epochs of configs[0] (n=10, d=50) timed by the CPU baseline")
+    ap.add_argument("--no-tick-window", action="store_true",
+                    help="do not pre-roll untimed epochs to put the first tick (t = delay) and the "
+                         "epoch after it inside the timed window")
     ap.add_argument("--semantics", choices=["reference", "torch1", "independent"],
                     default="reference",
                     help="weight_ups entries: aliased S_t (the reference under torch 2.x), zero "
@@ -85,20 +88,57 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(n, delay, throttle, n_ws, model="PerformantNet1"):
-    """The oracle's CPU port of the reference loop (torch CPU, all host cores of this job): the
-    first n_ws fwd_bkwd of epoch 0 (agents.py:32-40, sequential, accumulating), then rule()
-    (torch.stack(...).mean(0) per tensor, main.py:23-25) over those entries and one Adam step
-    (agents.py:9-21).  Returns executed worker-steps / s."""
+def host_cpu_info():
+    """CPU model, logical CPUs this job may run on, the cgroup CPU quota, and the physical cores
+    among the allowed CPUs; threads = the physical cores (capped by the quota when one is set)."""
+    aff = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else \
+        list(range(os.cpu_count() or 1))
+    model, phys, cur = None, set(), {}
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f.read().split("\n") + [""]:
+                if not line.strip():
+                    if cur.get("processor") is not None and int(cur["processor"]) in set(aff):
+                        phys.add((cur.get("physical id", "0"), cur.get("core id", cur["processor"])))
+                    cur = {}
+                    continue
+                k, _, v = line.partition(":")
+                cur[k.strip()] = v.strip()
+                if k.strip() == "model name" and model is None:
+                    model = v.strip()
+    except OSError:
+        pass
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    cores = len(phys) or len(aff)
+    threads = cores if quota is None else max(1, min(cores, int(quota)))
+    return dict(cpu_model=model, logical_cpus_allowed=len(aff), physical_cores_allowed=cores,
+                cgroup_cpu_quota=quota, omp_num_threads=os.environ.get("OMP_NUM_THREADS"),
+                threads=threads)
+
+
+def cpu_baseline(n, delay, throttle, model="PerformantNet1", configs0_epochs=3):
+    """The oracle's CPU port of the reference loop on this host's cores:
+      1. one FULL epoch 0 of the bench workload: every computing worker's fwd_bkwd
+         (agents.py:32-40, sequential, accumulating into the shared gradient), rule() =
+         torch.stack(entries).mean(0) per tensor over the aliased entries (main.py:23-25) and one
+         torch.optim.Adam step (agents.py:9-21) -> executed worker-steps / s;
+      2. configs[0]: n = 10, delay 50, no throttle, the port's whole server loop for a few epochs
+         -> per-epoch time and worker-steps / s."""
     from oracle import model_ref as MR
     from oracle import oracle as O
-    threads = min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
+    info = host_cpu_info()
+    torch.set_num_threads(info["threads"])
     pool = O.make_pool(0)
     sim = MR.OracleSim(n, delay=delay, throttle=throttle, pool=pool, model=model)
     sched = O.schedule(n, O.reference_delays(n, delay), throttle, 1)
     ks = O.worker_k_sequence(0, n, 1)[0]
-    active = np.nonzero(sched.computes[0])[0][:n_ws]
+    active = np.nonzero(sched.computes[0])[0]
     items = [(0, int(i), int(ks[i])) for i in active]
     params = [torch.tensor(a, requires_grad=True) for a in MR.split_flat(sim.theta, model)]
     opt = torch.optim.Adam(params, lr=1e-3)
@@ -106,15 +146,31 @@ def cpu_baseline(n, delay, throttle, n_ws, model="PerformantNet1"):
     t0 = time.perf_counter()
     g, _ = sim.grad_of(sim.theta, items)
     gl = [torch.from_numpy(a) for a in MR.split_flat(g, model)]
-    fin = [torch.stack([x] * len(items)).mean(0) for x in gl]
+    k = int(sched.c_t[0] + sched.s_t[0])
+    fin = [torch.stack([x] * k).mean(0) for x in gl]
     for p, f in zip(params, fin):
         p.grad = f
     opt.step()
     dt = time.perf_counter() - t0
-    return dict(value=len(items) / dt, unit="worker-steps/s", cores=threads, kind="port",
-                sample=f"{len(items)} {model} fwd_bkwd of epoch 0 (n={n}, d={delay}, "
-                       f"{'throttle' if throttle else 'no throttle'}) + rule() over them + one "
-                       f"Adam step; torch CPU, {threads} threads, {dt:.1f} s")
+    c0 = None
+    if configs0_epochs:
+        s0 = MR.OracleSim(10, delay=50, throttle=False, pool=pool, model=model)
+        s0.epoch()                                   # warm
+        ws0 = 0
+        t1 = time.perf_counter()
+        for _ in range(configs0_epochs):
+            s0.epoch()
+            ws0 += len(s0.trace[-1]["items"])
+        d0 = time.perf_counter() - t1
+        c0 = dict(workload="configs[0]: n_workers=10, delay=50, no throttle (epochs 1..%d)"
+                  % configs0_epochs, worker_steps_per_s=round(ws0 / d0, 3),
+                  s_per_epoch=round(d0 / configs0_epochs, 3))
+    return dict(value=len(items) / dt, unit="worker-steps/s", cores=info["threads"], kind="port",
+                sample=f"one full epoch 0 of the bench workload: {len(items)} {model} fwd_bkwd "
+                       f"(n={n}, d={delay}, {'throttle' if throttle else 'no throttle'}) + rule() "
+                       f"over the {k} entries + one Adam step; torch CPU, {info['threads']} threads, "
+                       f"{dt:.1f} s",
+                host=info, configs0=c0)
 
 
 def main():
@@ -150,7 +206,12 @@ def main():
     if buffers:
         sim.engine.load_buffers(buffers)
     flop_per_ws = sim.engine.FLOP_PER_WORKER_STEP
-    for _ in range(args.warmup):
+    # untimed pre-roll so the timed window holds the first tick (t = delay: the slow worker's
+    # stale entry S_{t-d} joins rule()) and the 1023-worker epoch after it, when that is cheap
+    pre = 0
+    if not args.no_tick_window and delays is None and 0 < args.delay <= 100:
+        pre = max(0, args.delay - args.warmup - args.steps // 2)
+    for _ in range(pre + args.warmup):
         sim.epoch(sync_loss=False)
     torch.cuda.synchronize()
     probe = None if args.no_probe else KernelProbe(capacity=64 * 1024)
@@ -175,7 +236,13 @@ def main():
     kern = probe.read() if probe else {}
     if probe:
         probe.close()
-    agg_rec = kern.pop("aggregate_adam", None)
+    # the rule() + Adam kernel of the timed epochs: the fused slab step at world = 1, the
+    # streaming kernel after the all-reduce at world > 1 (general order: the _seq forms)
+    agg_recs = {k: kern.pop(k) for k in ("slab_step", "slab_step_seq", "aggregate_adam",
+                                         "aggregate_adam_seq", "slab_sum") if k in kern}
+    agg_name = max((k for k in agg_recs if k != "slab_sum"), key=lambda k: agg_recs[k][1],
+                   default=None)
+    agg_rec = agg_recs.get(agg_name)
     roofline = None
     if kern:
         name, (cnt, ms, fl) = max(kern.items(), key=lambda kv: kv[1][1])
@@ -192,7 +259,8 @@ def main():
                         launches=cnt, avg_launch_ms=round(ms / cnt, 4),
                         alg_flop_per_launch=fl / cnt,
                         all_gemms=dict(achieved=round(gemm_fl / (gemm_ms / 1e3) / 1e12, 2),
-                                       share_of_step=round(gemm_ms / 1e3 / elapsed, 3)),
+                                       share_of_step=round(gemm_ms / 1e3 / elapsed, 3),
+                                       executed_tflop=round(gemm_fl / 1e12, 3)),
                         per_kernel={k: dict(launches=c, avg_ms=round(m / c, 4),
                                             tflops=round(f / (m / 1e3) / 1e12, 1))
                                     for k, (c, m, f) in sorted(kern.items())})
@@ -200,25 +268,32 @@ def main():
     if agg_rec:
         cnt, ms, byts = agg_rec
         gbps = byts / (ms / 1e3) / 1e9
-        # profiles/traffic.json is measured on the default (PerformantNet1) workload
-        traffic = TRAFFIC.get("aggregate_adam") if args.model == "PerformantNet1" else None
-        agg = dict(kernel="k_aggregate_adam", bound="hbm", achieved=round(gbps, 1),
+        kname = {"slab_step": "k_slab_step (fused slab reduction + rule() + Adam)",
+                 "slab_step_seq": "k_slab_step (fused, general entry order)",
+                 "aggregate_adam": "k_agg_stream (rule() + Adam from S_t)",
+                 "aggregate_adam_seq": "k_agg_stream (general entry order)"}[agg_name]
+        # profiles/traffic.json is measured on the default workload (PerformantNet1, n = 1024,
+        # one GPU): only borrowed for that workload and the same kernel
+        same = args.model == "PerformantNet1" and delays is None and world == 1 and \
+            args.n_workers == 1024
+        traffic = TRAFFIC.get(agg_name) if same else None
+        agg = dict(kernel=kname, probe=agg_name, bound="hbm", achieved=round(gbps, 1),
                    peak=HBM_PEAK_GBPS, unit="GB/s", frac=round(gbps / HBM_PEAK_GBPS, 4),
                    launches=cnt, avg_launch_us=round(ms / cnt * 1e3, 2),
                    alg_bytes_per_launch=int(byts / cnt),
                    traffic=traffic["bytes_per_launch"] if traffic else None,
-                   traffic_source=traffic["source"] if traffic else None)
+                   traffic_source=traffic["source"] if traffic else None,
+                   ticks_in_window=sum(1 for p in sim.trace[-args.steps:] if p.stale))
         if traffic and traffic.get("trace_avg_ns"):
-            # the same launch timed by the rocprofv3 kernel trace of that profile (no event
+            # the same kernel timed by the rocprofv3 kernel trace of that profile (no event
             # packets around it): context for `achieved`, which stays the live measurement
             rus = traffic["trace_avg_ns"] / 1e3
-            agg.update(rocprof_avg_launch_us=round(rus, 2),
-                       rocprof_frac=round(byts / cnt / (rus * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4))
+            agg.update(rocprof_avg_launch_us=round(rus, 2))
 
     value = ws / elapsed
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.n_workers, args.delay, throttle, args.cpu_sample, args.model)
+        cpu = cpu_baseline(args.n_workers, args.delay, throttle, args.model, args.configs0_epochs)
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 3), "unit": "worker-steps/s",
@@ -237,10 +312,18 @@ def main():
                                       if args.semantics != "reference" else "")
                                    + "128 samples/worker-step, Adam lr 1e-3",
                        "executed_worker_steps": ws, "chunk_workers": args.chunk,
+                       "timed_epochs": [sim.trace[-args.steps].t, sim.trace[-1].t],
+                       "backend": (args.backend if world > 1 else None),
+                       "world_size": (torch.distributed.get_world_size() if world > 1 else 1),
                        "parallelism": f"workers sharded over {world} GPU(s), "
                                       f"{'1 RCCL all-reduce/step' if world > 1 and args.backend == 'nccl' else '1 gloo all-reduce/step (rehearsal)' if world > 1 else 'no collective'}"},
-            "mfma_efficiency_whole_step": round(value * flop_per_ws / 1e12 /
-                                                (MFMA_F32_PEAK_TFLOPS * world), 4),
+            # executed GEMM FLOPs of this rank (the probe's per-launch counts: conv6 skips its
+            # never-pooled border) / wall time / peak; the nominal SURVEY 8d count beside it
+            "mfma_efficiency_whole_step": (round(roofline["all_gemms"]["executed_tflop"] /
+                                                 (elapsed * MFMA_F32_PEAK_TFLOPS), 4)
+                                           if roofline else None),
+            "nominal_mfma_efficiency": round(value * flop_per_ws / 1e12 /
+                                             (MFMA_F32_PEAK_TFLOPS * world), 4),
             "roofline": roofline,
             "aggregation": agg,
             "cpu_baseline": cpu,

@@ -2,35 +2,49 @@
 
 Same classes, signatures and aliasing semantics; the arithmetic runs in libflsim.so:
 
-  Worker.fwd_bkwd(inp, outp)   agents.py:32-40 -> flsim_pn1_fwd_bwd_input / flsim_vgg11_*
-                               (HIP fwd/bwd of the central model); gradients accumulate over the workers of
-                               an epoch exactly like .grad (agents.py:35) and the returned list
-                               holds views of ONE flat buffer (every worker of the epoch gets the
-                               same tensors, as in the reference)
+  Worker.fwd_bkwd(inp, outp)   agents.py:32-40 -> flsim_<net>_fwd_bwd_input (HIP fwd/bwd of the
+                               central model); gradients accumulate over the workers of an epoch
+                               exactly like .grad (agents.py:35) and the returned list holds
+                               views of ONE flat buffer (every worker of the epoch gets the same
+                               tensors, as in the reference)
   Agg(rule)                    agents.py:43-45; use FL.agents.rule (== main.py:23-25's mean) to
                                get the fused path: it returns a lazy mean that Central consumes
-  Central.update_model(ups)    agents.py:9-21 -> flsim_aggregate_adam (fused cascade mean + Adam
-                               with the optimizer's lr/betas/eps); parameters live in one flat
-                               device buffer, model.parameters() are views of it
+  Central.update_model(ups)    agents.py:9-21 -> flsim_aggregate_adam_rule (cascade mean over the
+                               entries in any order + Adam with the optimizer's lr/betas/eps);
+                               parameters live in one flat device buffer, model.parameters() are
+                               views of it
+
+Batches (main.py:43-44 --batch_size): any size up to 16,384 samples.  The engine pads a batch to
+whole groups of 128 samples (padding adds nothing) and scales the CrossEntropyLoss gradient by
+1/n, so the gradient is the reference's mean over the n samples.  Dropout masks follow the
+build's Philox spec: group b of worker i's batch in epoch t is keyed
+(t, i + b * 2^20).
+
+Worker.index is the worker's position in the worker list: workers are numbered in creation order
+from the last Central (main.py:110-113 builds Central, then the workers).
 
 vgg11_bn(): the module's BatchNorm running_mean / running_var alias the engine's device buffer;
-every train-mode fwd_bkwd call advances them (and num_batches_tracked) as nn.BatchNorm2d does.
+every train-mode fwd_bkwd call advances them (and num_batches_tracked) as nn.BatchNorm2d does;
+batches must be 128 samples (one BatchNorm batch per call).
 
 Requirements (raise otherwise): the model is FL.models.PerformantNet1, vgg11() or vgg11_bn() on
-a HIP device (vgg11_bn: train mode, 128-sample batches = one BatchNorm batch per call), the optimizer is torch.optim.Adam without weight decay / amsgrad / maximize, batches
-are multiples of 128 samples.  There is no CPU fallback.
+a HIP device, the optimizer is torch.optim.Adam without weight decay / amsgrad / maximize.
+There is no CPU fallback.
 """
 from __future__ import annotations
 
-import itertools
+import weakref
 
 import numpy as np
 import torch
 
-from flsim.engine import engine_for_parameters, padded, split_views, worker_table
+from flsim.engine import (ProgramStager, Rule, engine_for_parameters, padded, split_views,
+                          worker_table)
 
-_CONTEXTS = {}
-_WORKER_IDS = itertools.count()
+_CONTEXTS = weakref.WeakKeyDictionary()    # model -> _ModelContext (dies with the model)
+_NEXT_WORKER = [0]                          # Worker.index of the next Worker()
+MAX_BATCH = 16384                           # samples per fwd_bkwd call (32-bit index budget)
+GROUP_KEY_STRIDE = 1 << 20                  # dropout key of 128-sample group b: i + b * 2^20
 
 
 class _ModelContext:
@@ -52,18 +66,20 @@ class _ModelContext:
             p.data = view                       # parameters alias the flat buffer
         self.m = torch.zeros_like(self.theta)
         self.v = torch.zeros_like(self.theta)
-        self.model = model
         self.engine = self.engine_cls(dev, chunk_workers=1)
         self.bn_stats = None
+        self.bns = []
         if self.engine.STATS_PER_WORKER:
             self._alias_buffers(model)
             self.bn_stats = torch.zeros(self.engine.STATS_PER_WORKER, device=dev)
         self.seed = seed
         self.t = 0               # epoch counter (dropout RNG key)
         self.G = None            # flat gradient buffer of the current epoch (p.grad views)
+        self.carry = None        # gradient accumulated before an engine resize this epoch
         self.packed = False
         self.step = 0
         self.loss_buf = torch.zeros(64, device=dev)
+        self.stager = ProgramStager(dev)
 
     def _alias_buffers(self, model):
         """BatchNorm running buffers become views of the engine's device buffer (loaded from the
@@ -80,13 +96,21 @@ class _ModelContext:
         self.bns = bns
 
     def ensure_capacity(self, n_samples):
-        cw = n_samples // 128
+        """An engine whose workspace holds n_samples.  Growing it mid-epoch keeps what the epoch
+        has accumulated: the new engine's slabs start at zero, so the running sum so far is
+        carried and added back after every later reduction (agents.py:35 keeps accumulating)."""
+        if n_samples > MAX_BATCH:
+            raise ValueError(f"batch of {n_samples} samples: the HIP engine takes at most "
+                             f"{MAX_BATCH} per fwd_bkwd call")
+        cw = -(-n_samples // 128)
         if cw > self.engine.chunk_workers:
             old = self.engine
             self.engine = self.engine_cls(self.device, chunk_workers=cw)
             if old.STATS_PER_WORKER:        # the running buffers stay where the module sees them
                 self.engine.running = old.running
                 self.engine.num_batches_tracked = old.num_batches_tracked
+            if self.G is not None:
+                self.carry = self.G.clone()
             self.packed = False
         if cw > self.loss_buf.numel():
             self.loss_buf = torch.zeros(cw, device=self.device)
@@ -94,14 +118,15 @@ class _ModelContext:
     def new_epoch(self):
         self.t += 1
         self.G = None
+        self.carry = None
         self.packed = False
 
 
 def _context(model):
-    ctx = _CONTEXTS.get(id(model))
+    ctx = _CONTEXTS.get(model)
     if ctx is None:
         ctx = _ModelContext(model)
-        _CONTEXTS[id(model)] = ctx
+        _CONTEXTS[model] = ctx
     return ctx
 
 
@@ -133,6 +158,7 @@ class Central:
             raise NotImplementedError("fused update implements torch.optim.Adam "
                                       "(main.py:106: Adam(lr), no weight decay / amsgrad)")
         self.ctx = _context(model)
+        _NEXT_WORKER[0] = 0          # main.py:112-113: the workers built next are 0 .. n-1
 
     def _sync_optimizer_state(self):
         ctx = self.ctx
@@ -141,32 +167,43 @@ class Central:
             self.optim.state[p] = {"step": torch.tensor(float(ctx.step)), "exp_avg": mv,
                                    "exp_avg_sq": vv}
 
+    def _rule_of(self, ups):
+        """(S, Rule) for weight_ups: the entries that are this epoch's gradient buffer are S_t;
+        every other entry (a stale FIFO entry, main.py:161-165) is an array, in list order."""
+        ctx = self.ctx
+        entries = [u[0] for u in ups.ups_list]
+        S = ctx.G if ctx.G is not None else torch.zeros(padded(ctx.P), device=ctx.device)
+        sbase = S.untyped_storage().data_ptr()
+        arrays, bases, events = [], [], []
+        for pos, e in enumerate(entries):
+            b = e.untyped_storage().data_ptr()
+            if b == sbase:
+                continue
+            if b not in bases:
+                bases.append(b)
+                arrays.append(_flat_of(e, ctx))
+            events.append((pos, bases.index(b)))
+        k = len(entries)
+        c = k - len(events)
+        if len(events) <= 8 and all(p >= c for p, _ in events):    # reference order
+            return S, Rule(k, [arrays[j] for _, j in events], c=c)
+        return S, Rule(k, arrays, events=events, stager=ctx.stager)
+
     def update_model(self, ups):
         """agents.py:9-21: install the aggregated gradient, Adam step, clear .grad."""
         ctx = self.ctx
         g = self.optim.param_groups[0]
         eng = ctx.engine
         if isinstance(ups, _LazyMean):
-            entries = [u[0] for u in ups.ups_list]
-            bases = [e.untyped_storage().data_ptr() for e in entries]
-            first = bases[0]
-            c = 0
-            while c < len(bases) and bases[c] == first:
-                c += 1
-            stale = []
-            for e, b in zip(entries[c:], bases[c:]):
-                if b == first:
-                    raise NotImplementedError("fused rule: fresh entries after stale ones")
-                stale.append(_flat_of(e, ctx))
-            S = _flat_of(entries[0], ctx)
+            S, r = self._rule_of(ups)
         else:
             if len(ups) != len(ctx.shapes):
                 raise IndexError("list index out of range")
             S = torch.cat([u.detach().reshape(-1).float() for u in ups])
             S = torch.nn.functional.pad(S, (0, padded(ctx.P) - ctx.P))
-            c, stale = 1, []
+            r = Rule(1, [], c=1)
         ctx.step += 1
-        eng.aggregate_adam(S, c, stale, ctx.theta, ctx.m, ctx.v, ctx.step, lr=g["lr"],
+        eng.aggregate_rule(S, r, ctx.theta, ctx.m, ctx.v, ctx.step, lr=g["lr"],
                            betas=g["betas"], eps=g["eps"])
         for p in self.model.parameters():        # optim.zero_grad() (set_to_none, torch >= 2)
             p.grad = None
@@ -193,7 +230,8 @@ class Worker:
     def __init__(self, loss, key=None):
         self.model = None
         self.loss = loss
-        self.index = next(_WORKER_IDS)    # creation order == worker_list index (main.py:112-113)
+        self.index = _NEXT_WORKER[0]     # position in the worker list (main.py:112-113)
+        _NEXT_WORKER[0] += 1
 
     def fwd_bkwd(self, inp, outp):
         if not isinstance(self.loss, torch.nn.CrossEntropyLoss) or \
@@ -201,6 +239,9 @@ class Worker:
             raise NotImplementedError("fused loss implements nn.CrossEntropyLoss(mean)")
         ctx = _context(self.model)
         n = int(inp.shape[0])
+        if int(outp.shape[0]) != n:
+            raise ValueError(f"Expected input batch_size ({n}) to match target batch_size "
+                             f"({int(outp.shape[0])}).")
         ctx.ensure_capacity(n)
         eng = ctx.engine
         theta = ctx.theta
@@ -209,9 +250,10 @@ class Worker:
             ctx.packed = True
         if ctx.G is None:
             ctx.G = torch.zeros(padded(ctx.P), device=ctx.device)
-        recs = [(ctx.t, self.index, 0)] * (n // 128)
+        groups = -(-n // 128)
+        recs = [(ctx.t, self.index + b * GROUP_KEY_STRIDE, 0) for b in range(groups)]
         wt = worker_table(recs, ctx.device)
-        lb = ctx.loss_buf[:n // 128]
+        lb = ctx.loss_buf[:groups]
         kw = {}
         if ctx.bn_stats is not None:
             if not self.model.training or n != 128:
@@ -225,11 +267,14 @@ class Worker:
             for mod in ctx.bns:
                 mod.num_batches_tracked.fill_(eng.num_batches_tracked)
         eng.end_epoch(ctx.G)                     # running sum of the epoch's gradients
+        if ctx.carry is not None:
+            ctx.G.add_(ctx.carry)
         grads = split_views(ctx.G[:ctx.P], ctx.shapes)
         for p, gv in zip(self.model.parameters(), grads):
             p.grad = gv                          # agents.py:35: accumulated in place
-        lossval = lb.mean().detach().cpu().numpy()
-        return list(grads), lossval.astype(np.float32)
+        # CrossEntropyLoss(mean) over the n samples: group sums / n (padding contributes 0)
+        lossval = np.float32(float(lb.double().sum().cpu()) * 128.0 / n)
+        return list(grads), np.asarray(lossval, np.float32)
 
 
 class Agg:

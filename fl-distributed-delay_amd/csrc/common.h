@@ -31,6 +31,8 @@ const char* last_error();
         }                                                                               \
     } while (0)
 
+#define RC(x) do { int _r = (x); if (_r) return _r; } while (0)
+
 #define FLSIM_LAUNCH_CHECK()                                                            \
     do {                                                                                \
         hipError_t _e = hipGetLastError();                                              \

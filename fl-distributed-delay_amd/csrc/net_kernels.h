@@ -11,8 +11,6 @@
 #include "pn1.h"
 #include "probe.h"
 
-#define RC(x) do { int _r = (x); if (_r) return _r; } while (0)
-
 namespace flsim {
 
 // =============================================================================================
@@ -67,18 +65,22 @@ k_fill_seq(const uint8_t* __restrict__ pool, int first, int n_images, const floa
 
 // explicit input (Worker.fwd_bkwd(inp, outp) facade): x NCHW fp32 [S][3][32][32], y int64
 static __global__ void __launch_bounds__(256)
-k_load_input(const float* __restrict__ x, const int64_t* __restrict__ yin, float* __restrict__ x0,
-             int32_t* __restrict__ y) {
+k_load_input(const float* __restrict__ x, const int64_t* __restrict__ yin, int n,
+             float* __restrict__ x0, int32_t* __restrict__ y) {
+    // samples s >= n pad the batch to whole 128-sample groups: zero image, label -1 (the head
+    // gives them zero loss and zero gradient)
     const int s = blockIdx.x;
-    if (threadIdx.x == 0) y[s] = (int32_t)yin[s];
+    const bool real = s < n;
+    if (threadIdx.x == 0) y[s] = (real && yin) ? (int32_t)yin[s] : -1;
     const float* img = x + (long)s * 3072;
     float* out = x0 + (long)s * 4096;
     for (int p = threadIdx.x; p < 1024; p += 256) {
-        f32x4 v;
-        v.x = img[p];
-        v.y = img[1024 + p];
-        v.z = img[2048 + p];
-        v.w = 0.f;
+        f32x4 v = zero4();
+        if (real) {
+            v.x = img[p];
+            v.y = img[1024 + p];
+            v.z = img[2048 + p];
+        }
         *reinterpret_cast<f32x4*>(out + 4 * p) = v;
     }
 }
@@ -227,14 +229,16 @@ static int linear_finish(const float* part, int Z, const float* bias, float* out
 // head: last linear (K -> 10) + CrossEntropyLoss(mean over the worker's 128) forward and
 // backward (PerformantNet1 models.py:46 / VGG models.py:64, main.py:107, agents.py:34-35).
 // One wave per sample; lane l holds features 4l + 256c (c < K/256).
-//   loss_s[s] = logsumexp(z) - z_y ; dlog[s][j] = (softmax - onehot) / 128
+//   loss_s[s] = logsumexp(z) - z_y ; dlog[s][j] = (softmax - onehot) * gscale
+// gscale = 1/128 (one worker's mean over its 128 samples) or 1/n for an n-sample facade batch;
+// a label < 0 marks a padding sample: zero loss, zero gradient
 //   dh[s][k] = (sum_j dlog[s][j] W[j][k]) * sdrop * (e[s][k] > 0)   (dropout / ReLU backward)
 // =============================================================================================
 template <int K>
 __global__ void __launch_bounds__(256)
 k_head(const float* __restrict__ e2, const float* __restrict__ W3, const float* __restrict__ b3,
        const int32_t* __restrict__ y, float* __restrict__ loss_s, float* __restrict__ dlog,
-       float* __restrict__ dh2, int S, int backward, float sdrop,
+       float* __restrict__ dh2, int S, int backward, float sdrop, float gscale,
        int32_t* __restrict__ pred, int n_pred) {
     constexpr int NC = K / 256;
     static_assert(K % 256 == 0, "head width must be a multiple of 256");
@@ -268,7 +272,7 @@ k_head(const float* __restrict__ e2, const float* __restrict__ W3, const float* 
     float zy = 0.f;
 #pragma unroll
     for (int j = 0; j < 10; ++j) zy = (j == lab) ? z[j] : zy;
-    if (lane == 0) loss_s[s] = (mx + logf(se)) - zy;
+    if (lane == 0) loss_s[s] = lab >= 0 ? (mx + logf(se)) - zy : 0.f;
     if (pred && lane == 0 && s < n_pred) {       // torch.max(outputs, 1): first max wins
         int am = 0;
 #pragma unroll
@@ -280,7 +284,7 @@ k_head(const float* __restrict__ e2, const float* __restrict__ W3, const float* 
     const float inv = 1.f / se;
 #pragma unroll
     for (int j = 0; j < 10; ++j)
-        g[j] = (expf(z[j] - mx) * inv - (j == lab ? 1.f : 0.f)) * (1.f / SAMPLES_PER_WORKER);
+        g[j] = lab >= 0 ? (expf(z[j] - mx) * inv - (j == lab ? 1.f : 0.f)) * gscale : 0.f;
     if (lane < 10) {
         float gv = 0.f;
 #pragma unroll
@@ -324,9 +328,9 @@ k_worker_loss(const float* __restrict__ loss_s, float* __restrict__ out) {
 template <int K>
 static int head_and_loss(const float* e, const float* W, const float* b, const int32_t* y,
                          float* loss_s, float* dlog, float* dh, int S, int backward, float sdrop,
-                         float* worker_loss, hipStream_t st) {
+                         float gscale, float* worker_loss, hipStream_t st) {
     hipLaunchKernelGGL(k_head<K>, dim3(ceil_div(S, 4)), dim3(256), 0, st, e, W, b, y, loss_s, dlog,
-                       dh, S, backward, sdrop, (int32_t*)nullptr, 0);
+                       dh, S, backward, sdrop, gscale, (int32_t*)nullptr, 0);
     FLSIM_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_worker_loss, dim3(S / SAMPLES_PER_WORKER), dim3(128), 0, st, loss_s,
                        worker_loss);
@@ -339,7 +343,7 @@ template <int K>
 static int head_predict(const float* e, const float* W, const float* b, const int32_t* y,
                         float* loss_s, int S, int32_t* pred, int n_pred, hipStream_t st) {
     hipLaunchKernelGGL(k_head<K>, dim3(ceil_div(S, 4)), dim3(256), 0, st, e, W, b, y, loss_s,
-                       (float*)nullptr, (float*)nullptr, S, 0, 1.f, pred, n_pred);
+                       (float*)nullptr, (float*)nullptr, S, 0, 1.f, 1.f, pred, n_pred);
     FLSIM_LAUNCH_CHECK();
     return 0;
 }

@@ -14,6 +14,7 @@
 #include <string.h>
 
 #include "net_kernels.h"
+#include "slabstep.h"
 
 namespace flsim {
 
@@ -70,13 +71,36 @@ struct GradState {
     float* slab_begin;
     long slab_floats;
     long total_floats;
+    StepPlan plan;  // the fused server step over the slabs (slabstep.h)
+    long cnt_off;   // its tile counters (inside the zeroed slab range) and unit partials
+    long part_off;
 };
 
-static GradState gs_layout(float* base) {
+// one segment per parameter tensor (named_parameters order), offsets from the gradstate base
+static int pn1_segments(const GradState& g, const float* base, SegSpec* s) {
+    int i = 0;
+    for (int l = 0; l < 6; ++l) {
+        const ConvGeo& c = GEO[l];
+        s[i++] = SegSpec{g.sw[l] - base, c.ZW, (long)c.CO * c.KP, P_OFF[2 * l],
+                         (long)c.CO * c.CI * 9, c.CO, c.CI, c.CIP, c.KP};
+        s[i++] = SegSpec{g.sb[l] - base, c.ZW, c.CO, P_OFF[2 * l + 1], c.CO, 0, 0, 1, 1};
+    }
+    s[i++] = SegSpec{g.l1w - base, ZL1W, 512L * 9408, P_OFF[12], 512L * 9408, 0, 0, 1, 1};
+    s[i++] = SegSpec{g.l1b - base, ZL1W, 512, P_OFF[13], 512, 0, 0, 1, 1};
+    s[i++] = SegSpec{g.l2w - base, ZL2W, 256L * 512, P_OFF[14], 256L * 512, 0, 0, 1, 1};
+    s[i++] = SegSpec{g.l2b - base, ZL2W, 256, P_OFF[15], 256, 0, 0, 1, 1};
+    s[i++] = SegSpec{g.l3w - base, ZH, 2560, P_OFF[16], 2560, 0, 0, 1, 1};
+    s[i++] = SegSpec{g.l3b - base, ZH, 10, P_OFF[17], 10, 0, 0, 1, 1};
+    return i;
+}
+
+static GradState gs_layout(float* base_in) {
     GradState g;
+    // offsets only (sizes, plan) when base_in is null: lay out over a fake base, never dereferenced
+    float* const base = base_in ? base_in : reinterpret_cast<float*>(4096);
     long o = 0;
     auto take = [&](long n) {
-        float* p = base ? base + o : nullptr;
+        float* p = base + o;
         o += (n + 63) / 64 * 64;
         return p;
     };
@@ -85,7 +109,7 @@ static GradState gs_layout(float* base) {
         g.wd[l] = l ? take((long)GEO[l].CI * 9 * GEO[l].CO) : nullptr;
     }
     const long slab0 = o;
-    g.slab_begin = base ? base + o : nullptr;
+    g.slab_begin = base + o;
     for (int l = 0; l < 6; ++l) {
         g.sw[l] = take((long)GEO[l].ZW * GEO[l].CO * GEO[l].KP);
         g.sb[l] = take((long)GEO[l].ZW * GEO[l].CO);
@@ -96,7 +120,13 @@ static GradState gs_layout(float* base) {
     g.l2b = take((long)ZL2W * 256);
     g.l3w = take((long)ZH * 10 * 256);
     g.l3b = take((long)ZH * 10);
+    SegSpec specs[STEP_MAX_SEG];
+    plan_step(specs, pn1_segments(g, base, specs), &g.plan);
+    g.cnt_off = o;
+    take(step_counter_floats(g.plan));
     g.slab_floats = o - slab0;
+    g.part_off = o;
+    take(step_partial_floats(g.plan));
     g.total_floats = o;
     return g;
 }
@@ -269,13 +299,15 @@ int flsim_pn1_begin_epoch(void* gradstate, const float* theta, hipStream_t strea
 
 static int run_chunk(void* gradstate, const WS& w, const float* theta, const WorkerRec* workers,
                      int n_chunk_workers, uint64_t seed, int dropout, int backward_pass,
-                     float* worker_loss, hipStream_t stream) {
+                     float* worker_loss, hipStream_t stream,
+                     float gscale = 1.f / SAMPLES_PER_WORKER) {
     const int S = n_chunk_workers * SAMPLES_PER_WORKER;
     GradState g = gs_layout((float*)gradstate);
     RC(forward(g, w, theta, S, workers, seed, dropout, stream));
     // linear3 + CrossEntropyLoss (models.py:46, main.py:107); dropout2 precedes linear3
     RC(head_and_loss<256>(w.e2, theta + P_OFF[16], theta + P_OFF[17], w.y, w.loss_s, w.dlog, w.dh2,
-                          S, backward_pass, dropout ? SCALE_P50 : 1.f, worker_loss, stream));
+                          S, backward_pass, dropout ? SCALE_P50 : 1.f, gscale, worker_loss,
+                          stream));
     if (backward_pass) RC(backward(g, w, theta, S, dropout, stream));
     return 0;
 }
@@ -301,24 +333,51 @@ int flsim_pn1_fwd_bwd_chunk(void* gradstate, void* workspace, int max_samples, c
                      worker_loss, stream);
 }
 
-// explicit batch (the Worker.fwd_bkwd(inp, outp) facade): x NCHW fp32, y int64; n_samples is a
-// multiple of 128, workers[n_samples/128] give the dropout keys
+// explicit batch (the Worker.fwd_bkwd(inp, outp) facade, agents.py:32-35): x NCHW fp32, y int64,
+// any n_samples (main.py:43-44 --batch_size); the batch is padded to whole 128-sample groups
+// (padding has zero loss and gradient) and the CE gradient is the mean over the n samples.
+// workers[ceil(n/128)] give each group's dropout key; worker_loss[g] = group g's loss sum / 128.
 int flsim_pn1_fwd_bwd_input(void* gradstate, void* workspace, int max_samples, const float* theta,
                             const float* x, const int64_t* y, int n_samples,
                             const WorkerRec* workers, uint64_t seed, int dropout,
                             int backward_pass, float* worker_loss, hipStream_t stream) {
     FLSIM_REQUIRE(gradstate && workspace && theta && x && y && workers && worker_loss,
                   "null pointer");
-    FLSIM_REQUIRE(n_samples > 0 && n_samples % SAMPLES_PER_WORKER == 0,
-                  "batch of %d samples: must be a positive multiple of %d", n_samples,
-                  SAMPLES_PER_WORKER);
-    FLSIM_REQUIRE(n_samples <= max_samples, "batch of %d samples exceeds workspace (%d)", n_samples,
+    FLSIM_REQUIRE(n_samples > 0, "empty batch");
+    const int S = ceil_div(n_samples, SAMPLES_PER_WORKER) * SAMPLES_PER_WORKER;
+    FLSIM_REQUIRE(S <= max_samples, "batch of %d samples exceeds workspace (%d)", n_samples,
                   max_samples);
+    FLSIM_REQUIRE(S <= 16384, "batch of %d samples exceeds the 32-bit index budget", n_samples);
     WS w = ws_layout((char*)workspace, max_samples);
-    hipLaunchKernelGGL(k_load_input, dim3(n_samples), dim3(256), 0, stream, x, y, w.x0, w.y);
+    hipLaunchKernelGGL(k_load_input, dim3(S), dim3(256), 0, stream, x, y, n_samples, w.x0, w.y);
     FLSIM_LAUNCH_CHECK();
-    return run_chunk(gradstate, w, theta, workers, n_samples / SAMPLES_PER_WORKER, seed, dropout,
-                     backward_pass, worker_loss, stream);
+    return run_chunk(gradstate, w, theta, workers, S / SAMPLES_PER_WORKER, seed, dropout,
+                     backward_pass, worker_loss, stream, 1.f / (float)n_samples);
+}
+
+// Evaluation of an explicit batch (util.py:31-45: model(images) after central.model.eval(),
+// main.py:190): x NCHW fp32 [n][3][32][32] -> argmax predictions pred[n].  Re-packs theta.
+int flsim_pn1_eval_input(void* gradstate, void* workspace, int max_samples, const float* theta,
+                         const float* x, int n_images, int32_t* pred, hipStream_t stream) {
+    FLSIM_REQUIRE(gradstate && workspace && theta && x && pred, "null pointer");
+    FLSIM_REQUIRE(n_images > 0, "empty batch");
+    FLSIM_REQUIRE(max_samples >= SAMPLES_PER_WORKER && max_samples % SAMPLES_PER_WORKER == 0,
+                  "max_samples must be a positive multiple of %d", SAMPLES_PER_WORKER);
+    GradState g = gs_layout((float*)gradstate);
+    WS w = ws_layout((char*)workspace, max_samples);
+    RC(pack_weights(g, theta, stream));
+    const int cap = max_samples < 16384 ? max_samples : 16384;
+    for (int c0 = 0; c0 < n_images; c0 += cap) {
+        const int n = n_images - c0 < cap ? n_images - c0 : cap;
+        const int S = ceil_div(n, SAMPLES_PER_WORKER) * SAMPLES_PER_WORKER;
+        hipLaunchKernelGGL(k_load_input, dim3(S), dim3(256), 0, stream, x + (long)c0 * 3072,
+                           (const int64_t*)nullptr, n, w.x0, w.y);
+        FLSIM_LAUNCH_CHECK();
+        RC(forward(g, w, theta, S, nullptr, 0, 0, stream));
+        RC(head_predict<256>(w.e2, theta + P_OFF[16], theta + P_OFF[17], w.y, w.loss_s, S,
+                             pred + c0, n, stream));
+    }
+    return 0;
 }
 
 // Evaluation (util.py:31-45 print_test_accuracy; main.py:190 central.model.eval(), so dropout is
@@ -334,8 +393,9 @@ int flsim_pn1_eval_pool(void* gradstate, void* workspace, int max_samples, const
     GradState g = gs_layout((float*)gradstate);
     WS w = ws_layout((char*)workspace, max_samples);
     RC(pack_weights(g, theta, stream));
-    for (int c0 = 0; c0 < n_images; c0 += max_samples) {
-        const int n = n_images - c0 < max_samples ? n_images - c0 : max_samples;
+    const int cap = max_samples < 16384 ? max_samples : 16384;   // 32-bit index budget
+    for (int c0 = 0; c0 < n_images; c0 += cap) {
+        const int n = n_images - c0 < cap ? n_images - c0 : cap;
         const int S = ceil_div(n, SAMPLES_PER_WORKER) * SAMPLES_PER_WORKER;
         hipLaunchKernelGGL(k_fill_seq, dim3(S), dim3(256), 0, stream, pool, first + c0, n, lut,
                            w.x0, w.y);
@@ -347,23 +407,26 @@ int flsim_pn1_eval_pool(void* gradstate, void* workspace, int max_samples, const
     return 0;
 }
 
-// S_t (torch named_parameters layout, P floats) = sum of the epoch's slabs
+// S_t (torch named_parameters layout, P floats) = sum of the epoch's slabs (fixed order)
 int flsim_pn1_end_epoch(void* gradstate, float* grad_out, hipStream_t stream) {
     FLSIM_REQUIRE(gradstate && grad_out, "null pointer");
     GradState g = gs_layout((float*)gradstate);
-    for (int l = 0; l < 6; ++l) {
-        const ConvGeo& c = GEO[l];
-        RC(fin_sum(g.sw[l], c.ZW, (long)c.CO * c.KP, grad_out + P_OFF[2 * l], stream, c.CO, c.CI,
-                   c.CIP, c.KP));
-        RC(fin_sum(g.sb[l], c.ZW, c.CO, grad_out + P_OFF[2 * l + 1], stream));
-    }
-    RC(fin_sum(g.l1w, ZL1W, 512L * 9408, grad_out + P_OFF[12], stream));
-    RC(fin_sum(g.l1b, ZL1W, 512, grad_out + P_OFF[13], stream));
-    RC(fin_sum(g.l2w, ZL2W, 256L * 512, grad_out + P_OFF[14], stream));
-    RC(fin_sum(g.l2b, ZL2W, 256, grad_out + P_OFF[15], stream));
-    RC(fin_sum(g.l3w, ZH, 2560, grad_out + P_OFF[16], stream));
-    RC(fin_sum(g.l3b, ZH, 10, grad_out + P_OFF[17], stream));
-    return 0;
+    return slab_step_launch((float*)gradstate, g.plan, g.cnt_off, g.part_off, grad_out, nullptr,
+                            nullptr, nullptr, nullptr, nullptr, P_TOTAL, stream);
+}
+
+// the same reduction fused with rule() + Adam (world = 1)
+int flsim_pn1_server_step(void* gradstate, float* S_out, const flsim_rule* rule, float* p,
+                          float* m, float* v, long step, double lr, double beta1, double beta2,
+                          double eps, hipStream_t stream) {
+    FLSIM_REQUIRE(gradstate && rule && p && m && v, "null pointer");
+    GradState g = gs_layout((float*)gradstate);
+    RuleProg R;
+    RC(make_rule(rule, &R));
+    AdamConst ac;
+    RC(make_adam_const(rule->k, step, lr, beta1, beta2, eps, &ac));
+    return slab_step_launch((float*)gradstate, g.plan, g.cnt_off, g.part_off, S_out, &R, &ac, p,
+                            m, v, P_TOTAL, stream);
 }
 
 }  // extern "C"

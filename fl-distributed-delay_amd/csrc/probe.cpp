@@ -15,7 +15,8 @@ static const char* KNAME[K_COUNT] = {
     "vgg_conv2_dgrad", "vgg_conv3_dgrad", "vgg_conv4_dgrad", "vgg_conv5_dgrad", "vgg_conv6_dgrad",
     "vgg_conv7_dgrad", "vgg_conv8_dgrad", "vgg_conv1_wgrad", "vgg_conv2_wgrad", "vgg_conv3_wgrad",
     "vgg_conv4_wgrad", "vgg_conv5_wgrad", "vgg_conv6_wgrad", "vgg_conv7_wgrad", "vgg_conv8_wgrad",
-    "vgg_linear1_wgrad", "vgg_linear1_dgrad", "vgg_linear2_wgrad", "vgg_linear2_dgrad"};
+    "vgg_linear1_wgrad", "vgg_linear1_dgrad", "vgg_linear2_wgrad", "vgg_linear2_dgrad",
+    "aggregate_adam_seq", "slab_step", "slab_step_seq", "slab_sum"};
 
 struct Probe {
     bool on = false;

@@ -17,7 +17,10 @@ enum KernelId {
     K_VF1, K_VF2, K_VF3, K_VF4, K_VF5, K_VF6, K_VF7, K_VF8, K_VL1F, K_VL2F,
     K_VDG2, K_VDG3, K_VDG4, K_VDG5, K_VDG6, K_VDG7, K_VDG8,
     K_VWG1, K_VWG2, K_VWG3, K_VWG4, K_VWG5, K_VWG6, K_VWG7, K_VWG8,
-    K_VL1W, K_VL1D, K_VL2W, K_VL2D, K_COUNT
+    K_VL1W, K_VL1D, K_VL2W, K_VL2D,
+    // server step (server.hip): general-order aggregation, fused slab step (reference / general
+    // order), slab reduction only
+    K_AGG_SEQ, K_STEP, K_STEP_SEQ, K_SLABSUM, K_COUNT
 };
 
 // Event pair for the launch that follows (nullptr events when the probe is off or full).  The

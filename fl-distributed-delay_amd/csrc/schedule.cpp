@@ -54,9 +54,9 @@ void flsim_sched_destroy(flsim_sched* s) { delete s; }
 //                    is logged, main.py:171-172)
 //   stale_worker / stale_src [n]: the popped FIFO entries in append order (worker, source epoch)
 //   info[4] = {c_t, s_t, pushed (any slow worker stored S_t this epoch), epoch t}
-// Returns 0, or 1 when the reference would raise: delay 0 on the slow worker at t >= 1
-// (ZeroDivisionError, main.py:158) -- not representable here since delay 0 means fast -- or an
-// empty weight_ups (IndexError in rule(), main.py:25).  The state is advanced either way.
+// Returns 0, or 1 when the reference would raise: a slow worker with delay 0
+// (FLSIM_DELAY_ZERO) at t >= 1 (ZeroDivisionError, main.py:158), or an empty weight_ups
+// (IndexError in rule(), main.py:25).
 int flsim_sched_epoch(flsim_sched* s, uint8_t* computes, uint8_t* fast, int32_t* stale_worker,
                       int64_t* stale_src, int64_t* info) {
     if (!s) {
@@ -71,7 +71,12 @@ int flsim_sched_epoch(flsim_sched* s, uint8_t* computes, uint8_t* fast, int32_t*
         const int32_t di = s->delay[i];
         if (di != 0) {                                    // main.py:150 (slow worker)
             s->slow_guy_gone = 0;                         // main.py:151
-            const int64_t d = di < 0 ? -(int64_t)di : (int64_t)di;
+            if (di == FLSIM_DELAY_ZERO && t > 0) {        // main.py:158: t % 0
+                flsim::set_error("epoch %ld: ZeroDivisionError: integer division or modulo by "
+                                 "zero (--delay 0, main.py:158)", (long)t);
+                return 1;
+            }
+            const int64_t d = di == FLSIM_DELAY_ZERO ? 0 : (di < 0 ? -(int64_t)di : (int64_t)di);
             bool popped = false;
             int64_t src = -1;
             if (t == 0) {                                 // main.py:153-157

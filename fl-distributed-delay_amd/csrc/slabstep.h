@@ -1,0 +1,129 @@
+// Fused end of a server step (SURVEY 8 a6 + a8 + a9) over the weight-gradient slabs the networks'
+// GEMMs accumulate during an epoch:
+//
+//   S_t = sum_z slab[z]                 agents.py:35 -- .grad accumulates over the epoch's workers
+//   [S_out = S_t]                       main.py:156,161 -- the slow worker's FIFO entry (a tick)
+//   g   = rule(weight_ups)              main.py:23-25  -- cascade mean over [S_t]*c + stale entries
+//   Adam(p, m, v, g)                    agents.py:9-21 -- Central.update_model
+//
+// in ONE launch that streams every slab byte once.  A network describes its slabs as segments
+// (one per parameter tensor: slab base, split count Z, slab row length n, where the tensor sits in
+// the flat parameter vector, and the packed-conv layout that maps a slab column to torch's
+// [co][ci][kh][kw]).  The planner cuts each segment into units of <= UNIT_FLOATS slab floats:
+// 256 slab columns x a z-range.  A tile whose z-range is split over several units is finished by
+// the unit that arrives last (counter per tile); its partials are handed over through sc1
+// stores / loads (agent scope), the in-launch split-K recipe of cdna_hip_programming.md §5.
+#pragma once
+#include <stdint.h>
+
+#include "cascade.h"
+#include "common.h"
+#include "flsim.h"
+
+namespace flsim {
+
+constexpr int STEP_MAX_SEG = 40;      // parameter tensors per network (vgg11_bn: 38)
+constexpr int RULE_MAX_ARR = FLSIM_MAX_ARRAYS;   // weight_ups arrays besides S_t per launch
+constexpr int RULE_INL_PROG = 192;    // program words carried in the kernel arguments
+constexpr long STEP_UNIT_FLOATS = 65536;
+
+// host description of one parameter tensor's gradient slabs (offsets in floats)
+struct SegSpec {
+    long slab_off;     // slab [Z][n] at gradstate + slab_off
+    int Z;
+    long n;
+    long toff, numel;  // the tensor in the flat named_parameters vector
+    int CO, CI, CIP, KP;   // packed conv layout n = CO * KP, column = co*KP + khkw*CIP + ci; CO = 0: identity
+};
+
+// planned segment (kernel argument)
+struct SlabSeg {
+    long slab_off;
+    int Z, n, zc, nz, tiles, tpu, unit0, tile0, toff, numel;
+    uint16_t CO, CI, CIP, KP;
+};
+
+struct StepPlan {
+    SlabSeg seg[STEP_MAX_SEG];
+    int nseg, units, ctiles;
+    long slab_floats;     // sum of Z * n (the slab bytes the step streams / 4)
+};
+
+inline int plan_step(const SegSpec* s, int nseg, StepPlan* P) {
+    if (nseg > STEP_MAX_SEG) return 1;
+    P->nseg = nseg;
+    int u = 0, ct = 0;
+    long sf = 0;
+    for (int i = 0; i < nseg; ++i) {
+        SlabSeg& g = P->seg[i];
+        g.slab_off = s[i].slab_off;
+        g.Z = s[i].Z;
+        g.n = (int)s[i].n;
+        g.toff = (int)s[i].toff;
+        g.numel = (int)s[i].numel;
+        g.CO = (uint16_t)s[i].CO;
+        g.CI = (uint16_t)s[i].CI;
+        g.CIP = (uint16_t)s[i].CIP;
+        g.KP = (uint16_t)s[i].KP;
+        g.tiles = (int)((s[i].n + 255) / 256);
+        const long tile_f = 256L * s[i].Z;
+        int units;
+        if (tile_f <= STEP_UNIT_FLOATS) {
+            g.nz = 1;
+            g.zc = g.Z;
+            long tpu = STEP_UNIT_FLOATS / tile_f;
+            if (tpu > 4) tpu = 4;     // short units: many blocks in flight, no long serial tails
+            g.tpu = (int)(tpu < g.tiles ? tpu : g.tiles);
+            units = (g.tiles + g.tpu - 1) / g.tpu;
+            g.tile0 = 0;
+        } else {
+            int nz = (int)((tile_f + STEP_UNIT_FLOATS - 1) / STEP_UNIT_FLOATS);
+            g.zc = (g.Z + nz - 1) / nz;
+            g.zc = (g.zc + 3) / 4 * 4;
+            g.nz = (g.Z + g.zc - 1) / g.zc;
+            g.tpu = 1;
+            units = g.tiles * g.nz;
+            g.tile0 = ct;
+            ct += g.tiles;
+        }
+        g.unit0 = u;
+        u += units;
+        sf += (long)s[i].Z * s[i].n;
+    }
+    P->units = u;
+    P->ctiles = ct;
+    P->slab_floats = sf;
+    return 0;
+}
+
+// Adam hyper-parameters + rule() divisor, prepared on the host (agents.py:9-21, main.py:106)
+struct AdamConst {
+    float w1, b2, w2, bc2s, rbc2s, eps, neg_ss, fk, rk;
+};
+
+// rule(): which program and which arrays (host side, see flsim_rule in include/flsim.h)
+struct RuleProg {
+    const int32_t* prog;            // device program, or nullptr: iprog
+    int32_t iprog[RULE_INL_PROG];
+    CascInfo info;
+    int narr;
+    const float* arr[RULE_MAX_ARR]; // nullptr entry = zeros (torch-1.x stale semantics)
+    int distinct;                   // distinct non-null arrays (algorithmic bytes)
+};
+
+// gradstate extras the fused step needs: tile counters (zeroed with the slabs) and partials
+inline long step_counter_floats(const StepPlan& P) { return (P.ctiles + 63) / 64 * 64; }
+inline long step_partial_floats(const StepPlan& P) { return (long)P.units * 256; }
+
+// launch: S_out (nullable) receives S_t in the flat layout; rule == nullptr: reduce only (the
+// network's end_epoch); else rule() + Adam on p, m, v
+int slab_step_launch(float* gradstate, const StepPlan& plan, long cnt_off, long part_off,
+                     float* S_out, const RuleProg* rule, const AdamConst* ac, float* p, float* m,
+                     float* v, long P, hipStream_t stream);
+
+// host helpers shared with server.hip's C-ABI
+int make_rule(const flsim_rule* r, RuleProg* out);
+int make_adam_const(int divisor, long step, double lr, double beta1, double beta2, double eps,
+                    AdamConst* ac);
+
+}  // namespace flsim

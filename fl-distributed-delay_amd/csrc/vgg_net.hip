@@ -20,6 +20,7 @@
 // normalisation + ReLU (+ pool / dropout).  The backward turns the masked gradient of each
 // BatchNorm output into dz in place before the conv's weight / data gradients.
 #include "bn_kernels.h"
+#include "slabstep.h"
 
 namespace flsim {
 
@@ -88,13 +89,40 @@ struct VGrad {
     float* bnacc[8];   // vgg11_bn: epoch sums of the BatchNorm [weight | bias] gradients
     float* slab_begin;
     long slab_floats, total_floats;
+    StepPlan plan;  // the fused server step over the slabs (slabstep.h)
+    long cnt_off, part_off;
 };
 
-static VGrad vgs_layout(float* base, bool bn = false) {
+// one segment per parameter tensor (named_parameters order), offsets from the gradstate base
+static int vgg_segments(const VGrad& g, const float* base, bool bn, SegSpec* s) {
+    const VOff o = voff(bn);
+    int i = 0;
+    for (int l = 0; l < 8; ++l) {
+        const VConv& c = VG[l];
+        s[i++] = SegSpec{g.sw[l] - base, c.ZW, (long)c.CO * c.KP, o.w[l], (long)c.CO * c.CI * 9,
+                         c.CO, c.CI, c.CIP, c.KP};
+        s[i++] = SegSpec{g.sb[l] - base, c.ZW, c.CO, o.b[l], c.CO, 0, 0, 1, 1};
+        if (bn) {
+            s[i++] = SegSpec{g.bnacc[l] - base, 1, c.CO, o.g[l], c.CO, 0, 0, 1, 1};
+            s[i++] = SegSpec{g.bnacc[l] + c.CO - base, 1, c.CO, o.be[l], c.CO, 0, 0, 1, 1};
+        }
+    }
+    s[i++] = SegSpec{g.l1w - base, VZL, (long)VFEAT * VFEAT, o.l1w, (long)VFEAT * VFEAT, 0, 0, 1, 1};
+    s[i++] = SegSpec{g.l1b - base, VZL, VFEAT, o.l1b, VFEAT, 0, 0, 1, 1};
+    s[i++] = SegSpec{g.l2w - base, VZL, (long)VFEAT * VFEAT, o.l2w, (long)VFEAT * VFEAT, 0, 0, 1, 1};
+    s[i++] = SegSpec{g.l2b - base, VZL, VFEAT, o.l2b, VFEAT, 0, 0, 1, 1};
+    s[i++] = SegSpec{g.l3w - base, VZH, 10L * VFEAT, o.l3w, 10L * VFEAT, 0, 0, 1, 1};
+    s[i++] = SegSpec{g.l3b - base, VZH, 10, o.l3b, 10, 0, 0, 1, 1};
+    return i;
+}
+
+static VGrad vgs_layout(float* base_in, bool bn = false) {
     VGrad g;
+    // offsets only (sizes, plan) when base_in is null: lay out over a fake base, never dereferenced
+    float* const base = base_in ? base_in : reinterpret_cast<float*>(4096);
     long o = 0;
     auto take = [&](long n) {
-        float* p = base ? base + o : nullptr;
+        float* p = base + o;
         o += (n + 63) / 64 * 64;
         return p;
     };
@@ -103,7 +131,7 @@ static VGrad vgs_layout(float* base, bool bn = false) {
         g.wd[l] = l ? take((long)VG[l].CI * 9 * VG[l].CO) : nullptr;
     }
     const long slab0 = o;
-    g.slab_begin = base ? base + o : nullptr;
+    g.slab_begin = base + o;
     for (int l = 0; l < 8; ++l) {
         g.sw[l] = take((long)VG[l].ZW * VG[l].CO * VG[l].KP);
         g.sb[l] = take((long)VG[l].ZW * VG[l].CO);
@@ -115,7 +143,13 @@ static VGrad vgs_layout(float* base, bool bn = false) {
     g.l3w = take((long)VZH * 10 * VFEAT);
     g.l3b = take((long)VZH * 10);
     for (int l = 0; l < 8; ++l) g.bnacc[l] = bn ? take(2L * VG[l].CO) : nullptr;
+    SegSpec specs[STEP_MAX_SEG];
+    plan_step(specs, vgg_segments(g, base, bn, specs), &g.plan);
+    g.cnt_off = o;
+    take(step_counter_floats(g.plan));
     g.slab_floats = o - slab0;
+    g.part_off = o;
+    take(step_partial_floats(g.plan));
     g.total_floats = o;
     return g;
 }
@@ -382,7 +416,8 @@ static int vbackward(const VGrad& g, const VWS& w, const float* th, const VOff& 
 template <bool BN>
 static int vrun_chunk(void* gradstate, const VWS& w, const float* theta, const WorkerRec* workers,
                       int n_chunk_workers, uint64_t seed, int dropout, int backward_pass,
-                      float* worker_loss, float* bn_stats, hipStream_t stream) {
+                      float* worker_loss, float* bn_stats, hipStream_t stream,
+                      float gscale = 1.f / SAMPLES_PER_WORKER) {
     const int S = n_chunk_workers * SAMPLES_PER_WORKER;
     const VOff o = voff(BN);
     VGrad g = vgs_layout((float*)gradstate, BN);
@@ -390,7 +425,7 @@ static int vrun_chunk(void* gradstate, const VWS& w, const float* theta, const W
     RC(vforward<BN>(g, w, theta, o, S, workers, seed, dropout, &bn, stream));
     // Linear(512,10) + CrossEntropyLoss (models.py:64, main.py:107); no dropout after the ReLU
     RC(head_and_loss<VFEAT>(w.e2, theta + o.l3w, theta + o.l3b, w.y, w.loss_s, w.dlog, w.dh2, S,
-                            backward_pass, 1.f, worker_loss, stream));
+                            backward_pass, 1.f, gscale, worker_loss, stream));
     if (backward_pass) RC(vbackward<BN>(g, w, theta, o, S, dropout, stream));
     return 0;
 }
@@ -454,18 +489,21 @@ static int vgg_fwd_bwd_input(void* gradstate, void* workspace, int max_samples,
                              hipStream_t stream) {
     FLSIM_REQUIRE(gradstate && workspace && theta && x && y && workers && worker_loss,
                   "null pointer");
-    FLSIM_REQUIRE(n_samples > 0 && n_samples % SAMPLES_PER_WORKER == 0,
-                  "batch of %d samples: must be a positive multiple of %d", n_samples,
+    FLSIM_REQUIRE(n_samples > 0, "empty batch");
+    // vgg11_bn: one BatchNorm batch per 128-sample group, so only whole groups
+    FLSIM_REQUIRE(!BN || n_samples % SAMPLES_PER_WORKER == 0,
+                  "vgg11_bn batch of %d samples: must be a multiple of %d", n_samples,
                   SAMPLES_PER_WORKER);
-    FLSIM_REQUIRE(n_samples <= max_samples, "batch of %d samples exceeds workspace (%d)", n_samples,
+    const int S = ceil_div(n_samples, SAMPLES_PER_WORKER) * SAMPLES_PER_WORKER;
+    FLSIM_REQUIRE(S <= max_samples, "batch of %d samples exceeds workspace (%d)", n_samples,
                   max_samples);
-    FLSIM_REQUIRE(n_samples <= 16384, "batch of %d samples exceeds the 32-bit index budget",
-                  n_samples);
+    FLSIM_REQUIRE(S <= 16384, "batch of %d samples exceeds the 32-bit index budget", n_samples);
     VWS w = vws_layout((char*)workspace, max_samples, BN);
-    hipLaunchKernelGGL(k_load_input, dim3(n_samples), dim3(256), 0, stream, x, y, w.x0, w.y);
+    hipLaunchKernelGGL(k_load_input, dim3(S), dim3(256), 0, stream, x, y, n_samples, w.x0, w.y);
     FLSIM_LAUNCH_CHECK();
-    return vrun_chunk<BN>(gradstate, w, theta, workers, n_samples / SAMPLES_PER_WORKER, seed,
-                          dropout, backward_pass, worker_loss, bn_stats, stream);
+    return vrun_chunk<BN>(gradstate, w, theta, workers, S / SAMPLES_PER_WORKER, seed, dropout,
+                          backward_pass, worker_loss, bn_stats, stream,
+                          BN ? 1.f / SAMPLES_PER_WORKER : 1.f / (float)n_samples);
 }
 
 // Evaluation (util.py:31-45 after central.model.eval(), main.py:190: dropout off; vgg11_bn:
@@ -473,8 +511,12 @@ static int vgg_fwd_bwd_input(void* gradstate, void* workspace, int max_samples,
 template <bool BN>
 static int vgg_eval_pool(void* gradstate, void* workspace, int max_samples, const float* theta,
                          const uint8_t* pool, int first, int n_images, const float* lut,
-                         const float* running, int32_t* pred, hipStream_t stream) {
-    FLSIM_REQUIRE(gradstate && workspace && theta && pool && lut && pred, "null pointer");
+                         const float* running, int32_t* pred, hipStream_t stream,
+                         const float* xin = nullptr) {
+    // xin != nullptr: an explicit NCHW fp32 batch (util.py:31-45 over a test loader) instead of
+    // pool images
+    FLSIM_REQUIRE(gradstate && workspace && theta && (xin || (pool && lut)) && pred,
+                  "null pointer");
     FLSIM_REQUIRE(!BN || running, "null running buffers");
     FLSIM_REQUIRE(n_images > 0 && first >= 0, "bad image range");
     FLSIM_REQUIRE(max_samples >= SAMPLES_PER_WORKER && max_samples % SAMPLES_PER_WORKER == 0,
@@ -485,11 +527,16 @@ static int vgg_eval_pool(void* gradstate, void* workspace, int max_samples, cons
     RC(vpack(g, theta, o, stream));
     const VBN bn{&w, 0, nullptr};
     if (BN) RC(vbn_eval_coef(w, running, stream));
-    for (int c0 = 0; c0 < n_images; c0 += max_samples) {
-        const int n = n_images - c0 < max_samples ? n_images - c0 : max_samples;
+    const int cap = max_samples < 16384 ? max_samples : 16384;   // 32-bit index budget
+    for (int c0 = 0; c0 < n_images; c0 += cap) {
+        const int n = n_images - c0 < cap ? n_images - c0 : cap;
         const int S = ceil_div(n, SAMPLES_PER_WORKER) * SAMPLES_PER_WORKER;
-        hipLaunchKernelGGL(k_fill_seq, dim3(S), dim3(256), 0, stream, pool, first + c0, n, lut,
-                           w.x0, w.y);
+        if (xin)
+            hipLaunchKernelGGL(k_load_input, dim3(S), dim3(256), 0, stream, xin + (long)c0 * 3072,
+                               (const int64_t*)nullptr, n, w.x0, w.y);
+        else
+            hipLaunchKernelGGL(k_fill_seq, dim3(S), dim3(256), 0, stream, pool, first + c0, n, lut,
+                               w.x0, w.y);
         FLSIM_LAUNCH_CHECK();
         RC(vforward<BN>(g, w, theta, o, S, nullptr, 0, 0, &bn, stream));
         RC(head_predict<VFEAT>(w.e2, theta + o.l3w, theta + o.l3b, w.y, w.loss_s, S, pred + c0, n,
@@ -502,25 +549,24 @@ static int vgg_eval_pool(void* gradstate, void* workspace, int max_samples, cons
 template <bool BN>
 static int vgg_end_epoch(void* gradstate, float* grad_out, hipStream_t stream) {
     FLSIM_REQUIRE(gradstate && grad_out, "null pointer");
-    const VOff o = voff(BN);
     VGrad g = vgs_layout((float*)gradstate, BN);
-    for (int l = 0; l < 8; ++l) {
-        const VConv& c = VG[l];
-        RC(fin_sum(g.sw[l], c.ZW, (long)c.CO * c.KP, grad_out + o.w[l], stream, c.CO, c.CI, c.CIP,
-                   c.KP));
-        RC(fin_sum(g.sb[l], c.ZW, c.CO, grad_out + o.b[l], stream));
-        if (BN) {
-            RC(fin_sum(g.bnacc[l], 1, c.CO, grad_out + o.g[l], stream));
-            RC(fin_sum(g.bnacc[l] + c.CO, 1, c.CO, grad_out + o.be[l], stream));
-        }
-    }
-    RC(fin_sum(g.l1w, VZL, (long)VFEAT * VFEAT, grad_out + o.l1w, stream));
-    RC(fin_sum(g.l1b, VZL, VFEAT, grad_out + o.l1b, stream));
-    RC(fin_sum(g.l2w, VZL, (long)VFEAT * VFEAT, grad_out + o.l2w, stream));
-    RC(fin_sum(g.l2b, VZL, VFEAT, grad_out + o.l2b, stream));
-    RC(fin_sum(g.l3w, VZH, 10L * VFEAT, grad_out + o.l3w, stream));
-    RC(fin_sum(g.l3b, VZH, 10, grad_out + o.l3b, stream));
-    return 0;
+    return slab_step_launch((float*)gradstate, g.plan, g.cnt_off, g.part_off, grad_out, nullptr,
+                            nullptr, nullptr, nullptr, nullptr, voff(BN).total, stream);
+}
+
+// the same reduction fused with rule() + Adam (world = 1)
+template <bool BN>
+static int vgg_server_step(void* gradstate, float* S_out, const flsim_rule* rule, float* p,
+                           float* m, float* v, long step, double lr, double beta1, double beta2,
+                           double eps, hipStream_t stream) {
+    FLSIM_REQUIRE(gradstate && rule && p && m && v, "null pointer");
+    VGrad g = vgs_layout((float*)gradstate, BN);
+    RuleProg R;
+    RC(make_rule(rule, &R));
+    AdamConst ac;
+    RC(make_adam_const(rule->k, step, lr, beta1, beta2, eps, &ac));
+    return slab_step_launch((float*)gradstate, g.plan, g.cnt_off, g.part_off, S_out, &R, &ac, p,
+                            m, v, voff(BN).total, stream);
 }
 
 }  // namespace flsim
@@ -576,8 +622,21 @@ int flsim_vgg11_eval_pool(void* gradstate, void* workspace, int max_samples, con
                                 lut, nullptr, pred, stream);
 }
 
+int flsim_vgg11_eval_input(void* gradstate, void* workspace, int max_samples, const float* theta,
+                           const float* x, int n_images, int32_t* pred, hipStream_t stream) {
+    return vgg_eval_pool<false>(gradstate, workspace, max_samples, theta, nullptr, 0, n_images,
+                                nullptr, nullptr, pred, stream, x);
+}
+
 int flsim_vgg11_end_epoch(void* gradstate, float* grad_out, hipStream_t stream) {
     return vgg_end_epoch<false>(gradstate, grad_out, stream);
+}
+
+int flsim_vgg11_server_step(void* gradstate, float* S_out, const flsim_rule* rule, float* p,
+                            float* m, float* v, long step, double lr, double beta1, double beta2,
+                            double eps, hipStream_t stream) {
+    return vgg_server_step<false>(gradstate, S_out, rule, p, m, v, step, lr, beta1, beta2, eps,
+                                  stream);
 }
 
 // ---- vgg11_bn -------------------------------------------------------------------------------
@@ -630,8 +689,22 @@ int flsim_vgg11_bn_eval_pool(void* gradstate, void* workspace, int max_samples,
                                lut, running, pred, stream);
 }
 
+int flsim_vgg11_bn_eval_input(void* gradstate, void* workspace, int max_samples,
+                              const float* theta, const float* x, int n_images,
+                              const float* running, int32_t* pred, hipStream_t stream) {
+    return vgg_eval_pool<true>(gradstate, workspace, max_samples, theta, nullptr, 0, n_images,
+                               nullptr, running, pred, stream, x);
+}
+
 int flsim_vgg11_bn_end_epoch(void* gradstate, float* grad_out, hipStream_t stream) {
     return vgg_end_epoch<true>(gradstate, grad_out, stream);
+}
+
+int flsim_vgg11_bn_server_step(void* gradstate, float* S_out, const flsim_rule* rule, float* p,
+                               float* m, float* v, long step, double lr, double beta1,
+                               double beta2, double eps, hipStream_t stream) {
+    return vgg_server_step<true>(gradstate, S_out, rule, p, m, v, step, lr, beta1, beta2, eps,
+                                 stream);
 }
 
 int flsim_vgg11_bn_update_running(float* running, const float* bn_stats, int n_workers,

@@ -26,7 +26,10 @@ EXPORTS = [
     "flsim_vgg11_bn_stats_per_worker", "flsim_vgg11_bn_begin_epoch",
     "flsim_vgg11_bn_fwd_bwd_chunk", "flsim_vgg11_bn_fwd_bwd_input", "flsim_vgg11_bn_end_epoch",
     "flsim_vgg11_bn_eval_pool", "flsim_vgg11_bn_update_running",
-    "flsim_aggregate_adam", "flsim_aggregate_adam_seq", "flsim_aggregate_adam_sum",
+    "flsim_pn1_eval_input", "flsim_vgg11_eval_input", "flsim_vgg11_bn_eval_input",
+    "flsim_pn1_server_step", "flsim_vgg11_server_step", "flsim_vgg11_bn_server_step",
+    "flsim_aggregate_adam", "flsim_aggregate_adam_rule", "flsim_aggregate_adam_sum",
+    "flsim_cascade_program", "flsim_cascade_eval_host",
     "flsim_probe_enable", "flsim_probe_read", "flsim_probe_disable",
     "flsim_probe_kernel_count", "flsim_probe_kernel_name",
 ]
@@ -34,6 +37,16 @@ EXPORTS = [
 
 class FLSimError(RuntimeError):
     pass
+
+
+MAX_ARRAYS = 64          # FLSIM_MAX_ARRAYS
+
+
+class FlsimRule(ctypes.Structure):
+    """flsim_rule (include/flsim.h): weight_ups of one rule() call."""
+    _fields_ = [("k", ctypes.c_int32), ("c", ctypes.c_int32), ("prog", ctypes.c_void_p),
+                ("info", ctypes.c_int32 * 4), ("n_arrays", ctypes.c_int32),
+                ("arrays", ctypes.c_void_p * MAX_ARRAYS)]
 
 
 class WorkerRec(ctypes.Structure):
@@ -77,6 +90,9 @@ def lib():
             vp, vp, ctypes.c_int, vp, vp, vp, ctypes.c_int, vp, ctypes.c_uint64, ctypes.c_int,
             ctypes.c_int, vp] + bn + [vp]
         f("end_epoch").argtypes = [vp, vp, vp]
+        f("eval_input").argtypes = [vp, vp, ctypes.c_int, vp, vp, ctypes.c_int] + bn + [vp, vp]
+        f("server_step").argtypes = [vp, vp, vp, vp, vp, vp, ctypes.c_long, ctypes.c_double,
+                                     ctypes.c_double, ctypes.c_double, ctypes.c_double, vp]
         f("eval_pool").argtypes = [vp, vp, ctypes.c_int, vp, vp, ctypes.c_int, ctypes.c_int,
                                    vp] + bn + [vp, vp]
     L.flsim_vgg11_bn_update_running.argtypes = [vp, vp, ctypes.c_int, vp]
@@ -86,10 +102,11 @@ def lib():
     L.flsim_aggregate_adam_sum.argtypes = [
         vp, ctypes.c_int, vp, vp, vp, ctypes.c_long, vp, ctypes.c_int,
         ctypes.c_long, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp]
-    L.flsim_aggregate_adam_seq.argtypes = [
-        vp, ctypes.c_int, vp, ctypes.c_int, vp, ctypes.c_int, vp, vp, vp, ctypes.c_long, vp,
-        ctypes.c_int,
+    L.flsim_aggregate_adam_rule.argtypes = [
+        vp, vp, vp, vp, vp, ctypes.c_long, vp, ctypes.c_int,
         ctypes.c_long, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp]
+    L.flsim_cascade_program.argtypes = [ctypes.c_int, vp, vp, ctypes.c_int, vp, ctypes.c_int, vp]
+    L.flsim_cascade_eval_host.argtypes = [vp, vp, vp, vp, ctypes.c_int, vp, ctypes.c_long, vp]
     L.flsim_probe_enable.argtypes = [ctypes.c_int]
     L.flsim_probe_read.argtypes = [vp, vp, vp]
     L.flsim_probe_kernel_name.restype = ctypes.c_char_p
@@ -104,6 +121,8 @@ def check(rc):
         if rc == 1:
             if "IndexError" in msg:
                 raise IndexError(msg)
+            if "ZeroDivisionError" in msg:
+                raise ZeroDivisionError(msg)
             raise ValueError(msg)
         raise FLSimError(msg)
 

@@ -17,7 +17,7 @@ import ctypes
 import numpy as np
 import torch
 
-from ._lib import WorkerRec, check, lib, ptr, stream_ptr
+from ._lib import MAX_ARRAYS, FlsimRule, WorkerRec, check, lib, ptr, stream_ptr
 
 # named_parameters() order of models.py:PerformantNet1 (models.py:13-25)
 PN1_SHAPES = [
@@ -123,6 +123,17 @@ class NetEngine:
             int(n_chunk), int(n_workers_total), ctypes.c_uint64(seed), int(bool(dropout)),
             int(bool(backward)), ptr(loss_out), *self._stats_arg(stats_out), stream_ptr()))
 
+    def evaluate_input(self, theta, x):
+        """Predictions for an explicit NCHW fp32 batch (util.py:31-45's model(images) in eval
+        mode): device int32 tensor of argmax indices."""
+        x = x.to(self.device, torch.float32).contiguous()
+        n = int(x.shape[0])
+        pred = torch.empty(n, dtype=torch.int32, device=self.device)
+        extra = (ptr(self.running),) if self.STATS_PER_WORKER else ()
+        check(self._fn("eval_input")(ptr(self.gradstate), ptr(self.workspace), self.max_samples,
+                                     ptr(theta), ptr(x), n, *extra, ptr(pred), stream_ptr()))
+        return pred
+
     def run_input(self, theta, x, y, workers_dev, seed, dropout, loss_out, backward=True,
                   stats_out=None):
         x = x.contiguous()
@@ -157,6 +168,13 @@ class NetEngine:
     def end_epoch(self, grad_out):
         check(self._fn("end_epoch")(ptr(self.gradstate), ptr(grad_out), stream_ptr()))
 
+    def server_step(self, S_out, rule, theta, m, v, step, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
+        """world = 1: the epoch's slabs -> S_t [-> S_out] -> rule() + Adam in one launch
+        (flsim_<net>_server_step).  rule: a Rule."""
+        check(self._fn("server_step")(
+            ptr(self.gradstate), ptr(S_out), ctypes.byref(rule.c_rule), ptr(theta), ptr(m), ptr(v),
+            int(step), float(lr), float(betas[0]), float(betas[1]), float(eps), stream_ptr()))
+
     def workspace_view(self, which, shape, dtype=torch.float32, samples=None):
         """Debug view of a workspace tensor by id (PN1Engine.WORKSPACE / VGG11Engine.WORKSPACE)."""
         off = ctypes.c_long()
@@ -173,9 +191,8 @@ class NetEngine:
     def aggregate_adam_sum(self, S, k, theta, m, v, step, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
         aggregate_adam_sum(S, k, theta, m, v, step, self.SIZES, lr, betas, eps)
 
-    def aggregate_adam_seq(self, S, k, events, arrays, theta, m, v, step, lr=1e-3,
-                           betas=(0.9, 0.999), eps=1e-8):
-        aggregate_adam_seq(S, k, events, arrays, theta, m, v, step, self.SIZES, lr, betas, eps)
+    def aggregate_rule(self, S, rule, theta, m, v, step, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
+        aggregate_rule(S, rule, theta, m, v, step, self.SIZES, lr, betas, eps)
 
 
 class PN1Engine(NetEngine):
@@ -288,20 +305,93 @@ def aggregate_adam_sum(S, k, theta, m, v, step, sizes, lr=1e-3, betas=(0.9, 0.99
         int(step), float(lr), float(betas[0]), float(betas[1]), float(eps), stream_ptr()))
 
 
-def aggregate_adam_seq(S, k, events, arrays, theta, m, v, step, sizes, lr=1e-3,
-                       betas=(0.9, 0.999), eps=1e-8):
-    """rule() + Adam for weight_ups in general order (heterogeneous-delay extension): k entries,
-    events = [(position, array index)] of the non-S_t entries sorted by position, arrays = device
-    tensors (None = zeros).  The small event / pointer tables are copied to the device here."""
-    dev = S.device
-    ev = torch.tensor(np.asarray(events, np.int32).reshape(-1, 2), device=dev)
-    tab = torch.tensor([(a.data_ptr() if a is not None else 0) for a in arrays] or [0],
-                       dtype=torch.int64, device=dev)
+def cascade_program(k, events):
+    """rule()'s summation program (host, flsim_cascade_program) for k entries whose non-S_t
+    entries are events = [(position, array index)] (positions increasing).  -> (int32 words,
+    info[4])."""
+    ev = np.asarray(events, np.int32).reshape(-1, 2)
+    pos = np.ascontiguousarray(ev[:, 0])
+    arr = np.ascontiguousarray(ev[:, 1])
+    cap = 64 + 40 * (len(ev) + 8)
+    prog = np.zeros(cap, np.int32)
+    info = np.zeros(4, np.int32)
+    vp = ctypes.c_void_p
+    check(lib().flsim_cascade_program(int(k), pos.ctypes.data_as(vp), arr.ctypes.data_as(vp),
+                                      len(ev), prog.ctypes.data_as(vp), cap,
+                                      info.ctypes.data_as(vp)))
+    return prog[:info[0]].copy(), info
+
+
+class Rule:
+    """weight_ups of one rule() call (flsim_rule): k entries (the mean's divisor); either the
+    reference order [S_t] * c + arrays, or a general order given as events [(position, array
+    index)] whose program is built on the host and staged to the device (`stager`).  arrays:
+    device tensors or None (a zero entry, torch-1.x)."""
+
+    def __init__(self, k, arrays=(), c=None, events=None, stager=None):
+        arrays = list(arrays)
+        if len(arrays) > MAX_ARRAYS:
+            raise NotImplementedError(f"{len(arrays)} distinct weight_ups arrays in one step "
+                                      f"(max {MAX_ARRAYS})")
+        r = FlsimRule()
+        r.k = int(k)
+        r.n_arrays = len(arrays)
+        for q, a in enumerate(arrays):
+            r.arrays[q] = a.data_ptr() if a is not None else None
+        self.arrays = arrays            # keep the tensors alive with the rule
+        self.k, self.c, self.events = int(k), c, events
+        if events is None:
+            r.c = int(c)
+            r.prog = None
+            self.prog_dev = None
+        else:
+            words, info = cascade_program(k, events)
+            self.prog_dev = stager.upload(words)
+            r.c = -1
+            r.prog = self.prog_dev.data_ptr()
+            for j in range(4):
+                r.info[j] = int(info[j])
+        self.c_rule = r
+
+
+class ProgramStager:
+    """Pinned host -> device staging of rule programs, double-buffered.  The host waits only for
+    the copy out of a pinned buffer two uploads ago; the device buffer is rewritten two uploads
+    later, behind (stream order) the launch that reads it now."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.cap = 0
+        self.i = 0
+
+    def upload(self, words):
+        n = int(words.size)
+        if n > self.cap:
+            self.cap = max(1024, 2 * n)
+            pin = self.device.type == "cuda"
+            self.host = [torch.empty(self.cap, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
+            self.dev = [torch.empty(self.cap, dtype=torch.int32, device=self.device)
+                        for _ in range(2)]
+            self.ev = [None, None]
+        j = self.i = self.i ^ 1
+        if self.ev[j] is not None:
+            self.ev[j].synchronize()
+        self.host[j][:n].numpy()[:] = words
+        self.dev[j][:n].copy_(self.host[j][:n], non_blocking=True)
+        if self.device.type == "cuda":
+            ev = torch.cuda.Event()
+            ev.record()
+            self.ev[j] = ev
+        return self.dev[j]
+
+
+def aggregate_rule(S, rule, theta, m, v, step, sizes, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
+    """rule() + Adam from S_t in a buffer (flsim_aggregate_adam_rule)."""
     csz = (ctypes.c_long * len(sizes))(*[int(n) for n in sizes])
-    check(lib().flsim_aggregate_adam_seq(
-        ptr(S), int(k), ptr(ev), len(events), ptr(tab), len(arrays), ptr(theta), ptr(m), ptr(v),
-        sum(int(n) for n in sizes), csz, len(sizes), int(step), float(lr), float(betas[0]),
-        float(betas[1]), float(eps), stream_ptr()))
+    check(lib().flsim_aggregate_adam_rule(
+        ptr(S), ctypes.byref(rule.c_rule), ptr(theta), ptr(m), ptr(v), sum(int(n) for n in sizes),
+        csz, len(sizes), int(step), float(lr), float(betas[0]), float(betas[1]), float(eps),
+        stream_ptr()))
 
 
 def worker_table(recs, device):

@@ -20,10 +20,14 @@ class EpochPlan:
     pushed: bool                # a slow worker stored S_t in its FIFO this epoch
 
 
+DELAY_ZERO = -(1 << 31)     # FLSIM_DELAY_ZERO: the slow worker under --delay 0
+
+
 def reference_delays(n, delay):
-    """main.py: exactly one slow worker, index n-1, with --delay."""
+    """main.py: exactly one slow worker, index n-1, with --delay (main.py:150 tests the index,
+    not the delay: under --delay 0 worker n-1 is still the slow one, DELAY_ZERO)."""
     d = np.zeros(n, np.int32)
-    d[n - 1] = delay
+    d[n - 1] = delay if delay != 0 else DELAY_ZERO
     return d
 
 

@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from .data import DevicePool, make_test_pool
-from .engine import PN1_SIZES, engine_class, padded, split_views
+from .engine import PN1_SIZES, ProgramStager, Rule, engine_class, padded, split_views
 from .schedule import Schedule, reference_delays
 
 SEMANTICS = ("reference", "torch1", "independent")
@@ -54,7 +54,8 @@ class FLSimulation:
     def __init__(self, n_workers, delay=100, delays=None, throttle=False, lr=1e-3, seed=0,
                  semantics="reference", dropout=True, chunk_workers=128, device=None, theta0=None,
                  group=None, max_throttle=32, pool=None, betas=(0.9, 0.999), eps=1e-8,
-                 engine=None, device_pool=None, test_pool=None, model="PerformantNet1"):
+                 engine=None, device_pool=None, test_pool=None, model="PerformantNet1",
+                 fused=True, keep_S=False):
         if semantics not in SEMANTICS:
             raise NotImplementedError(f"semantics {semantics!r} (supported: {SEMANTICS})")
         self.n = int(n_workers)
@@ -68,6 +69,10 @@ class FLSimulation:
         self.seed = int(seed)
         self.semantics = semantics
         self.dropout = bool(dropout)
+        # fused: at world = 1 the epoch ends in ONE launch, slabs -> S_t -> rule() + Adam
+        # (flsim_<net>_server_step); keep_S also writes S_t into comm[:P] (tests, debugging)
+        self.fused = bool(fused)
+        self.keep_S = bool(keep_S)
         self.group = group
         self.model = model
         dist = torch.distributed
@@ -85,6 +90,7 @@ class FLSimulation:
             engine_class(model)(self.device, min(int(chunk_workers), self.n))
         self.pool = device_pool if device_pool is not None else \
             DevicePool(self.device, self.seed, pool)
+        self.max_throttle = int(max_throttle)
         self.sched = Schedule(self.n, self.delays, self.throttle, max_throttle)
         self.rs = np.random.RandomState(self.seed)   # main.py:138 np.random stream
         P = self.engine.P
@@ -102,6 +108,7 @@ class FLSimulation:
             raise NotImplementedError("independent entries with BatchNorm models")
         self.stats_off = self.Ppad + padded(self.n)
         self.comm = torch.zeros(self.stats_off + self.n * self.nstat, device=self.device)
+        self._stager = ProgramStager(self.device)
         self.stale_store = {}     # epoch -> [slot tensor, refcount]
         self.free_slots = []
         self.trace = []
@@ -144,6 +151,23 @@ class FLSimulation:
             self._wt_ev[j] = ev
         return dev
 
+    def _rule(self, plan, stale):
+        """weight_ups of this epoch as a Rule: k = c_t + s_t entries, the stale ones in append
+        (worker-index) order; identical arrays (several FIFOs popping the same epoch) share one
+        array index."""
+        k = plan.c_t + plan.s_t
+        order = self._entry_order(plan)
+        if order is None:       # reference order: c_t copies of S_t, then the stale entries
+            return Rule(k, stale, c=plan.c_t)
+        uniq, ev = [], []
+        for pos, a in zip(order[0], stale):
+            j = next((q for q, u in enumerate(uniq) if u is a), None)
+            if j is None:
+                uniq.append(a)
+                j = len(uniq) - 1
+            ev.append((pos, j))
+        return Rule(k, uniq, events=ev, stager=self._stager)
+
     @staticmethod
     def _entry_order(plan):
         """None when weight_ups is [S_t] * c_t followed by <= 8 stale entries (the reference:
@@ -174,10 +198,10 @@ class FLSimulation:
         return lo, hi
 
     def epoch(self, sync_loss=True):
-        plan = self.sched.next_epoch()          # raises IndexError like rule() on empty weight_ups
+        # raises IndexError like rule() on an empty weight_ups, ZeroDivisionError like main.py:158
+        # under --delay 0
+        plan = self.sched.next_epoch()
         t = plan.t
-        if t >= 1 and self.delay_arg == 0 and self.delays[self.n - 1] == 0:
-            raise ZeroDivisionError("integer division or modulo by zero")   # main.py:158
         ks = self.rs.randint(0, self.n, size=self.n)
         if self.semantics == "independent":
             return self._epoch_independent(plan, ks, sync_loss)
@@ -197,18 +221,22 @@ class FLSimulation:
             kw = {"stats_out": stats[c0:c1]} if self.nstat else {}
             eng.run_chunk(self.theta, self.pool, wt[c0 - lo:c1 - lo], c1 - c0, self.n, self.seed,
                           self.dropout, losses[c0:c1], **kw)
-        eng.end_epoch(S)
+        fused = self.fused and self.world == 1 and hasattr(eng, "server_step")
+        if not fused or self.keep_S:
+            eng.end_epoch(S)
         if self.world > 1:
             end = self.stats_off + len(active) * self.nstat if self.nstat else \
                 self.Ppad + len(active)
             torch.distributed.all_reduce(self.comm[:end], group=self.group)
         if self.nstat:   # BatchNorm running buffers: every computing worker's call, in order
             eng.update_running(stats, len(active))
+        push = None
         if plan.pushed and self.semantics == "reference":
             n_push = int(sum(1 for i in range(self.n) if self.delays[i] != 0 and plan.computes[i]))
-            slot = self._slot()
-            slot[:self.P].copy_(S)
-            self.stale_store[t] = [slot, n_push]
+            push = self._slot()
+            if not fused or self.keep_S:
+                push[:self.P].copy_(S)
+            self.stale_store[t] = [push, n_push]
         stale = []
         for (_, src) in plan.stale:
             if self.semantics == "reference":
@@ -217,21 +245,12 @@ class FLSimulation:
             else:
                 stale.append(None)
         self.step += 1
-        order = self._entry_order(plan)
-        if order is None:       # reference order: c_t copies of S_t, then the stale entries
-            eng.aggregate_adam(S, plan.c_t, stale, self.theta, self.m, self.v, self.step,
-                               self.lr, self.betas, self.eps)
-        else:                   # stale entries interleaved in worker order (extension)
-            events, arrays = order
-            uniq, ev = [], []
-            for pos, a in zip(events, stale):
-                j = next((q for q, u in enumerate(uniq) if u is a), None)
-                if j is None:
-                    uniq.append(a)
-                    j = len(uniq) - 1
-                ev.append((pos, j))
-            eng.aggregate_adam_seq(S, plan.c_t + plan.s_t, ev, uniq, self.theta, self.m, self.v,
-                                   self.step, self.lr, self.betas, self.eps)
+        rule = self._rule(plan, stale)
+        hp = dict(lr=self.lr, betas=self.betas, eps=self.eps)
+        if fused and not self.keep_S:
+            eng.server_step(push, rule, self.theta, self.m, self.v, self.step, **hp)
+        else:
+            eng.aggregate_rule(S, rule, self.theta, self.m, self.v, self.step, **hp)
         for (_, src) in plan.stale:
             if self.semantics == "reference":
                 entry = self.stale_store[src]
@@ -363,7 +382,8 @@ class FLSimulation:
             "config": {"n": self.n, "delays": torch.from_numpy(self.delays.copy()),
                        "model": self.model,
                        "throttle": self.throttle, "seed": self.seed, "semantics": self.semantics,
-                       "dropout": self.dropout, "lr": self.lr},
+                       "dropout": self.dropout, "lr": self.lr, "betas": list(self.betas),
+                       "eps": self.eps, "max_throttle": self.max_throttle},
             "epoch": len(self.trace), "step": self.step,
             "theta": self.theta.detach().cpu(), "m": self.m.detach().cpu(),
             "v": self.v.detach().cpu(),
@@ -385,10 +405,12 @@ class FLSimulation:
             raise ValueError("not an flsim checkpoint")
         cfg = ck["config"]
         mine = {"n": self.n, "throttle": self.throttle, "seed": self.seed,
-                "semantics": self.semantics, "dropout": self.dropout, "model": self.model}
+                "semantics": self.semantics, "dropout": self.dropout, "model": self.model,
+                "lr": self.lr, "betas": list(self.betas), "eps": self.eps,
+                "max_throttle": self.max_throttle}
         for k, v in mine.items():
             if cfg.get(k, "PerformantNet1" if k == "model" else None) != v:
-                raise ValueError(f"checkpoint {k}={cfg[k]!r} differs from this run ({v!r})")
+                raise ValueError(f"checkpoint {k}={cfg.get(k)!r} differs from this run ({v!r})")
         if not np.array_equal(cfg["delays"].numpy(), self.delays):
             raise ValueError("checkpoint delays differ from this run")
         if self.trace:

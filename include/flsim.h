@@ -34,8 +34,11 @@ const char* flsim_last_error(void);
 /* ---------------------------------------------------------------------------------------------
  * Schedule (host): replaces the integer scan of main.py:119-123 (state), :150-166 (slow worker
  * + pesky_worker_grads FIFO), :167-178 (fast worker + throttle), :180-181 (window decrement).
- * delays[i] != 0 marks a slow worker (reference: only i = n-1, delay = --delay).
+ * delays[i] != 0 marks a slow worker (reference: only i = n-1, delay = --delay);
+ * FLSIM_DELAY_ZERO marks the reference's slow worker under --delay 0: it computes and pushes at
+ * t = 0 (main.py:153-157), and the epoch t = 1 fails like main.py:158's t % 0.
  * ------------------------------------------------------------------------------------------- */
+#define FLSIM_DELAY_ZERO ((int32_t)0x80000000)
 typedef struct flsim_sched flsim_sched;
 flsim_sched* flsim_sched_create(int32_t n, const int32_t* delays, int32_t throttle,
                                 int32_t max_throttle);
@@ -70,12 +73,19 @@ int flsim_pn1_fwd_bwd_chunk(void* gradstate, void* workspace, int max_samples, c
                             uint64_t seed, int dropout, int backward_pass, float* worker_loss,
                             flsim_stream_t stream);
 /* explicit batch variant (Worker.fwd_bkwd(inp, outp), agents.py:32): x NCHW fp32 [n][3][32][32],
- * y int64 [n], n a multiple of 128; workers[n/128] give the dropout RNG keys */
+ * y int64 [n], any n >= 1 (main.py:43-44 --batch_size; at most 16384): padded to whole groups of
+ * 128 samples that add nothing; the gradient is CrossEntropyLoss's mean over the n samples
+ * (agents.py:34-35).  workers[ceil(n/128)] give each group's dropout RNG key; worker_loss[g] =
+ * group g's summed loss / 128 (so the batch loss = sum_g worker_loss[g] * 128 / n). */
 int flsim_pn1_fwd_bwd_input(void* gradstate, void* workspace, int max_samples, const float* theta,
                             const float* x, const int64_t* y, int n_samples,
                             const WorkerRec* workers, uint64_t seed, int dropout,
                             int backward_pass, float* worker_loss, flsim_stream_t stream);
 int flsim_pn1_end_epoch(void* gradstate, float* grad_out, flsim_stream_t stream);
+/* eval of an explicit batch (util.py:31-45 print_test_accuracy's model(images), dropout off):
+ * x NCHW fp32 [n_images][3][32][32] -> pred (device int32[n_images]) */
+int flsim_pn1_eval_input(void* gradstate, void* workspace, int max_samples, const float* theta,
+                         const float* x, int n_images, int32_t* pred, flsim_stream_t stream);
 /* Evaluation: replaces util.print_test_accuracy (util.py:31-45) as called at main.py:196-210
  * after central.model.eval() (main.py:190: dropout off).  Forward of pool images
  * [first, first + n_images) (u8 NCHW 3x32x32, normalised through `lut`), predictions = argmax of
@@ -109,6 +119,8 @@ int flsim_vgg11_fwd_bwd_input(void* gradstate, void* workspace, int max_samples,
                               const WorkerRec* workers, uint64_t seed, int dropout,
                               int backward_pass, float* worker_loss, flsim_stream_t stream);
 int flsim_vgg11_end_epoch(void* gradstate, float* grad_out, flsim_stream_t stream);
+int flsim_vgg11_eval_input(void* gradstate, void* workspace, int max_samples, const float* theta,
+                           const float* x, int n_images, int32_t* pred, flsim_stream_t stream);
 int flsim_vgg11_eval_pool(void* gradstate, void* workspace, int max_samples, const float* theta,
                           const uint8_t* pool, int first, int n_images, const float* lut,
                           int32_t* pred, flsim_stream_t stream);
@@ -143,6 +155,10 @@ int flsim_vgg11_bn_fwd_bwd_input(void* gradstate, void* workspace, int max_sampl
                                  int dropout, int backward_pass, float* worker_loss,
                                  float* bn_stats, flsim_stream_t stream);
 int flsim_vgg11_bn_end_epoch(void* gradstate, float* grad_out, flsim_stream_t stream);
+/* vgg11_bn: explicit batches must be whole 128-sample groups (one BatchNorm batch each) */
+int flsim_vgg11_bn_eval_input(void* gradstate, void* workspace, int max_samples,
+                              const float* theta, const float* x, int n_images,
+                              const float* running, int32_t* pred, flsim_stream_t stream);
 /* util.py:31-45 in eval mode: BatchNorm normalises with the running buffers `running`. */
 int flsim_vgg11_bn_eval_pool(void* gradstate, void* workspace, int max_samples,
                              const float* theta, const uint8_t* pool, int first, int n_images,
@@ -154,35 +170,71 @@ int flsim_vgg11_bn_update_running(float* running, const float* bn_stats, int n_w
                                   flsim_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
- * Fused server step: replaces Agg.rule = rule() (main.py:23-25, agents.py:43-45: per-tensor
+ * Server step: replaces Agg.rule = rule() (main.py:23-25, agents.py:43-45: per-tensor
  * torch.stack(weight_ups).mean(0)) + Central.update_model (agents.py:9-21: Adam step,
- * main.py:106).  weight_ups = c copies of S (the aliased fast entries) followed by n_stale stale
- * entries (nullptr entry = zeros, the torch-1.x semantics).  Bit-exact with torch 2.10 CPU
- * except sqrt rounding.  step = Adam step count after increment.
+ * main.py:106).  Bit-exact with torch 2.10 CPU except sqrt rounding;
+ * step = Adam step count after increment.
+ *
+ * flsim_rule describes weight_ups: the entries are S_t (every fast worker's aliased .grad,
+ * main.py:172) or one of `arrays` (popped stale FIFO entries, main.py:161-165; NULL = zeros, the
+ * torch-1.x semantics).
+ *   prog == NULL : reference order, [S_t] * c followed by arrays[0 .. n_arrays) (the slow worker
+ *                  is the last worker, main.py:150);
+ *   prog != NULL : general order (heterogeneous-delay extension, SURVEY 8 a1: entries appended in
+ *                  worker-index order): a device program from flsim_cascade_program, info = its
+ *                  info words.
+ * k is the divisor of the mean (= the entry count, main.py:24; the independent-entry semantics
+ * passes S = the sum of k distinct entries with c = 1).
  * ------------------------------------------------------------------------------------------- */
+#define FLSIM_MAX_ARRAYS 64
+typedef struct flsim_rule {
+    int32_t k;
+    int32_t c;
+    const int32_t* prog;
+    int32_t info[4];
+    int32_t n_arrays;
+    const float* arrays[FLSIM_MAX_ARRAYS];
+} flsim_rule;
+
+/* host: the summation program of rule() over k entries whose non-S_t entries sit at positions
+ * pos[0 .. n_events) (increasing) and hold arrays arr[] (indices into flsim_rule.arrays);
+ * info[4] = {length, row_sum offset, flags, level power}.  k <= 524288. */
+int flsim_cascade_program(int k, const int32_t* pos, const int32_t* arr, int n_events,
+                          int32_t* prog, int cap, int32_t* info);
+/* host (testing): run a program on the host, out[e] = cascade sum for element e (x = S[e],
+ * entry arrays ys[q][e]; tail[e] != 0 selects the row_sum part) */
+int flsim_cascade_eval_host(const int32_t* prog, const int32_t* info, const float* S,
+                            const float* const* ys, int n_arrays, const uint8_t* tail, long n,
+                            float* out);
+
+/* rule() + Adam from S_t in a buffer (world > 1 after the all-reduce; the FL.agents facade).
+ * tensor_sizes: numel of each parameter tensor in named_parameters order (the cascade's column
+ * rule is per tensor). */
+int flsim_aggregate_adam_rule(const float* S, const flsim_rule* rule, float* p, float* m, float* v,
+                              long P, const long* tensor_sizes, int n_tensors, long step, double lr,
+                              double beta1, double beta2, double eps, flsim_stream_t stream);
+/* convenience forms of the above: reference order with n_stale <= 8 stale entries; and the
+ * independent-entry semantics (S = sum of k distinct entries, mean = S / k) */
 int flsim_aggregate_adam(const float* S, int c, const float* const* stale, int n_stale,
                          float* p, float* m, float* v, long P, const long* tensor_sizes,
                          int n_tensors, long step, double lr, double beta1, double beta2,
                          double eps, flsim_stream_t stream);
-
-/* Independent-entry semantics (every weight_ups entry a distinct per-worker
- * gradient, the stale one the slow worker's own gradient from step t - d): S = the sum of the k
- * entries (the fast workers' gradients plus the popped stale gradients, already combined across
- * ranks by the one all-reduce), then mean = S / k (fp32) and the same Adam step. */
 int flsim_aggregate_adam_sum(const float* S, int k, float* p, float* m, float* v, long P,
                              const long* tensor_sizes, int n_tensors, long step, double lr,
                              double beta1, double beta2, double eps, flsim_stream_t stream);
 
-/* General entry order (the heterogeneous-delay extension of main.py:150-166, SURVEY 8 a1: every
- * worker with a delay is a slow worker with its own FIFO; weight_ups is appended in worker-index
- * order, so popped entries sit among the S_t copies).  k entries; events = device int32
- * [n_events][2] (position in weight_ups, index into `arrays`), sorted by position; every other
- * position is S.  arrays = device table of n_arrays stale arrays (nullptr entry = zeros). */
-int flsim_aggregate_adam_seq(const float* S, int k, const int32_t* events, int n_events,
-                             const float* const* arrays, int n_arrays, float* p, float* m,
-                             float* v, long P,
-                             const long* tensor_sizes, int n_tensors, long step, double lr,
-                             double beta1, double beta2, double eps, flsim_stream_t stream);
+/* Fused end of an epoch at world = 1: S_t = sum of the gradstate's slabs (what
+ * flsim_<net>_end_epoch computes), written to S_out if non-NULL (the slow worker's FIFO entry at a
+ * tick, main.py:156,161), then rule() + Adam -- one launch, S_t never round-trips through HBM. */
+int flsim_pn1_server_step(void* gradstate, float* S_out, const flsim_rule* rule, float* p,
+                          float* m, float* v, long step, double lr, double beta1, double beta2,
+                          double eps, flsim_stream_t stream);
+int flsim_vgg11_server_step(void* gradstate, float* S_out, const flsim_rule* rule, float* p,
+                            float* m, float* v, long step, double lr, double beta1, double beta2,
+                            double eps, flsim_stream_t stream);
+int flsim_vgg11_bn_server_step(void* gradstate, float* S_out, const flsim_rule* rule, float* p,
+                               float* m, float* v, long step, double lr, double beta1,
+                               double beta2, double eps, flsim_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Measurement (no reference counterpart): HIP events around every worker-batched GEMM launch on

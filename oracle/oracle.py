@@ -197,3 +197,24 @@ def adam_step(p, m, v, g, step, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8):
     for a in (p, m, v, g):
         assert a.dtype == np.float32 and a.flags.c_contiguous
     lib().oracle_adam_step(_p(p), _p(m), _p(v), _p(g), p.size, step, lr, beta1, beta2, eps)
+
+
+# ---------------------------------------------------------------------------------------------
+# Trajectory drift measure (test infrastructure): a Johnson-Lindenstrauss sketch of a flat
+# parameter vector.  ||sketch(a) - sketch(b)|| / sqrt(rows) estimates ||a - b|| (within ~20 % at
+# 64 rows) without storing a or b; the Gaussian rows come from torch's CPU generator (the same
+# numbers on every machine).
+# ---------------------------------------------------------------------------------------------
+def theta_sketch(theta, rows=64, seed=1234):
+    import torch
+    th = torch.as_tensor(np.asarray(theta, np.float32)).to(torch.float64)
+    out = np.empty(rows, np.float64)
+    g = torch.Generator()
+    for r in range(rows):
+        g.manual_seed(seed + r)
+        out[r] = float(torch.dot(torch.randn(th.numel(), generator=g).to(torch.float64), th))
+    return out
+
+
+def sketch_distance(sa, sb):
+    return float(np.linalg.norm(np.asarray(sa) - np.asarray(sb)) / np.sqrt(len(sa)))

@@ -38,24 +38,21 @@ class StandInEngine:
     def end_epoch(self, S):
         S.copy_(self.acc.float())
 
-    def aggregate_adam(self, S, c, stale, theta, m, v, step, lr=1e-3, betas=(0.9, 0.999),
-                       eps=1e-8):
-        tot = S * c
-        for s in stale:
-            if s is not None:
-                tot = tot + s[:P]
-        theta -= lr * tot / (c + len(stale))
-
     def aggregate_adam_sum(self, S, k, theta, m, v, step, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
         theta -= lr * S / k
 
-    def aggregate_adam_seq(self, S, k, events, arrays, theta, m, v, step, lr=1e-3,
-                           betas=(0.9, 0.999), eps=1e-8):
-        tot = S * (k - len(events))
-        for (_, j) in events:
-            if arrays[j] is not None:
-                tot = tot + arrays[j][:P]
-        theta -= lr * tot / k
+    def aggregate_rule(self, S, rule, theta, m, v, step, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
+        """rule.arrays in order after c copies of S (reference order) or at the event
+        positions (general order); a plain weighted mean, enough to check the sharding."""
+        if rule.events is None:
+            n_s, extra = rule.c, rule.arrays
+        else:
+            n_s, extra = rule.k - len(rule.events), [rule.arrays[j] for (_, j) in rule.events]
+        tot = S * n_s
+        for a in extra:
+            if a is not None:
+                tot = tot + a[:P]
+        theta -= lr * tot / rule.k
 
 
 def _run(rank, world, n, d, thr, epochs, out, port, delays=None, semantics="reference"):

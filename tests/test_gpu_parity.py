@@ -445,12 +445,13 @@ def test_simulation_evaluate_and_checkpoint_resume(pool, tmp_path):
     (700, 40, [1000, 31, 4099]),               # pure level-1 groups between mixed blocks
     (5000, 3, [2048, 7]),                      # pure level-2 groups (k > 4096)
     (12, 12, [40, 10]),                        # every entry a stale one
+    (16383, 50, [5000, 4099, 31, 70000]),      # configs[3]'s size: 16k entries, ~50 events
 ])
 def test_aggregate_adam_general_order_bit_exact(k, nev, sizes):
     """Heterogeneous-delay extension: stale entries interleaved with the S_t copies in worker
     order, several entries sharing one stale array, a zero (torch-1.x) entry; bit-exact vs the
     oracle's cascade over the explicit entry list."""
-    from flsim.engine import aggregate_adam_seq
+    from flsim.engine import ProgramStager, Rule, aggregate_rule
     from oracle import oracle as O
     P = sum(sizes)
     rs = np.random.RandomState(k + nev)
@@ -464,7 +465,9 @@ def test_aggregate_adam_general_order_bit_exact(k, nev, sizes):
     dS = torch.from_numpy(S).to(DEV)
     darr = [torch.from_numpy(a).to(DEV) for a in arrays] + [None]
     dp, dm, dv = (torch.from_numpy(a.copy()).to(DEV) for a in (p, m, v))
-    aggregate_adam_seq(dS, k, list(zip(pos.tolist(), which.tolist())), darr, dp, dm, dv, 4, sizes)
+    rule = Rule(k, darr, events=list(zip(pos.tolist(), which.tolist())),
+                stager=ProgramStager(DEV))
+    aggregate_rule(dS, rule, dp, dm, dv, 4, sizes)
     torch.cuda.synchronize()
     zero = np.zeros(P, np.float32)
     ents = [S] * k
@@ -483,7 +486,7 @@ def test_aggregate_adam_general_order_bit_exact(k, nev, sizes):
 
 def test_general_order_kernel_equals_reference_kernel():
     """On the reference order ([S_t] * c, stale last) both aggregation kernels agree bit for bit."""
-    from flsim.engine import PN1Engine, PN1_SIZES, aggregate_adam_seq
+    from flsim.engine import PN1Engine, PN1_SIZES, ProgramStager, Rule, aggregate_rule
     eng = PN1Engine(DEV, chunk_workers=1)
     P = eng.P
     g = torch.Generator(device="cpu").manual_seed(5)
@@ -494,7 +497,8 @@ def test_general_order_kernel_equals_reference_kernel():
     a = [t.clone() for t in base]
     b = [t.clone() for t in base]
     eng.aggregate_adam(S, 511, [st], *a, 1)
-    aggregate_adam_seq(S, 512, [(511, 0)], [st], *b, 1, PN1_SIZES)
+    aggregate_rule(S, Rule(512, [st], events=[(511, 0)], stager=ProgramStager(DEV)), *b, 1,
+                   PN1_SIZES)
     for x, y in zip(a, b):
         assert torch.equal(x, y)
 
@@ -528,8 +532,10 @@ def test_max_chunk_matches_small_chunks(pool):
     from flsim.engine import PN1_SHAPES
     from flsim.sim import FLSimulation
     n = 129                                   # epoch 1: the 128 fast workers, no tick
-    a = FLSimulation(n, delay=50, throttle=False, device=DEV, chunk_workers=32, pool=pool)
-    b = FLSimulation(n, delay=50, throttle=False, device=DEV, chunk_workers=128, pool=pool)
+    a = FLSimulation(n, delay=50, throttle=False, device=DEV, chunk_workers=32, pool=pool,
+                     keep_S=True)
+    b = FLSimulation(n, delay=50, throttle=False, device=DEV, chunk_workers=128, pool=pool,
+                     keep_S=True)
     a.epoch()
     b.epoch()
     for x, y in ((b.theta, a.theta), (b.m, a.m), (b.v, a.v)):

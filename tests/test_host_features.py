@@ -102,3 +102,42 @@ def test_model_file_warm_start_loads_state_dict(tmp_path, model):
     torch.save(sd, path)
     with pytest.raises(RuntimeError):
         load_model_file(path, model)
+
+
+def test_restore_rejects_other_hyperparameters():
+    """lr, betas, eps and max_throttle are part of the checkpoint's config."""
+    from flsim.sim import FLSimulation
+    a = _sim(11, 3, True)
+    a.epoch()
+    ck = a.checkpoint()
+    for kw in (dict(lr=2e-3), dict(betas=(0.8, 0.999)), dict(eps=1e-7), dict(max_throttle=8)):
+        b = FLSimulation(11, delay=3, throttle=True, device="cpu", engine=StandInEngine(),
+                         device_pool=object(), theta0=torch.zeros(P), **kw)
+        with pytest.raises(ValueError):
+            b.restore(ck)
+
+
+def test_delay_zero_is_the_reference_slow_worker():
+    """--delay 0 (main.py:150-158): worker n-1 is still the slow one -- it computes and pushes
+    at t = 0 without an entry or a logged loss -- and t = 1 raises ZeroDivisionError (t % 0)."""
+    from flsim.schedule import Schedule, reference_delays
+    n = 5
+    s = Schedule(n, reference_delays(n, 0), False)
+    p = s.next_epoch()
+    assert p.computes.tolist() == [1] * n
+    assert p.fast.tolist() == [1] * (n - 1) + [0]
+    assert p.c_t == n - 1 and p.s_t == 0 and p.pushed
+    with pytest.raises(ZeroDivisionError):
+        s.next_epoch()
+    sim = _sim(n, 0, False)
+    sim.epoch()
+    with pytest.raises(ZeroDivisionError):
+        sim.epoch()
+
+
+def test_fl_util_drop_in_names():
+    """main.py:19 `from FL.util import *` resolves to the package with the reference's names."""
+    ns = {}
+    exec("from FL.util import *", ns)
+    for name in ("save_data", "plot_data", "imshow", "print_test_accuracy", "check_mem"):
+        assert callable(ns[name]), name

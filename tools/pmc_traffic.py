@@ -21,8 +21,14 @@ DGRAD = {(36, 36, 48): 2, (20, 20, 96): 3, (22, 22, 96): 4, (13, 13, 192): 5, (1
 
 
 def probe_name(kname):
-    if "k_aggregate_adam" in kname:
-        return "aggregate_adam"
+    m = re.search(r"k_slab_step<(true|false), (true|false)>", kname)
+    if m:
+        if m.group(1) == "false":
+            return "slab_sum"
+        return "slab_step" if m.group(2) == "true" else "slab_step_seq"
+    m = re.search(r"k_agg_stream<(true|false)>", kname)
+    if m:
+        return "aggregate_adam" if m.group(1) == "true" else "aggregate_adam_seq"
     m = re.search(r"Im2colKM<(\d+), (\d+), (\d+),", kname)
     if m:
         return f"conv{FWD[tuple(map(int, m.groups()))]}_wgrad"
