@@ -197,6 +197,7 @@ struct StepArgs {
     float* m;
     float* v;
     int nseg, units;
+    int u_lo;                       // first unit of this launch (block b runs unit u_lo + b)
     AdamConst ac;
     RuleProg R;
     SlabSeg seg[STEP_MAX_SEG];
@@ -220,6 +221,15 @@ __device__ __forceinline__ float reduce_cols(const float* slab, const SlabSeg& g
         if (col < g.n) {
             const float* pz = slab + col;
             int z = z0 + tz;
+            for (; z + 28 < z1; z += 32) {        // eight rows in flight per thread
+                f32x4 x[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    x[u] = __builtin_nontemporal_load(
+                        reinterpret_cast<const f32x4*>(pz + (long)(z + 4 * u) * g.n));
+#pragma unroll
+                for (int u = 0; u < 8; ++u) acc[u & 3] += x[u];
+            }
             for (; z + 12 < z1; z += 16) {
                 f32x4 x[4];
 #pragma unroll
@@ -287,6 +297,130 @@ __device__ __forceinline__ bool col_to_param(const SlabSeg& g, long col, long& t
     return valid;
 }
 
+// Identity-layout segments (the linear layers): tiles of 1024 elements, thread t owns the float4
+// column 4t; it sums its Z slab rows itself (small Z, four accumulators) and finishes with 16-B
+// parameter-side loads and stores; the parameter loads are issued before the slab reads.
+template <bool ADAM, bool INL>
+__device__ __forceinline__ void slab_step_wide(const StepArgs& A, const SlabSeg& g, int u, int ul,
+                                               float* lds) {
+    constexpr int NYW = 2;          // entry arrays held in registers (the rest load on demand)
+    const int tid = threadIdx.x;
+    const float* slab = A.base + g.slab_off;
+    const ProgRef<INL> prog{A.R};
+    int tile, t_end, j;
+    if (g.nz == 1) {
+        tile = ul * g.tpu;
+        t_end = tile + g.tpu < g.tiles ? tile + g.tpu : g.tiles;
+        j = 0;
+    } else {
+        tile = ul / g.nz;
+        j = ul - tile * g.nz;
+        t_end = tile + 1;
+    }
+    const int z0 = j * g.zc;
+    const int z1 = z0 + g.zc < g.Z ? z0 + g.zc : g.Z;
+    auto ld = [](const float* ptr) -> f32x4 {
+        return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(ptr));
+    };
+    for (; tile < t_end; ++tile) {
+        const long c = (long)tile * 1024 + 4 * tid;
+        const bool valid = c < g.n;
+        const long e = g.toff + c;
+        f32x4 p, m, v, ys[NYW];
+        auto load_param_side = [&]() {
+#pragma unroll
+            for (int q = 0; q < NYW; ++q)
+                ys[q] = (q < A.R.narr && A.R.arr[q]) ? ld(A.R.arr[q] + e) : f32x4{0.f, 0.f, 0.f, 0.f};
+            p = ld(A.p + e);
+            m = ld(A.m + e);
+            v = ld(A.v + e);
+        };
+        if (ADAM && valid && g.nz == 1) load_param_side();
+        f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
+        if (valid) {
+            const float* pz = slab + c;
+            int z = z0;
+            for (; z + 7 < z1; z += 8) {               // eight rows in flight
+                f32x4 x[8];
+#pragma unroll
+                for (int r = 0; r < 8; ++r) x[r] = ld(pz + (long)(z + r) * g.n);
+                a0 += x[0];
+                a1 += x[1];
+                a2 += x[2];
+                a3 += x[3];
+                a0 += x[4];
+                a1 += x[5];
+                a2 += x[6];
+                a3 += x[7];
+            }
+            for (; z + 3 < z1; z += 4) {
+                const f32x4 x0 = ld(pz + (long)z * g.n), x1 = ld(pz + (long)(z + 1) * g.n);
+                const f32x4 x2 = ld(pz + (long)(z + 2) * g.n), x3 = ld(pz + (long)(z + 3) * g.n);
+                a0 += x0;
+                a1 += x1;
+                a2 += x2;
+                a3 += x3;
+            }
+            if (z < z1) a0 += ld(pz + (long)z * g.n);
+            if (z + 1 < z1) a1 += ld(pz + (long)(z + 1) * g.n);
+            if (z + 2 < z1) a2 += ld(pz + (long)(z + 2) * g.n);
+        }
+        a0 += a1;
+        a0 += a2;
+        a0 += a3;
+        if (g.nz > 1) {
+            // the conv path's hand-off with 1024 floats per unit (sc1 stores / loads)
+            float* part = A.base + A.part_off;
+            float* mine = part + (long)u * 1024 + 4 * tid;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                __hip_atomic_store(mine + k, a0[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            int* cnt = reinterpret_cast<int*>(A.base + A.cnt_off) + g.tile0 + tile;
+            if (tid == 0) {
+                const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+                lds[L_FLAG] = __int_as_float(old);
+            }
+            __syncthreads();
+            if (__float_as_int(lds[L_FLAG]) != g.nz - 1) return;
+            if (ADAM && valid) load_param_side();
+            float* pt = part + (long)(g.unit0 + tile * g.nz) * 1024 + 4 * tid;
+            for (int jj = 0; jj < g.nz; ++jj) {
+                f32x4 x;
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    x[k] = __hip_atomic_load(pt + (long)jj * 1024 + k, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+                if (jj == 0) a0 = x;
+                else a0 += x;
+            }
+            if (tid == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (!valid) continue;
+        if (A.S_out) *reinterpret_cast<f32x4*>(A.S_out + e) = a0;
+        if constexpr (ADAM) {
+            auto yf = [&](int q) -> f32x4 {
+                if (q < NYW) return ys[q];
+                return A.R.arr[q] ? ld(A.R.arr[q] + e) : f32x4{0.f, 0.f, 0.f, 0.f};
+            };
+            const f32x4 sum = casc_run(prog, 0, casc_values(a0, A.R.info.need, A.R.info.lp), yf);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float pp = p[k], mm = m[k], vv = v[k];
+                adam_elem(A.ac, sum[k], pp, mm, vv);
+                p[k] = pp;
+                m[k] = mm;
+                v[k] = vv;
+            }
+            __builtin_nontemporal_store(p, reinterpret_cast<f32x4*>(A.p + e));
+            __builtin_nontemporal_store(m, reinterpret_cast<f32x4*>(A.m + e));
+            __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(A.v + e));
+        }
+    }
+}
+
 // Units are dispatched round-robin (block b -> unit b): consecutive units, hence every segment's
 // mix of cheap and heavy units, are spread over all XCDs.  The partial hand-off uses sc1 stores /
 // loads, whose cost does not depend on which XCD the last arriver sits on.  Each thread's
@@ -296,12 +430,24 @@ template <bool ADAM, bool INL>
 __global__ void __launch_bounds__(256) k_slab_step(StepArgs A) {
     __shared__ float lds[L_Y + NYR * 256];
     const int tid = threadIdx.x;
-    const int u = (int)blockIdx.x;
+    // runs of XG consecutive units (a tile's z-units, neighbouring tiles: one parameter region)
+    // share an XCD (blocks b and b + 8 do), the runs themselves go round-robin over the XCDs so
+    // every XCD gets the same mix of segments
+    constexpr int XG = 8;
+    const int nb = (int)gridDim.x;
+    const int b = (int)blockIdx.x;
+    const int nfull = nb / (8 * XG) * (8 * XG);
+    const int lb = b < nfull ? ((b >> 3) / XG * 8 + (b & 7)) * XG + (b >> 3) % XG : b;
+    const int u = A.u_lo + lb;
     if (u >= A.units) return;
     int si = 0;
     while (si + 1 < A.nseg && A.seg[si + 1].unit0 <= u) ++si;
     const SlabSeg& g = A.seg[si];
     const int ul = u - g.unit0;
+    if (g.wide) {
+        slab_step_wide<ADAM, INL>(A, g, u, ul, lds);
+        return;
+    }
     int tile, t_end, j;
     if (g.nz == 1) {
         tile = ul * g.tpu;
@@ -337,7 +483,7 @@ __global__ void __launch_bounds__(256) k_slab_step(StepArgs A) {
             // hand the partial to the tile's last-arriving unit: sc1 stores, every wave's vmcnt
             // drained, one agent-scope ticket; the last arriver reads all partials with sc1 loads
             float* part = A.base + A.part_off;
-            __hip_atomic_store(part + (long)u * 256 + tid, s, __ATOMIC_RELAXED,
+            __hip_atomic_store(part + (long)u * 1024 + tid, s, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
@@ -351,14 +497,14 @@ __global__ void __launch_bounds__(256) k_slab_step(StepArgs A) {
             if (__float_as_int(lds[L_FLAG]) != g.nz - 1) return;
             if (ADAM && valid) load_param_side();
             // the nz partials in z order, eight loads in flight
-            float* pt = part + (long)(g.unit0 + tile * g.nz) * 256 + tid;
+            float* pt = part + (long)(g.unit0 + tile * g.nz) * 1024 + tid;
             s = 0.f;
             bool first = true;
             for (int j0 = 0; j0 < g.nz; j0 += 8) {
                 float pv[8];
 #pragma unroll
                 for (int jj = 0; jj < 8; ++jj)
-                    pv[jj] = j0 + jj < g.nz ? __hip_atomic_load(pt + (long)(j0 + jj) * 256,
+                    pv[jj] = j0 + jj < g.nz ? __hip_atomic_load(pt + (long)(j0 + jj) * 1024,
                                                                 __ATOMIC_RELAXED,
                                                                 __HIP_MEMORY_SCOPE_AGENT)
                                             : 0.f;
@@ -478,7 +624,18 @@ int slab_step_launch(float* gradstate, const StepPlan& plan, long cnt_off, long 
         A.R = *rule;
         A.ac = *ac;
     }
-    const unsigned nblk = (unsigned)plan.units;
+    // FLSIM_STEP_UNITS="lo,hi" (measurement only): run units [lo, hi) of the plan -- whole
+    // segments, so every split tile completes and resets its counter
+    A.u_lo = 0;
+    int u_hi = plan.units;
+    if (const char* env = getenv("FLSIM_STEP_UNITS")) {
+        int lo = 0, hi = 0;
+        if (sscanf(env, "%d,%d", &lo, &hi) == 2 && 0 <= lo && lo < hi && hi <= plan.units) {
+            A.u_lo = lo;
+            u_hi = hi;
+        }
+    }
+    const unsigned nblk = (unsigned)(u_hi - A.u_lo);
     // algorithmic HBM bytes: every slab byte once; S_out written; p, m, v read + written; each
     // distinct entry array read once
     double bytes = 4.0 * (double)plan.slab_floats + (S_out ? 4.0 * P : 0.0);

@@ -41,6 +41,7 @@ struct SlabSeg {
     long slab_off;
     int Z, n, zc, nz, tiles, tpu, unit0, tile0, toff, numel;
     uint16_t CO, CI, CIP, KP;
+    uint16_t wide;   // identity layout, 16-B aligned, no row_sum tail: 1024-element float4 tiles
 };
 
 struct StepPlan {
@@ -49,8 +50,23 @@ struct StepPlan {
     long slab_floats;     // sum of Z * n (the slab bytes the step streams / 4)
 };
 
-inline int plan_step(const SegSpec* s, int nseg, StepPlan* P) {
+// wide (float4) tiles: identity layout, 16-B aligned, no row_sum tail, a real weight matrix
+inline bool seg_wide(const SegSpec& s) {
+    return s.CO == 0 && s.n % 4 == 0 && s.toff % 4 == 0 && s.numel % 32 == 0 && s.n >= 4096;
+}
+
+// Dispatch order of the units: small tensors first (biases, the head, conv1: few units, each a
+// long serial z-reduction), then the wide segments (the linear layers: many short units), then
+// the packed conv segments (uniform 256 KB streaming units), so the launch ends on uniform work.
+inline int seg_class(const SegSpec& s) { return s.n < 4096 ? 0 : (seg_wide(s) ? 1 : 2); }
+
+inline int plan_step(const SegSpec* s_in, int nseg, StepPlan* P) {
     if (nseg > STEP_MAX_SEG) return 1;
+    SegSpec s[STEP_MAX_SEG];
+    int k = 0;
+    for (int pass = 0; pass < 3; ++pass)
+        for (int i = 0; i < nseg; ++i)
+            if (seg_class(s_in[i]) == pass) s[k++] = s_in[i];
     P->nseg = nseg;
     int u = 0, ct = 0;
     long sf = 0;
@@ -65,19 +81,22 @@ inline int plan_step(const SegSpec* s, int nseg, StepPlan* P) {
         g.CI = (uint16_t)s[i].CI;
         g.CIP = (uint16_t)s[i].CIP;
         g.KP = (uint16_t)s[i].KP;
-        g.tiles = (int)((s[i].n + 255) / 256);
-        const long tile_f = 256L * s[i].Z;
+        g.wide = seg_wide(s[i]);
+        g.tiles = (int)((s[i].n + (g.wide ? 1023 : 255)) / (g.wide ? 1024 : 256));
+        const long tile_f = (g.wide ? 1024L : 256L) * s[i].Z;
+        // wide tiles: 64 KB units (one tile of a few rows per block: many blocks in flight)
+        const long unit_f = g.wide ? STEP_UNIT_FLOATS / 4 : STEP_UNIT_FLOATS;
         int units;
-        if (tile_f <= STEP_UNIT_FLOATS) {
+        if (tile_f <= unit_f) {
             g.nz = 1;
             g.zc = g.Z;
-            long tpu = STEP_UNIT_FLOATS / tile_f;
-            if (tpu > 4) tpu = 4;     // short units: many blocks in flight, no long serial tails
+            long tpu = unit_f / tile_f;
+            if (tpu > (g.wide ? 1 : 4)) tpu = g.wide ? 1 : 4;   // short units, no serial tails
             g.tpu = (int)(tpu < g.tiles ? tpu : g.tiles);
             units = (g.tiles + g.tpu - 1) / g.tpu;
             g.tile0 = 0;
         } else {
-            int nz = (int)((tile_f + STEP_UNIT_FLOATS - 1) / STEP_UNIT_FLOATS);
+            int nz = (int)((tile_f + unit_f - 1) / unit_f);
             g.zc = (g.Z + nz - 1) / nz;
             g.zc = (g.zc + 3) / 4 * 4;
             g.nz = (g.Z + g.zc - 1) / g.zc;
@@ -113,7 +132,7 @@ struct RuleProg {
 
 // gradstate extras the fused step needs: tile counters (zeroed with the slabs) and partials
 inline long step_counter_floats(const StepPlan& P) { return (P.ctiles + 63) / 64 * 64; }
-inline long step_partial_floats(const StepPlan& P) { return (long)P.units * 256; }
+inline long step_partial_floats(const StepPlan& P) { return (long)P.units * 1024; }
 
 // launch: S_out (nullable) receives S_t in the flat layout; rule == nullptr: reduce only (the
 // network's end_epoch); else rule() + Adam on p, m, v

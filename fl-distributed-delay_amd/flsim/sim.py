@@ -270,41 +270,60 @@ class FLSimulation:
 
     def _epoch_independent(self, plan, ks, sync_loss):
         """Independent-entry semantics: every weight_ups entry is a distinct
-        per-worker gradient and a slow worker's FIFO holds its own gradient.  A slow worker's
-        gradient is computed and kept by its owner rank (worker index mod world); the fast
-        workers are sharded as usual.  Each rank adds the stale gradients it owns to its partial
-        sum, so the one all-reduce combines the partial sums of all k entries; mean = sum / k,
-        then the same Adam step, replicated."""
+        per-worker gradient and a slow worker's FIFO holds its own gradient.  Slow workers with
+        the same delay d tick together (t == 0 or t % d == 0) and pop together d epochs later, so
+        their FIFO entries are kept as ONE slot per delay class holding the class's summed
+        gradient: each class is one worker-batched launch, owned by rank d mod world.  The fast
+        workers are sharded as usual.  Each rank adds the popped class slots it owns to its
+        partial sum, so the one all-reduce combines the partial sums of all k entries; mean =
+        sum / k, then the same Adam step, replicated."""
+        from .schedule import DELAY_ZERO
         t = plan.t
         eng = self.engine
         active = np.nonzero(plan.computes)[0]
         slow_mask = self.delays[active] != 0
         fast, slow = active[~slow_mask], active[slow_mask]
-        own_slow = np.asarray([i for i in slow if int(i) % self.world == self.rank], np.int64)
+
+        def dclass(i):
+            d = int(self.delays[i])
+            return 0 if d == DELAY_ZERO else abs(d)
+        classes = {}
+        for i in slow:
+            classes.setdefault(dclass(i), []).append(int(i))
+        own = [(d, ws) for d, ws in sorted(classes.items()) if d % self.world == self.rank]
         lo, hi = self.shard(fast)
         S = self.comm[:self.P]
         losses = self.comm[self.Ppad:self.Ppad + len(fast)]
         if self.world > 1:
             losses.zero_()
-        wt = self._worker_table(t, np.concatenate([own_slow, fast[lo:hi]]), ks)
-        if not hasattr(self, "_slow_loss"):
-            self._slow_loss = torch.zeros(1, device=self.device)
-        ns = len(own_slow)
-        for j, i in enumerate(own_slow):           # the slow worker's own gradient (FIFO push)
+        own_workers = np.asarray([i for _, ws in own for i in ws], np.int64)
+        wt = self._worker_table(t, np.concatenate([own_workers, fast[lo:hi]]), ks)
+        cw = self.engine.chunk_workers
+        if getattr(self, "_slow_loss", None) is None or self._slow_loss.numel() < cw:
+            self._slow_loss = torch.zeros(cw, device=self.device)
+        off = 0
+        for d, ws in own:                        # one FIFO slot per delay class (its sum)
             eng.begin_epoch(self.theta)
-            eng.run_chunk(self.theta, self.pool, wt[j:j + 1], 1, self.n, self.seed, self.dropout,
-                          self._slow_loss)
+            n_ws = len(ws)
+            k = -(-n_ws // cw)
+            for j in range(k):
+                c0, c1 = (j * n_ws) // k, ((j + 1) * n_ws) // k
+                eng.run_chunk(self.theta, self.pool, wt[off + c0:off + c1], c1 - c0, self.n,
+                              self.seed, self.dropout, self._slow_loss[:c1 - c0])
             slot = self._slot()
             eng.end_epoch(slot[:self.P])
-            self.stale_store[(int(i), t)] = slot
+            self.stale_store[(d, t)] = slot
+            off += n_ws
+        ns = off
         eng.begin_epoch(self.theta)
         for c0, c1 in self.chunks(lo, hi):
             eng.run_chunk(self.theta, self.pool, wt[ns + c0 - lo:ns + c1 - lo], c1 - c0, self.n,
                           self.seed, self.dropout, losses[c0:c1])
         eng.end_epoch(S)
-        for (i, src) in plan.stale:                 # popped entries, added by their owner rank
-            if int(i) % self.world == self.rank:
-                slot = self.stale_store.pop((int(i), int(src)))
+        for (i, src) in plan.stale:              # popped entries, added once per class slot
+            key = (dclass(int(i)), int(src))
+            if key[0] % self.world == self.rank and key in self.stale_store:
+                slot = self.stale_store.pop(key)
                 S.add_(slot[:self.P])
                 self.free_slots.append(slot)
         if self.world > 1:

@@ -1,0 +1,141 @@
+"""Gradient parity with decision flips separated from arithmetic (test helper, GPU box).
+
+A worker-step gradient of PerformantNet1 depends on discrete forward decisions: ReLU signs
+(conv1/3/5, linear1/2), max-pool argmax and the pooled ReLU (conv2/4/6).  A pre-activation within
+rounding of zero, or a window whose two largest values are within rounding of each other, can go
+either way in ANY fp32 implementation, and one such flip moves the gradient of its sample -- up
+to ~5e-3 of the batch gradient for a linear2 unit (profiles/r02a/flip_census.txt).  So the check
+is in two parts:
+
+  arithmetic  ||g_gpu - g_tf|| <= TF_TOL ||g_tf||, g_tf = the fp64 oracle (models.py:27-47 +
+              CrossEntropyLoss) forced to take the GPU's own decisions, read back from the
+              engine's workspace;
+  decisions   the GPU's decisions that differ from the fp64 oracle's own are at most
+              FLIP_C * (the CPU fp32 port's own disagreements with fp64) + FLIP_FLOOR, out of
+              ~10^7 decisions per 128 samples -- a wrong mask or argmax rule would flip thousands.
+"""
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from oracle import model_ref as MR
+
+TF_TOL = 2e-6
+FLIP_C, FLIP_FLOOR = 3, 6
+GROUP = 1 << 20
+LAYERS = ("a1", "i1", "a3", "i2", "a5", "i3", "e1", "e2")
+
+
+def rel(a, b):
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
+
+
+def pool_idx(z):
+    """2x2 max-pool argmax, first maximum in row-major window order (torch's rule)."""
+    N, C, H, W = z.shape
+    PH, PW = H // 2, W // 2
+    w = z[:, :, :2 * PH, :2 * PW].reshape(N, C, PH, 2, PW, 2).permute(0, 1, 2, 4, 3, 5)
+    return torch.argmax(w.reshape(N, C, PH, PW, 4), -1)
+
+
+def gather(z, idx):
+    N, C, PH, PW = idx.shape
+    rows = 2 * torch.arange(PH).view(1, 1, PH, 1) + (idx >> 1)
+    cols = 2 * torch.arange(PW).view(1, 1, 1, PW) + (idx & 1)
+    return z[torch.arange(N).view(N, 1, 1, 1), torch.arange(C).view(1, C, 1, 1), rows, cols]
+
+
+def forward(P, x, y, noise, scale, forced=None):
+    """PerformantNet1 forward + scale * sum of per-sample CE, in P's dtype.  Decisions are the
+    masks AFTER dropout (what the GPU stores).  forced: the GPU's decisions, or None (own)."""
+    (w1, b1, w2, b2, w3, b3, w4, b4, w5, b5, w6, b6, l1w, l1b, l2w, l2b, l3w, l3b) = P
+    dec = {}
+    nz = (lambda i: None) if noise is None else (lambda i: noise[i])
+    mul = (lambda h, i: h) if noise is None else (lambda h, i: h * noise[i])
+
+    def relu(z, key, keep=None):
+        m = (z > 0) if forced is None else forced[key]
+        if forced is None and keep is not None:
+            m = m & (keep > 0)
+        dec[key] = m
+        return z * m.to(z.dtype)
+
+    def pool(z, key, keep):
+        idx = pool_idx(F.relu(z)) if forced is None else forced[key]
+        dec[key] = idx
+        p = gather(z, idx)
+        if forced is None:
+            m = (p > 0) if keep is None else (p > 0) & (keep > 0)
+        else:
+            m = forced[key + "m"]
+        dec[key + "m"] = m
+        return p * m.to(z.dtype)
+
+    h = relu(F.conv2d(x, w1, b1, padding=2), "a1")
+    h = mul(pool(F.conv2d(h, w2, b2, padding=2), "i1", nz(0)), 0)
+    h = relu(F.conv2d(h, w3, b3, padding=2), "a3")
+    h = mul(pool(F.conv2d(h, w4, b4, padding=2), "i2", nz(1)), 1)
+    h = relu(F.conv2d(h, w5, b5, padding=2), "a5")
+    h = mul(pool(F.conv2d(h, w6, b6, padding=2), "i3", nz(2)), 2).reshape(x.shape[0], -1)
+    h = mul(relu(F.linear(h, l1w, l1b), "e1", nz(3)), 3)
+    h = mul(relu(F.linear(h, l2w, l2b), "e2", nz(4)), 4)
+    return F.cross_entropy(F.linear(h, l3w, l3b), y, reduction="sum") * scale, dec
+
+
+def grad(theta, dtype, x, y, noise, scale, forced=None):
+    P = [torch.tensor(a, dtype=dtype, requires_grad=True)
+         for a in MR.split_flat(theta.astype(np.float64 if dtype == torch.float64 else np.float32))]
+    nz = None if noise is None else [t.to(dtype) for t in noise]
+    loss, dec = forward(P, x.to(dtype), y, nz, scale, forced)
+    loss.backward()
+    return torch.cat([p.grad.reshape(-1) for p in P]).double().numpy(), dec
+
+
+def gpu_decisions(eng, n):
+    """The GPU's forward decisions for the first n samples of the engine's last chunk, from its
+    workspace (NHWC -> NCHW)."""
+    NS = eng.max_samples
+    W = lambda i, shp, dt=torch.float32: eng.workspace_view(i, shp, dt).cpu()[:n]  # noqa: E731
+    nchw = lambda a: a.permute(0, 3, 1, 2).contiguous()                            # noqa: E731
+    d = dict(a1=nchw(W(1, (NS, 34, 34, 48))) > 0, a3=nchw(W(4, (NS, 20, 20, 96))) > 0,
+             a5=nchw(W(7, (NS, 13, 13, 192))) > 0, e1=W(10, (NS, 512)) > 0,
+             e2=W(11, (NS, 256)) > 0,
+             i1=nchw(W(19, (NS, 18, 18, 48), torch.uint8)).long(),
+             i2=nchw(W(20, (NS, 11, 11, 96), torch.uint8)).long(),
+             i3=nchw(W(21, (NS, 7, 7, 192), torch.uint8)).long(),
+             i1m=nchw(W(3, (NS, 18, 18, 48))) > 0, i2m=nchw(W(6, (NS, 11, 11, 96))) > 0,
+             i3m=W(9, (NS, 9408)).reshape(n, 192, 7, 7) > 0)
+    return d
+
+
+def flips(dec, ref):
+    out = {}
+    for k in ("a1", "a3", "a5", "e1", "e2"):
+        out[k] = int((dec[k] != ref[k]).sum())
+    for k in ("i1", "i2", "i3"):
+        live = ref[k + "m"] | dec[k + "m"]
+        out[k] = int(((dec[k] != ref[k]) & live).sum() + (dec[k + "m"] != ref[k + "m"]).sum())
+    return out
+
+
+def noise_groups(keys, n, dropout=True):
+    """Dropout noise of an n-sample batch whose 128-sample groups are keyed (t, worker) =
+    keys[b] (None when dropout is off)."""
+    if not dropout:
+        return None
+    per = [MR.dropout_noise(0, t, i, 128, torch.float64) for (t, i) in keys]
+    return [torch.cat([p[s] for p in per])[:n] for s in range(len(per[0]))]
+
+
+def check_worker_step(g_gpu, eng, theta, x, y, noise, scale):
+    """Both checks above for a GPU gradient g_gpu of the batch (x, y) the engine ran last."""
+    n = x.shape[0]
+    forced = gpu_decisions(eng, n)
+    g_tf, _ = grad(theta, torch.float64, x, y, noise, scale, forced)
+    g_64, d64 = grad(theta, torch.float64, x, y, noise, scale)
+    _, d32 = grad(theta, torch.float32, x, y, noise, scale)
+    fg, fc = flips(forced, d64), flips(d32, d64)
+    stats = dict(tf=rel(g_gpu, g_tf), vs64=rel(g_gpu, g_64), flips_gpu=fg, flips_cpu32=fc)
+    assert stats["tf"] <= TF_TOL, stats
+    assert sum(fg.values()) <= FLIP_C * sum(fc.values()) + FLIP_FLOOR, stats
+    return stats

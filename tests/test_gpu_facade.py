@@ -66,14 +66,13 @@ def _oracle_grad(theta, batches, dtype):
     return torch.cat([p.grad.reshape(-1) for p in params]).numpy().astype(np.float64), losses
 
 
-def _check_grad(g_gpu, g64):
-    from flsim.engine import PN1_SHAPES, PN1_SIZES
-    off = 0
-    for (name, _), n in zip(PN1_SHAPES, PN1_SIZES):
-        r = _rel_l2(g_gpu[off:off + n], g64[off:off + n])
-        assert r <= 5e-3, (name, r)
-        off += n
-    assert np.linalg.norm(g_gpu - g64) <= 2.5e-4 * np.linalg.norm(g64)
+def _check_facade_step(g_gpu, model, x, y, keys, theta, n):
+    """Arithmetic (teacher forced) and decision checks of one fwd_bkwd call (tests/_flips.py)."""
+    import _flips
+    from FL.agents import _context
+    eng = _context(model).engine
+    noise = _flips.noise_groups(keys, n)
+    return _flips.check_worker_step(g_gpu, eng, theta, x, y, noise, 1.0 / n)
 
 
 @pytest.mark.parametrize("n", [100, 256])
@@ -91,7 +90,8 @@ def test_worker_batch_sizes_match_oracle(pool, n):
     g64, l64 = _oracle_grad(theta, [(x, y, 0, 0)], torch.float64)
     g = torch.cat([t.reshape(-1) for t in grads]).cpu().numpy().astype(np.float64)
     assert abs(float(loss) - l64[0]) <= 1e-4, (float(loss), l64[0])
-    _check_grad(g, g64)
+    keys = [(0, 0 + b * GROUP) for b in range(-(-n // 128))]
+    _check_facade_step(g, model, x, y, keys, theta, n)
 
 
 def test_mixed_batch_sizes_in_one_epoch(pool):
@@ -102,14 +102,19 @@ def test_mixed_batch_sizes_in_one_epoch(pool):
     model, central = _fresh_central()
     ws = [Worker(nn.CrossEntropyLoss()) for _ in range(2)]
     model.train()
+    theta = MR.init_params(0)
     xa, ya = _batch(pool, 128, 1)
     xb, yb = _batch(pool, 256, 2)
-    for w, (x, y) in zip(ws, ((xa, ya), (xb, yb))):
-        w.model = model
-        grads, _ = w.fwd_bkwd(x.to(DEV), y.to(DEV))
-    g64, _ = _oracle_grad(MR.init_params(0), [(xa, ya, 0, 0), (xb, yb, 1, 0)], torch.float64)
-    g = torch.cat([t.reshape(-1) for t in grads]).cpu().numpy().astype(np.float64)
-    _check_grad(g, g64)
+    ws[0].model = model
+    grads, _ = ws[0].fwd_bkwd(xa.to(DEV), ya.to(DEV))
+    ga = torch.cat([t.reshape(-1) for t in grads]).cpu().numpy().astype(np.float64)
+    _check_facade_step(ga, model, xa, ya, [(0, 0)], theta, 128)
+    ws[1].model = model
+    grads, _ = ws[1].fwd_bkwd(xb.to(DEV), yb.to(DEV))
+    gab = torch.cat([t.reshape(-1) for t in grads]).cpu().numpy().astype(np.float64)
+    _check_facade_step(gab - ga, model, xb, yb, [(0, 1), (0, 1 + GROUP)], theta, 256)
+    g64, _ = _oracle_grad(theta, [(xa, ya, 0, 0), (xb, yb, 1, 0)], torch.float64)
+    assert _rel_l2(gab, g64) <= 1e-2
     assert all(p.grad.data_ptr() == t.data_ptr() for p, t in zip(model.parameters(), grads))
 
 
@@ -243,7 +248,11 @@ def test_cifar10_binary_pool_through_hip_path(pool, tmp_path):
     S = torch.zeros(eng.P, device=DEV)
     eng.end_epoch(S)
     np.testing.assert_allclose(loss.cpu().numpy(), l64, atol=1e-4)
-    _check_grad(S.cpu().numpy().astype(np.float64), g64.astype(np.float64))
+    import _flips
+    xs, ys = zip(*[osim.batch(*it, dtype=torch.float64) for it in items])
+    _flips.check_worker_step(S.cpu().numpy().astype(np.float64), eng, osim.theta,
+                             torch.cat(xs), torch.cat(ys),
+                             _flips.noise_groups([(0, 0), (0, 3)], 256), 1.0 / 128)
     sim = FLSimulation(4, delay=2, throttle=True, device=DEV, chunk_workers=2, pool=cpool,
                        test_pool=(te_x, te_y))
     o2 = MR.OracleSim(4, delay=2, throttle=True, pool=cpool)

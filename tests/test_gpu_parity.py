@@ -1,9 +1,12 @@
 """GPU parity: the HIP path (through the C-ABI) against the CPU oracle on the same seeded inputs.
 
-Tolerances (calibrated on the reference's own fp32-vs-fp64 spread):
+Tolerances:
   * aggregation + Adam kernel: bit-exact with the oracle (same correctly rounded sqrt);
-  * one worker-step gradient: per-tensor rel-L2 vs fp64 <= 5e-3 and
-    ||g_gpu - g64|| <= 2 ||g_cpu32 - g64|| + 1e-6 ||g64||;
+  * one worker-step gradient (tests/_flips.py): the arithmetic within 2e-6 (rel-L2) of an fp64
+    oracle that takes the GPU's own forward decisions, and the decisions (ReLU signs, pool
+    argmax) that differ from the fp64 oracle's own at most 3x the CPU fp32 port's count + 6 --
+    a single knife-edge flip moves the gradient by up to ~5e-3 (profiles/r02a/flip_census.txt),
+    so a flat tolerance against fp64 is either loose or flaky;
   * losses: |dloss| <= 1e-4 on the first step, <= 1e-3 over the first epochs;
   * staleness trace: bit-exact.
 """
@@ -125,23 +128,13 @@ def _rel_l2(a, b):
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
 
 
-def _grad_checks(g_gpu, g32, g64):
-    """Per tensor: rel-L2 vs fp64 <= 5e-3.  Whole gradient: rel-L2 <= 1e-4.  (Per tensor, the early conv layers differ from fp64 mostly through ReLU /
-    max-pool decision flips at near-zero activations, whose count depends on summation order;
-    test_gradient_teacher_forced_decisions checks every tensor to 2e-5 with the decisions fixed.)"""
-    off = 0
-    from flsim.engine import PN1_SHAPES
-    for (name, _), n in zip(PN1_SHAPES, _sizes()):
-        a, b64 = g_gpu[off:off + n], g64[off:off + n]
-        off += n
-        r = _rel_l2(a, b64)
-        assert r <= 5e-3, (name, r)
-    # whole gradient: within 2.5e-4 of |g|.  Measured on MI355X: 1e-5 .. 1.2e-4 (1.2e-4 for the
-    # 3-worker chunk); the CPU's own fp32 error is 4e-6 .. 3.4e-5.  The excess is discrete ReLU /
-    # argmax flips at near-zero pre-activations (a different summation order flips different
-    # ones); test_gradient_teacher_forced_decisions pins the arithmetic itself to 2e-5.
-    e_gpu = np.linalg.norm(g_gpu - g64)
-    assert e_gpu <= 2.5e-4 * np.linalg.norm(g64), (e_gpu, np.linalg.norm(g32 - g64))
+def _items_batch(sim, items, dropout=True):
+    """The chunk's inputs as one batch: x, y and the dropout noise of each worker-step's
+    128-sample group (key (t, i))."""
+    import _flips
+    xs, ys = zip(*[sim.batch(*it, dtype=torch.float64) for it in items])
+    x, y = torch.cat(xs), torch.cat(ys)
+    return x, y, _flips.noise_groups([(t, i) for (t, i, _) in items], x.shape[0], dropout)
 
 
 @pytest.mark.parametrize("dropout", [False, True])
@@ -150,9 +143,9 @@ def test_single_worker_step_gradient(pool, dropout):
     from flsim.data import DevicePool
     from flsim.engine import PN1Engine, worker_table
     from oracle import model_ref as MR
+    import _flips
     sim = MR.OracleSim(4, delay=2, pool=pool, dropout=dropout)
     items = [(0, 0, 0)]
-    g32, l32 = sim.grad_of(sim.theta, items)
     g64, l64 = sim.grad_of(sim.theta, items, dtype=T.float64)
     eng = PN1Engine(DEV, chunk_workers=1)
     dpool = DevicePool(DEV, 0, pool)
@@ -164,7 +157,9 @@ def test_single_worker_step_gradient(pool, dropout):
     eng.end_epoch(S)
     T.cuda.synchronize()
     assert abs(float(loss.item()) - l64[0]) <= 1e-4
-    _grad_checks(S.cpu().numpy().astype(np.float64), g32.astype(np.float64), g64)
+    x, y, noise = _items_batch(sim, items, dropout)
+    _flips.check_worker_step(S.cpu().numpy().astype(np.float64), eng, sim.theta, x, y, noise,
+                             1.0 / 128)
 
 
 def test_chunk_of_workers_sums_gradients(pool):
@@ -174,9 +169,9 @@ def test_chunk_of_workers_sums_gradients(pool):
     from flsim.data import DevicePool
     from flsim.engine import PN1Engine, worker_table
     from oracle import model_ref as MR
+    import _flips
     sim = MR.OracleSim(4, delay=2, pool=pool)
     items = [(2, 0, 1), (2, 1, 3), (2, 3, 0)]
-    g32, l32 = sim.grad_of(sim.theta, items)
     g64, l64 = sim.grad_of(sim.theta, items, dtype=T.float64)
     eng = PN1Engine(DEV, chunk_workers=2)
     dpool = DevicePool(DEV, 0, pool)
@@ -184,12 +179,20 @@ def test_chunk_of_workers_sums_gradients(pool):
     eng.begin_epoch(theta)
     loss = T.zeros(3, device=DEV)
     eng.run_chunk(theta, dpool, worker_table(items[:2], DEV), 2, 4, 0, True, loss[:2])
+    S1 = T.zeros(eng.P, device=DEV)
+    eng.end_epoch(S1)
+    x, y, noise = _items_batch(sim, items[:2])
+    _flips.check_worker_step(S1.cpu().numpy().astype(np.float64), eng, sim.theta, x, y, noise,
+                             1.0 / 128)
     eng.run_chunk(theta, dpool, worker_table(items[2:], DEV), 1, 4, 0, True, loss[2:])
     S = T.zeros(eng.P, device=DEV)
-    eng.end_epoch(S)
+    eng.end_epoch(S)                  # the slabs kept chunk 1: S = both chunks (agents.py:35)
     T.cuda.synchronize()
     np.testing.assert_allclose(loss.cpu().numpy(), l64, atol=1e-4)
-    _grad_checks(S.cpu().numpy().astype(np.float64), g32.astype(np.float64), g64)
+    x, y, noise = _items_batch(sim, items[2:])
+    d2 = S.cpu().numpy().astype(np.float64) - S1.cpu().numpy().astype(np.float64)
+    _flips.check_worker_step(d2, eng, sim.theta, x, y, noise, 1.0 / 128)
+    assert _rel_l2(S.cpu().numpy().astype(np.float64), g64) <= 1e-2
 
 
 @pytest.mark.parametrize("thr", [False, True])

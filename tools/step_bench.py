@@ -1,0 +1,100 @@
+"""Micro-benchmark of the fused server step (k_slab_step) on PerformantNet1's gradstate (GPU box):
+the whole plan and each segment alone (FLSIM_STEP_UNITS), reduce-only and with rule() + Adam.
+
+  python tools/step_bench.py
+Prints per segment: units, slab MB, time (us), algorithmic GB/s.
+"""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "fl-distributed-delay_amd")]
+import torch  # noqa: E402
+
+GEO = [(3, 4, 48, 48, 8192), (48, 48, 48, 432, 4096), (48, 48, 96, 432, 2048),
+       (96, 96, 96, 864, 1024), (96, 96, 192, 864, 512), (192, 192, 192, 1728, 256)]
+UNIT = 65536
+
+
+def plan():
+    """Mirror of slabstep.h plan_step for PerformantNet1's segments (pn1_net.hip)."""
+    segs = []
+    offs = [0, 1296, 1344, 22080, 22128, 63600, 63696, 146640, 146736, 312624, 312816, 644592,
+            644784, 5461680, 5462192, 5593264, 5593520, 5596080, 5596090]
+    j = 0
+    for CI, CIP, CO, KP, ZW in GEO:
+        segs.append((f"conv{j // 2 + 1}.w", ZW, CO * KP, False, CO * CI * 9))
+        segs.append((f"conv{j // 2 + 1}.b", ZW, CO, True, CO))
+        j += 2
+    for name, Z, n in (("linear1.w", 8, 512 * 9408), ("linear1.b", 8, 512),
+                       ("linear2.w", 64, 256 * 512), ("linear2.b", 64, 256),
+                       ("linear3.w", 32, 2560), ("linear3.b", 32, 10)):
+        segs.append((name, Z, n, True, n))
+    out, u = [], 0
+    segs = [(sg, o) for sg, o in zip(segs, offs)]
+    iswide = [sg[3] and sg[2] % 4 == 0 and o % 4 == 0 and sg[4] % 32 == 0 and sg[2] >= 4096
+              for sg, o in segs]
+    cls = [0 if sg[2] < 4096 else (1 if iswide[i] else 2) for i, (sg, _) in enumerate(segs)]
+    order = [i for c in range(3) for i in range(len(segs)) if cls[i] == c]
+    for i in order:
+        (name, Z, n, ident, numel), _ = segs[i]
+        wide = iswide[i]
+        tw = 1024 if wide else 256
+        tiles = -(-n // tw)
+        tf = tw * Z
+        uf = UNIT // 4 if wide else UNIT
+        if tf <= uf:
+            tpu = max(1, min(uf // tf, tiles, 1 if wide else 4))
+            units = -(-tiles // tpu)
+        else:
+            nz = -(-tf // uf)
+            zc = (-(-Z // nz) + 3) // 4 * 4
+            nz = -(-Z // zc)
+            units = tiles * nz
+        out.append((name, u, u + units, Z * n * 4, numel))
+        u += units
+    return out, u
+
+
+def main():
+    from flsim.engine import PN1Engine, Rule
+    dev = "cuda:0"
+    eng = PN1Engine(dev, chunk_workers=128)
+    P = eng.P
+    theta = torch.randn(P + 64, device=dev) * 0.05
+    m = torch.zeros_like(theta)
+    v = torch.zeros_like(theta)
+    stale = torch.randn(P + 64, device=dev) * 1e-3
+    eng.begin_epoch(theta)
+    S = torch.zeros(P + 64, device=dev)
+    segs, total = plan()
+    rule = Rule(513, [stale], c=512)
+
+    def timeit(fn, reps=20):
+        fn()
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(reps):
+            fn()
+        b.record()
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) / reps * 1e3
+
+    full_red = timeit(lambda: eng.end_epoch(S))
+    full_step = timeit(lambda: eng.server_step(None, rule, theta, m, v, 5))
+    slab = sum(s[3] for s in segs)
+    print(f"plan: {total} units, slabs {slab / 1e6:.1f} MB")
+    print(f"FULL reduce-only {full_red:8.1f} us  {(slab + 4 * P) / full_red / 1e3:7.1f} GB/s")
+    print(f"FULL step        {full_step:8.1f} us  {(slab + 4 * P * 7) / full_step / 1e3:7.1f} GB/s")
+    for name, u0, u1, sb, numel in segs:
+        os.environ["FLSIM_STEP_UNITS"] = f"{u0},{u1}"
+        t = timeit(lambda: eng.server_step(None, rule, theta, m, v, 5))
+        byts = sb + 4 * numel * 7
+        print(f"{name:10s} units {u1 - u0:5d}  slab {sb / 1e6:7.1f} MB  {t:8.1f} us  "
+              f"{byts / t / 1e3:7.1f} GB/s", flush=True)
+    os.environ.pop("FLSIM_STEP_UNITS")
+
+
+if __name__ == "__main__":
+    main()
