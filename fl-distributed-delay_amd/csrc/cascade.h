@@ -39,8 +39,13 @@ enum CascOp : int32_t {
     COP_LX = 10,   // r0 += x           (row_sum leftover rows)
     COP_LY = 11,   // r0 += y[n]
     COP_RS = 12,   // r0 = ((r0 + r1) + r2) + r3
+    // fused pairs (emitted by the builder's peephole; halve the ops of event blocks)
+    COP_XY = 13,   // a0 += x, n times; a0 += y[q]       (n = bits 4..15, q = bits 16..31)
+    COP_XC1 = 14,  // a0 += x, n times; a1 += a0, a0 = 0
+    COP_BXC2 = 15, // a1 += bx, n times; a2 += a1, a1 = 0
 };
 constexpr int COP_SHIFT = 4;
+constexpr int CASC_PAD = 8;             // words the interpreter may fetch past a COP_END
 constexpr int CASC_MAX_K = 1 << 19;     // lp == 4 for the whole sequence and its row_sum streams
 
 // program header (info[]) written by build_cascade_program
@@ -58,12 +63,29 @@ struct CascEmitter {
     int32_t* out;
     int cap, len = 0, need = 0;
     bool ok = true;
+    int stream_start = 0;     // no fusion across a program boundary
     void put(int op, int n = 0) {
-        if (len >= cap) { ok = false; return; }
-        out[len++] = (int32_t)(((uint32_t)n << COP_SHIFT) | (uint32_t)op);
         if (op == COP_BX) need |= 1;
         if (op == COP_G1) need |= 3;
         if (op == COP_G2) need |= 7;
+        if (len > stream_start) {         // peephole: fuse with the previous word
+            const uint32_t prev = (uint32_t)out[len - 1];
+            const int pop = (int)(prev & 15u), pn = (int)(prev >> COP_SHIFT);
+            if (op == COP_Y && pop == COP_X && pn < 4096 && n < 65536) {
+                out[len - 1] = (int32_t)((uint32_t)COP_XY | ((uint32_t)pn << 4) | ((uint32_t)n << 16));
+                return;
+            }
+            if (op == COP_C1 && pop == COP_X) {
+                out[len - 1] = (int32_t)(((uint32_t)pn << COP_SHIFT) | (uint32_t)COP_XC1);
+                return;
+            }
+            if (op == COP_C2 && pop == COP_BX) {
+                out[len - 1] = (int32_t)(((uint32_t)pn << COP_SHIFT) | (uint32_t)COP_BXC2);
+                return;
+            }
+        }
+        if (len >= cap) { ok = false; return; }
+        out[len++] = (int32_t)(((uint32_t)n << COP_SHIFT) | (uint32_t)op);
     }
 };
 
@@ -147,6 +169,7 @@ inline int build_cascade_program(int k, const int32_t* pos, const int32_t* arr, 
         delete[] rows;
     }
     const int tail_off = E.len;
+    E.stream_start = E.len;
     // row_sum program: 4 strided streams of k/4 rows, then the leftover rows into stream 0
     const int sz = k / 4;
     {
@@ -169,7 +192,8 @@ inline int build_cascade_program(int k, const int32_t* pos, const int32_t* arr, 
         delete[] rows;
         delete[] qs;
     }
-    if (!E.ok) return -2;
+    if (!E.ok || E.len + CASC_PAD - 1 > cap) return -2;
+    for (int j = E.len; j < cap && j < E.len + CASC_PAD; ++j) prog[j] = COP_END;   // fetch pad
     if (info) *info = CascInfo{E.len, tail_off, E.need, lp};
     return E.len;
 }
@@ -201,51 +225,103 @@ __host__ __device__ inline CascVals<T> casc_values(T x, int need, int lp) {
     return c;
 }
 
-template <class T, class PROG, class YF>
+// a += v, n times in sequence (8-way unrolled body + fall-through remainder: one loop overhead
+// per eight adds on the device)
+template <class T>
+__host__ __device__ inline void casc_add_n(T& a, const T& v, int n) {
+    for (; n >= 8; n -= 8) {
+        a += v;
+        a += v;
+        a += v;
+        a += v;
+        a += v;
+        a += v;
+        a += v;
+        a += v;
+    }
+    switch (n) {
+        case 7: a += v; [[fallthrough]];
+        case 6: a += v; [[fallthrough]];
+        case 5: a += v; [[fallthrough]];
+        case 4: a += v; [[fallthrough]];
+        case 3: a += v; [[fallthrough]];
+        case 2: a += v; [[fallthrough]];
+        case 1: a += v; [[fallthrough]];
+        default: break;
+    }
+}
+
+// FETCH words are read per step (the device passes CASC_PAD = 8: one wide scalar load per eight
+// ops); the program buffer then needs FETCH - 1 readable words past its last COP_END.
+
+// MAIN_ONLY: the caller runs main programs only (no row_sum part), so r1..r3 stay dead
+template <int FETCH = 1, bool MAIN_ONLY = false, class T, class PROG, class YF>
 __host__ __device__ inline T casc_run(const PROG& prog, int pc, const CascVals<T>& c, YF&& y) {
     T a0 = T(0.f), a1 = T(0.f), a2 = T(0.f), a3 = T(0.f);
     T r0 = T(0.f), r1 = T(0.f), r2 = T(0.f), r3 = T(0.f);
-    for (;; ++pc) {
-        const uint32_t w = (uint32_t)prog[pc];
-        const int op = (int)(w & 15u);
-        const int n = (int)(w >> COP_SHIFT);
-        switch (op) {
-            case COP_X:
-                for (int j = 0; j < n; ++j) a0 += c.x;
-                break;
-            case COP_Y: a0 += y(n); break;
-            case COP_C1: a1 += a0; a0 = T(0.f); break;
-            case COP_C2: a2 += a1; a1 = T(0.f); break;
-            case COP_C3: a3 += a2; a2 = T(0.f); break;
-            case COP_BX:
-                for (int j = 0; j < n; ++j) a1 += c.bx;
-                break;
-            case COP_G1:
-                for (int j = 0; j < n; ++j) a2 += c.g1;
-                break;
-            case COP_G2:
-                for (int j = 0; j < n; ++j) a3 += c.g2;
-                break;
-            case COP_FIN: {
+    for (;; pc += FETCH) {
+        int32_t wv[FETCH];
+#pragma unroll
+        for (int k = 0; k < FETCH; ++k) wv[k] = prog[pc + k];
+#pragma unroll
+        for (int k = 0; k < FETCH; ++k) {
+            const uint32_t w = (uint32_t)wv[k];
+            const int op = (int)(w & 15u);
+            const int n = (int)(w >> COP_SHIFT);
+            // most frequent first: the event-block ops, then the group structure
+            if (op == COP_XY) {
+                casc_add_n(a0, c.x, n & 4095);
+                a0 += y((int)(w >> 16));
+            } else if (op == COP_X) {
+                casc_add_n(a0, c.x, n);
+            } else if (op == COP_XC1) {
+                casc_add_n(a0, c.x, n);
+                a1 += a0;
+                a0 = T(0.f);
+            } else if (op == COP_Y) {
+                a0 += y(n);
+            } else if (op == COP_BX) {
+                casc_add_n(a1, c.bx, n);
+            } else if (op == COP_BXC2) {
+                casc_add_n(a1, c.bx, n);
+                a2 += a1;
+                a1 = T(0.f);
+            } else if (op == COP_C1) {
+                a1 += a0;
+                a0 = T(0.f);
+            } else if (op == COP_C2) {
+                a2 += a1;
+                a1 = T(0.f);
+            } else if (op == COP_G1) {
+                casc_add_n(a2, c.g1, n);
+            } else if (op == COP_C3) {
+                a3 += a2;
+                a2 = T(0.f);
+            } else if (op == COP_G2) {
+                casc_add_n(a3, c.g2, n);
+            } else if (op == COP_FIN) {
                 T r = a0;
                 r += a1;
                 r += a2;
                 r += a3;
                 a0 = a1 = a2 = a3 = T(0.f);
-                if (n == 0) r0 = r;
+                if (MAIN_ONLY || n == 0) r0 = r;
                 else if (n == 1) r1 = r;
                 else if (n == 2) r2 = r;
                 else r3 = r;
-                break;
+            } else if (op == COP_LX) {
+                r0 += c.x;
+            } else if (op == COP_LY) {
+                r0 += y(n);
+            } else if (op == COP_RS) {
+                if constexpr (!MAIN_ONLY) {
+                    r0 += r1;
+                    r0 += r2;
+                    r0 += r3;
+                }
+            } else {
+                return r0;      // COP_END
             }
-            case COP_LX: r0 += c.x; break;
-            case COP_LY: r0 += y(n); break;
-            case COP_RS:
-                r0 += r1;
-                r0 += r2;
-                r0 += r3;
-                break;
-            default: return r0;      // COP_END
         }
     }
 }

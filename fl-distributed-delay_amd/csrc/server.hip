@@ -75,16 +75,34 @@ __device__ __forceinline__ void adam_elem(const AdamConst& A, float s, float& p,
     v = vi;
 }
 
-// program access: inline words in the kernel arguments (kernarg loads) or a device buffer; the
-// program counter is uniform either way, so the loads are scalar
+// Program access.  The interpreter reads one word per op at a uniform address, so the words must
+// come through the scalar cache: the reference-order program rides in the kernel arguments; a
+// general-order program is copied (device to device, stream-ordered, right before the launch)
+// into this constant-address-space buffer.  A plain global buffer would be read with vector loads
+// (the compiler cannot prove the kernel does not write it) and every op would wait on one.
+constexpr int CASC_CONST_WORDS = 16384;
+__constant__ int32_t g_casc_prog[CASC_CONST_WORDS];
+
 template <bool INL>
 struct ProgRef {
     const RuleProg& R;
     __device__ __forceinline__ int32_t operator[](int i) const {
         if constexpr (INL) return R.iprog[i];
-        else return R.prog[i];
+        else return g_casc_prog[i];
     }
 };
+
+// stage a general-order program into g_casc_prog on `stream` (no-op for inline programs)
+static int stage_program(const RuleProg& R, hipStream_t stream) {
+    if (R.prog == nullptr) return 0;
+    FLSIM_REQUIRE(R.info.len + CASC_PAD <= CASC_CONST_WORDS, "rule program of %d words (max %d)",
+                  R.info.len, CASC_CONST_WORDS - CASC_PAD);
+    static void* dst = nullptr;
+    if (!dst) FLSIM_CHECK_HIP(hipGetSymbolAddress(&dst, HIP_SYMBOL(g_casc_prog)));
+    FLSIM_CHECK_HIP(hipMemcpyAsync(dst, R.prog, (size_t)(R.info.len + CASC_PAD) * 4,
+                                   hipMemcpyDeviceToDevice, stream));
+    return 0;
+}
 
 // ================================================================================================
 // k_agg_stream: S_t from a buffer
@@ -142,8 +160,8 @@ __global__ void __launch_bounds__(256) k_agg_stream(AggArgs A) {
         const CascVals<float> cv = casc_values(x, A.R.info.need, A.R.info.lp);
         const bool tail = in_tail(A, e);
         float s = 0.f;
-        if (!tail) s = casc_run(prog, 0, cv, yf);
-        if (tail) s = casc_run(prog, A.R.info.tail_off, cv, yf);
+        if (!tail) s = casc_run<INL ? 1 : CASC_PAD>(prog, 0, cv, yf);
+        if (tail) s = casc_run<INL ? 1 : CASC_PAD>(prog, A.R.info.tail_off, cv, yf);
         adam_elem(A.ac, s, p, m, v);
         A.p[e] = p;
         A.m[e] = m;
@@ -172,7 +190,8 @@ __global__ void __launch_bounds__(256) k_agg_stream(AggArgs A) {
         if (q < NYR) return ys_lds[q * 256 + tid];
         return A.R.arr[q] ? ld(A.R.arr[q] + e0) : f32x4{0.f, 0.f, 0.f, 0.f};
     };
-    const f32x4 sum = casc_run(prog, 0, casc_values(x, A.R.info.need, A.R.info.lp), yf);
+    const f32x4 sum = casc_run<INL ? 1 : CASC_PAD, true>(
+        prog, 0, casc_values(x, A.R.info.need, A.R.info.lp), yf);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         float pp = p[u], mm = m[u], vv = v[u];
@@ -405,7 +424,8 @@ __device__ __forceinline__ void slab_step_wide(const StepArgs& A, const SlabSeg&
                 if (q < NYW) return ys[q];
                 return A.R.arr[q] ? ld(A.R.arr[q] + e) : f32x4{0.f, 0.f, 0.f, 0.f};
             };
-            const f32x4 sum = casc_run(prog, 0, casc_values(a0, A.R.info.need, A.R.info.lp), yf);
+            const f32x4 sum = casc_run<INL ? 1 : CASC_PAD, true>(
+                prog, 0, casc_values(a0, A.R.info.need, A.R.info.lp), yf);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 float pp = p[k], mm = m[k], vv = v[k];
@@ -531,8 +551,8 @@ __global__ void __launch_bounds__(256) k_slab_step(StepArgs A) {
             const CascVals<float> cv = casc_values(s, A.R.info.need, A.R.info.lp);
             const bool tail = tl >= (long)(g.numel / 32) * 32;
             float sum = 0.f;
-            if (!tail) sum = casc_run(prog, 0, cv, yf);
-            if (tail) sum = casc_run(prog, A.R.info.tail_off, cv, yf);
+            if (!tail) sum = casc_run<INL ? 1 : CASC_PAD>(prog, 0, cv, yf);
+            if (tail) sum = casc_run<INL ? 1 : CASC_PAD>(prog, A.R.info.tail_off, cv, yf);
             adam_elem(A.ac, sum, p, m, v);
             A.p[e] = p;
             A.m[e] = m;
@@ -648,6 +668,7 @@ int slab_step_launch(float* gradstate, const StepPlan& plan, long cnt_off, long 
         hipExtLaunchKernelGGL(k_slab_step<true, true>, dim3(nblk), dim3(256), 0, stream, ps.start,
                               ps.stop, 0, A);
     } else {
+        RC(stage_program(*rule, stream));
         hipExtLaunchKernelGGL(k_slab_step<true, false>, dim3(nblk), dim3(256), 0, stream, ps.start,
                               ps.stop, 0, A);
     }
@@ -736,9 +757,11 @@ int flsim_aggregate_adam_rule(const float* S, const flsim_rule* rule, float* p, 
         if (A.R.prog == nullptr)
             hipExtLaunchKernelGGL(k_agg_stream<true>, dim3((unsigned)(nblk + A.nedge)), dim3(256),
                                   0, stream, ps.start, ps.stop, 0, A);
-        else
+        else {
+            RC(stage_program(A.R, stream));
             hipExtLaunchKernelGGL(k_agg_stream<false>, dim3((unsigned)(nblk + A.nedge)), dim3(256),
                                   0, stream, ps.start, ps.stop, 0, A);
+        }
         FLSIM_LAUNCH_CHECK();
         if (probe_end(ps, A.R.prog == nullptr ? K_AGG : K_AGG_SEQ, bytes)) return 2;
         lo = hi;
@@ -803,7 +826,7 @@ int flsim_cascade_eval_host(const int32_t* prog, const int32_t* info, const floa
         auto yf = [&](int q) -> float {
             return (q < n_arrays && ys[q]) ? ys[q][e] : 0.f;
         };
-        out[e] = casc_run(prog, (tail && tail[e]) ? info[1] : 0, cv, yf);
+        out[e] = casc_run<CASC_PAD>(prog, (tail && tail[e]) ? info[1] : 0, cv, yf);
     }
     return 0;
 }

@@ -312,14 +312,14 @@ def cascade_program(k, events):
     ev = np.asarray(events, np.int32).reshape(-1, 2)
     pos = np.ascontiguousarray(ev[:, 0])
     arr = np.ascontiguousarray(ev[:, 1])
-    cap = 64 + 40 * (len(ev) + 8)
+    cap = 72 + 40 * (len(ev) + 8)          # + the interpreter's fetch padding (CASC_PAD)
     prog = np.zeros(cap, np.int32)
     info = np.zeros(4, np.int32)
     vp = ctypes.c_void_p
     check(lib().flsim_cascade_program(int(k), pos.ctypes.data_as(vp), arr.ctypes.data_as(vp),
                                       len(ev), prog.ctypes.data_as(vp), cap,
                                       info.ctypes.data_as(vp)))
-    return prog[:info[0]].copy(), info
+    return prog[:info[0] + 8].copy(), info      # with the 8 padding words
 
 
 class Rule:

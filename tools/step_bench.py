@@ -68,7 +68,18 @@ def main():
     eng.begin_epoch(theta)
     S = torch.zeros(P + 64, device=dev)
     segs, total = plan()
-    rule = Rule(513, [stale], c=512)
+    mode = sys.argv[1] if len(sys.argv) > 1 else "ref"
+    if mode == "seq":          # a configs[3]-like general order: k = 8100, 72 events, 6 arrays
+        import numpy as np
+        from flsim.engine import ProgramStager
+        rs = np.random.RandomState(0)
+        arrs = [torch.randn(P + 64, device=dev) * 1e-3 for _ in range(6)]
+        pos = np.sort(rs.choice(8100, 72, replace=False))
+        ev = list(zip(pos.tolist(), rs.randint(0, 6, 72).tolist()))
+        rule = Rule(8100, arrs, events=ev, stager=ProgramStager(dev))
+        print("seq program words", int(rule.c_rule.info[0]))
+    else:
+        rule = Rule(513, [stale], c=512)
 
     def timeit(fn, reps=20):
         fn()
