@@ -11,7 +11,8 @@ __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 // ---------------------------------------------------------------------------------------------
 // A operand of a 3x3 / stride-1 convolution run as implicit GEMM (forward, or data-gradient as
 // a "valid" convolution of dZ with the flipped weights).  Rows = output pixels m = (n, oh, ow);
-// k = (kh*3 + kw) * CI + ci (CI >= 16 and a multiple of 16, or CI == 4 for the padded input).
+// k = (ci / 16) * 144 + (kh*3 + kw) * 16 + ci % 16 for CI a multiple of 16 (channel-slice-major),
+// k = (kh*3 + kw) * 4 + ci for CI == 4 (the padded input).
 // Input X is NHWC.  Output spatial OH = IH + 2*PAD - 2.
 // ---------------------------------------------------------------------------------------------
 // WIN = true: output rows in max-pool window order, m = ((n * PH + ph) * PW + pw) * 4 + 2 dy + dx
@@ -76,9 +77,13 @@ struct Im2colKC {
     }
     __device__ void load(int ks, f32x4 (&r)[UNITS]) const {
         if constexpr (TAP_UNIFORM) {
-            const int kk = ks * GK;                 // uniform
-            const int khkw = kk / CI;
-            const int ci0 = kk - khkw * CI;
+            // channel-slice-major K order: k-step ks = 9 * (ci0 / 16) + tap, so the nine taps of
+            // one 16-channel slice of the input window are read in nine consecutive k-steps and
+            // their re-reads hit L1/L2 (conv6 forward: 15.7 -> 3.3 GB fetched per launch,
+            // profiles/r02d/lab_order.txt).  The packed weights follow (k_pack_fwd/_dgrad).
+            const int cs = ks / 9;                  // uniform
+            const int khkw = ks - 9 * cs;
+            const int ci0 = cs * GK;
             const int kh = khkw / 3;
             const long off = (long)(kh * IW + (khkw - 3 * kh)) * CI + ci0;
 #pragma unroll

@@ -4,8 +4,8 @@
 //
 // Layout conventions (both nets): activations NHWC fp32, one 128-sample block per simulated
 // worker (main.py:43-44 batch_size); conv weights re-packed once per epoch into
-// Wf[co][(kh*3+kw)*CIP + ci] (forward) and Wd[ci][(kh'*3+kw')*CO + co] = W[co][ci][2-kh'][2-kw']
-// (data gradient).
+// Wf[co][k(khkw, ci)] (forward) and Wd[ci][k(khkw', co)] = W[co][ci][2-kh'][2-kw'] (data
+// gradient), k in Im2colKC's channel-slice-major order (k_pack_fwd).
 #pragma once
 #include "loaders.h"
 #include "pn1.h"
@@ -387,21 +387,32 @@ static int head_wgrad(const float* dlog, const float* e, float* slab, float* sla
 // =============================================================================================
 // per-epoch weight packing (theta in torch layout -> kernel layouts)
 // =============================================================================================
-// forward: Wf[co][khkw*CIP + ci] = W[co][ci][kh][kw]   (ci < CI; zero padding ci in [CI, CIP)
-// and k >= 9*CIP up to KP)
+// forward: Wf[co][k] = W[co][ci][kh][kw] in Im2colKC's K order (loaders.h):
+//   CIP % 16 == 0: k = (ci/16)*144 + khkw*16 + ci%16   (channel-slice-major)
+//   otherwise:     k = khkw*CIP + ci  (ci < CI; zero padding ci in [CI, CIP) and k >= 9*CIP up
+//                  to KP)
 static __global__ void k_pack_fwd(const float* __restrict__ W, float* __restrict__ Wf, int CO,
                                   int CI, int CIP, int KP) {
     const int e = blockIdx.x * 256 + threadIdx.x;
     if (e >= CO * KP) return;
     const int co = e / KP;
     const int k = e - co * KP;
-    const int khkw = k / CIP;
-    const int ci = k - khkw * CIP;
+    int khkw, ci;
+    if (CIP % 16 == 0) {
+        const int cs = k / 144, r = k - 144 * cs;
+        khkw = r >> 4;
+        ci = 16 * cs + (r & 15);
+    } else {
+        khkw = k / CIP;
+        ci = k - khkw * CIP;
+    }
     float v = 0.f;
     if (khkw < 9 && ci < CI) v = W[(co * CI + ci) * 9 + khkw];
     Wf[e] = v;
 }
-// data gradient: Wd[ci][khkw'*CO + co] = W[co][ci][8 - khkw']
+// data gradient: Wd[ci][k] = W[co][ci][8 - khkw'], k = (co/16)*144 + khkw'*16 + co%16 (the
+// channel-slice-major order of Im2colKC over dZ; CO % 16 == 0 for every layer with a data
+// gradient)
 static __global__ void k_pack_dgrad(const float* __restrict__ W, float* __restrict__ Wd, int CO,
                                     int CI) {
     const int e = blockIdx.x * 256 + threadIdx.x;
@@ -409,8 +420,9 @@ static __global__ void k_pack_dgrad(const float* __restrict__ W, float* __restri
     if (e >= CI * KD) return;
     const int ci = e / KD;
     const int k = e - ci * KD;
-    const int khkw = k / CO;
-    const int co = k - khkw * CO;
+    const int cs = k / 144, r = k - 144 * cs;
+    const int khkw = r >> 4;
+    const int co = 16 * cs + (r & 15);
     Wd[e] = W[(co * CI + ci) * 9 + (8 - khkw)];
 }
 
@@ -421,6 +433,7 @@ static int pack_conv(const float* W, float* wf, float* wd, int CO, int CI, int C
                        CI, CIP, KP);
     FLSIM_LAUNCH_CHECK();
     if (wd) {
+        if (CO % 16 != 0) return 1;
         hipLaunchKernelGGL(k_pack_dgrad, dim3(ceil_div((long)CI * 9 * CO, 256)), dim3(256), 0, st,
                            W, wd, CO, CI);
         FLSIM_LAUNCH_CHECK();
