@@ -7,6 +7,37 @@ namespace flsim {
 
 __device__ __forceinline__ f32x4 ldg4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+// streaming store (non-temporal): activations and gradients written once per chunk, far larger
+// than L2 + MALL.  Plain stores of them reach ~3.8 TB/s, these ~5.4 (profiles/r02d/lab_conv1.txt)
+__device__ __forceinline__ void st_nt4(float* p, f32x4 v) {
+    __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+}
+
+// Predicated operand load: lanes whose unit is padding or out of range issue no memory request
+// (exec-masked).  A branch-free form that loads from a fixed valid address and selects zero was
+// 6-12 % slower on every conv GEMM (all masked lanes hit one line; profiles/r02d/lab_ablation.txt).
+__device__ __forceinline__ f32x4 ldg4_or0(const float* p, const float* /*safe*/, bool ok) {
+    return ok ? ldg4(p) : zero4();
+}
+
+// r / D for 0 <= r < R by one 24-bit multiply and a shift (exact on that range, checked at
+// compile time): the per-unit pixel -> (row, column) split of the k-major loaders
+template <unsigned D, unsigned R>
+struct SmallDiv {
+    static constexpr unsigned find(bool want_shift) {
+        for (unsigned sh = 4; sh < 24; ++sh) {
+            const unsigned m = ((1u << sh) + D - 1) / D;
+            if ((unsigned long long)(R - 1) * m >= (1ull << 24) * 256ull) break;
+            bool ok = true;
+            for (unsigned r = 0; r < R && ok; ++r) ok = ((r * m) >> sh) == r / D;
+            if (ok) return want_shift ? sh : m;
+        }
+        return 0;
+    }
+    static constexpr unsigned M = find(false), SH = find(true);
+    static_assert(M != 0 && R * M < (1u << 31) && R < (1u << 24), "no 24-bit magic for this range");
+    __device__ static unsigned div(unsigned r) { return __umul24(r, M) >> SH; }
+};
 
 // ---------------------------------------------------------------------------------------------
 // A operand of a 3x3 / stride-1 convolution run as implicit GEMM (forward, or data-gradient as
@@ -88,8 +119,8 @@ struct Im2colKC {
             const long off = (long)(kh * IW + (khkw - 3 * kh)) * CI + ci0;
 #pragma unroll
             for (int j = 0; j < UNITS; ++j) {
-                const bool ok = khkw < 9 && ((tapmask[j] >> khkw) & 1);
-                r[j] = ok ? ldg4(X + base[j] + off) : zero4();
+                const bool ok = (tapmask[j] >> khkw) & 1;
+                r[j] = ldg4_or0(X + base[j] + off, X, ok);
             }
         } else {
             const int k = ks * GK + 4 * q;          // CI == 4: one tap per lane quad
@@ -99,7 +130,7 @@ struct Im2colKC {
 #pragma unroll
             for (int j = 0; j < UNITS; ++j) {
                 const bool ok = khkw < 9 && ((tapmask[j] >> khkw) & 1);
-                r[j] = ok ? ldg4(X + base[j] + off) : zero4();
+                r[j] = ldg4_or0(X + base[j] + off, X, ok);
             }
         }
     }
@@ -139,7 +170,7 @@ struct RowsKC {
     }
     __device__ void load(int ks, f32x4 (&r)[UNITS]) const {
 #pragma unroll
-        for (int j = 0; j < UNITS; ++j) r[j] = rowp[j] ? ldg4(rowp[j] + ks * GK) : zero4();
+        for (int j = 0; j < UNITS; ++j) r[j] = ldg4_or0(rowp[j] + ks * GK, P, rowp[j] != nullptr);
     }
     __device__ void store(float* lds, const f32x4 (&r)[UNITS]) const {
 #pragma unroll
@@ -160,42 +191,50 @@ struct RowsKM {
     static constexpr int ROWS = TR;
     static constexpr bool KC = false;
     static constexpr int C4 = ROWS / 4;
-    static constexpr int TOTAL = GK * C4;
-    static constexpr int UNITS = (TOTAL + NT - 1) / NT;
+    // thread -> (one k row, UNITS column chunks): the row's address (and for PO > 0 its window
+    // split) is computed once per thread and k-step, not once per unit
+    static constexpr int TPR = NT / GK;
+    static_assert(NT % GK == 0, "");
+    static constexpr int UNITS = (C4 + TPR - 1) / TPR;
     const float* P;
     long ld;
     int NK;
     int NC;
+    int krow;
     int c_off[UNITS];
-    short krow[UNITS], c4[UNITS];
+    short c4[UNITS];
     __device__ void setup(int c0, int tid) {
+        krow = tid / TPR;
 #pragma unroll
         for (int j = 0; j < UNITS; ++j) {
-            const int u = tid + j * NT;
-            krow[j] = (short)(u / C4);
-            c4[j] = (short)(u % C4);
-            const int col = c0 + 4 * (u % C4);
-            c_off[j] = (u < TOTAL && col < NC) ? col : -1;
+            const int c = tid % TPR + TPR * j;
+            c4[j] = (short)c;
+            const int col = c0 + 4 * c;
+            c_off[j] = (c < C4 && col < NC) ? col : -1;
         }
     }
     __device__ void load(int ks, f32x4 (&r)[UNITS]) const {
-#pragma unroll
-        for (int j = 0; j < UNITS; ++j) {
-            const int k = ks * GK + krow[j];
-            long row = k;
-            if constexpr (PO > 0) {
-                const unsigned img = (unsigned)k / (unsigned)(PV * PV);
-                const unsigned rem = (unsigned)k - img * (PV * PV);
-                const unsigned oh = rem / (unsigned)PV;
-                row = (long)img * (PO * PO) + oh * PO + (rem - oh * PV);
-            }
-            r[j] = (c_off[j] >= 0 && k < NK) ? ldg4(P + row * ld + c_off[j]) : zero4();
+        const int k = ks * GK + krow;
+        long row = k;
+        if constexpr (PO > 0) {
+            // window split: block-uniform base once (scalar), the thread's row by a carry and a
+            // small division
+            const unsigned img0 = (unsigned)(ks * GK) / (unsigned)(PV * PV);
+            unsigned rem = (unsigned)(ks * GK) - img0 * (PV * PV) + krow, img = img0;
+            static_assert(PV * PV >= GK, "window split assumes one image carry at most");
+            if (rem >= (unsigned)(PV * PV)) { rem -= PV * PV; ++img; }
+            const unsigned oh = SmallDiv<PV, PV * PV + GK>::div(rem);
+            row = (long)img * (PO * PO) + oh * PO + (rem - oh * PV);
         }
+        const float* rp = P + row * ld;
+        const bool rok = k < NK;
+#pragma unroll
+        for (int j = 0; j < UNITS; ++j) r[j] = ldg4_or0(rp + c_off[j], P, rok && c_off[j] >= 0);
     }
     __device__ void store(float* lds, const f32x4 (&r)[UNITS]) const {
 #pragma unroll
         for (int j = 0; j < UNITS; ++j)
-            if (TOTAL % NT == 0 || krow[j] < GK) store_unit<false, ROWS>(lds, krow[j], c4[j], r[j]);
+            if (C4 % TPR == 0 || c4[j] < C4) store_unit<false, ROWS>(lds, krow, c4[j], r[j]);
     }
 };
 
@@ -212,49 +251,58 @@ struct Im2colKM {
     static constexpr int OH = VO > 0 ? VO : IH + 2 * PAD - 2;
     static constexpr int OW = VO > 0 ? VO : IW + 2 * PAD - 2;
     static constexpr int C4 = ROWS / 4;
-    static constexpr int TOTAL = GK * C4;
-    static constexpr int UNITS = (TOTAL + NT - 1) / NT;
+    // thread -> (one pixel row of the tile, UNITS column chunks): the pixel split is done once
+    // per thread and k-step, each unit only adds its tap
+    static constexpr int TPR = NT / GK;
+    static_assert(NT % GK == 0, "");
+    static constexpr int UNITS = (C4 + TPR - 1) / TPR;
     const float* X;
     int M;  // total pixels
-    int coff[UNITS];   // ci, or -1 when the column is padding / out of range
-    short kh[UNITS], kw[UNITS];
-    short krow[UNITS], c4[UNITS];
+    int krow;
+    int coff[UNITS];   // ((kh - PAD) * IW + kw - PAD) * CI + ci: the column's offset from pixel (oh, ow)
+    short kh[UNITS], kw[UNITS];   // tap of the column; kh = -64 when it is padding
+    short c4[UNITS];
     __device__ void setup(int c0, int tid) {
+        krow = tid / TPR;
 #pragma unroll
         for (int j = 0; j < UNITS; ++j) {
-            const int u = tid + j * NT;
-            krow[j] = (short)(u / C4);
-            c4[j] = (short)(u % C4);
-            const int kk = c0 + 4 * (u % C4);
+            const int c = tid % TPR + TPR * j;
+            c4[j] = (short)c;
+            const int kk = c0 + 4 * c;
             const int khkw = kk / CI;
             const int ci = kk - khkw * CI;
-            kh[j] = (short)(khkw / 3);
+            const bool real = c < C4 && khkw < 9;
+            kh[j] = (short)(real ? khkw / 3 : -64);
             kw[j] = (short)(khkw % 3);
-            coff[j] = (u < TOTAL && khkw < 9) ? ci : -1;
+            coff[j] = real ? ((khkw / 3 - PAD) * IW + (khkw % 3 - PAD)) * CI + ci : 0;
         }
     }
     __device__ void load(int ks, f32x4 (&r)[UNITS]) const {
+        const int p = ks * GK + krow;
+        const unsigned img0 = (unsigned)(ks * GK) / (unsigned)(OH * OW);   // block-uniform
+        unsigned rem = (unsigned)(ks * GK) - img0 * (OH * OW) + krow, img = img0;
+        if constexpr (OH * OW >= GK) {        // the thread's pixel is at most one image further
+            if (rem >= (unsigned)(OH * OW)) { rem -= OH * OW; ++img; }
+        } else {                              // tiny maps (VGG's 2x2): several images per k-step
+            const unsigned q = SmallDiv<OH * OW, OH * OW + GK>::div(rem);
+            img += q;
+            rem -= q * (OH * OW);
+        }
+        const int oh = (int)SmallDiv<OW, OH * OW + GK>::div(rem);
+        const int ow = (int)rem - oh * OW;
+        const float* xp = X + ((long)img * IH * IW + oh * IW + ow) * CI;
+        const bool pok = p < M;
 #pragma unroll
         for (int j = 0; j < UNITS; ++j) {
-            const int p = ks * GK + krow[j];
-            f32x4 v = zero4();
-            if (coff[j] >= 0 && p < M) {
-                const int nimg = p / (OH * OW);
-                const int rem = p - nimg * (OH * OW);
-                const int oh = rem / OW;
-                const int ow = rem - oh * OW;
-                const int ih = oh + kh[j] - PAD;
-                const int iw = ow + kw[j] - PAD;
-                if ((unsigned)ih < (unsigned)IH && (unsigned)iw < (unsigned)IW)
-                    v = ldg4(X + ((long)nimg * IH * IW + ih * IW + iw) * CI + coff[j]);
-            }
-            r[j] = v;
+            const int ih = oh + kh[j] - PAD, iw = ow + kw[j] - PAD;
+            const bool ok = pok && (unsigned)ih < (unsigned)IH && (unsigned)iw < (unsigned)IW;
+            r[j] = ldg4_or0(xp + coff[j], X, ok);
         }
     }
     __device__ void store(float* lds, const f32x4 (&r)[UNITS]) const {
 #pragma unroll
         for (int j = 0; j < UNITS; ++j)
-            if (TOTAL % NT == 0 || krow[j] < GK) store_unit<false, ROWS>(lds, krow[j], c4[j], r[j]);
+            if (C4 % TPR == 0 || c4[j] < C4) store_unit<false, ROWS>(lds, krow, c4[j], r[j]);
     }
 };
 
@@ -309,7 +357,7 @@ struct EpiBiasReluRows {
         f32x4* dst = reinterpret_cast<f32x4*>(Y + (long)m0 * NC);
         for (int q = tid; q < rows * N4; q += nt) {
             const int r = q / N4, c = q - r * N4;
-            dst[q] = *reinterpret_cast<const f32x4*>(tile + r * ld + 4 * c);
+            st_nt4(reinterpret_cast<float*>(dst + q), *reinterpret_cast<const f32x4*>(tile + r * ld + 4 * c));
         }
     }
 };
@@ -407,7 +455,7 @@ struct EpiMaskRows {
             o.y = a.y > 0.f ? t.y : 0.f;
             o.z = a.z > 0.f ? t.z : 0.f;
             o.w = a.w > 0.f ? t.w : 0.f;
-            dst[q] = o;
+            st_nt4(reinterpret_cast<float*>(dst + q), o);
         }
     }
 };

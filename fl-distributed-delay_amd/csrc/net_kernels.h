@@ -129,7 +129,7 @@ k_pool_scatter(const float* __restrict__ gy, const uint8_t* __restrict__ idx,
         v.y = (((id >> 8) & 0xff) == (uint32_t)pos) ? g.y : 0.f;
         v.z = (((id >> 16) & 0xff) == (uint32_t)pos) ? g.z : 0.f;
         v.w = ((id >> 24) == (uint32_t)pos) ? g.w : 0.f;
-        *reinterpret_cast<f32x4*>(dz + (((long)n * H + h) * W + w) * C + c) = v;
+        st_nt4(dz + (((long)n * H + h) * W + w) * C + c, v);
     }
 }
 
@@ -174,7 +174,7 @@ k_pool_scatter_nchw(const float* __restrict__ gy, const uint8_t* __restrict__ id
             v.y = (((id >> 8) & 0xff) == (uint32_t)pos) ? g.y : 0.f;
             v.z = (((id >> 16) & 0xff) == (uint32_t)pos) ? g.z : 0.f;
             v.w = ((id >> 24) == (uint32_t)pos) ? g.w : 0.f;
-            *reinterpret_cast<f32x4*>(dz + (((long)n * H + h) * W + w) * C + c) = v;
+            st_nt4(dz + (((long)n * H + h) * W + w) * C + c, v);
         }
     }
 }

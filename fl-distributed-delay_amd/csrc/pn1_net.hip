@@ -170,11 +170,112 @@ static int pack_weights(const GradState& g, const float* theta, hipStream_t st) 
     return 0;
 }
 
+// conv1 + bias + ReLU (models.py:29), direct.  K is only 27 (3 channels x 9 taps), so the GEMM
+// pipeline (LDS-staged operands, K padded to 48) spends its time on staging, not on MFMAs, and the
+// kernel is bound by writing a1 (S*34*34*48 floats).  Here each wave keeps conv1's weights in
+// registers, loads its input pixels straight into MFMA operands and writes a1 through a private
+// LDS tile as whole contiguous rows (float4, coalesced).  No block barrier: waves are independent.
+//
+// 16x16x4 f32 MFMA, lane l: i = l & 15 (output pixel of the row tile / output channel of the
+// column tile), g = l >> 4 (k slot).  Taps 0..7 run as two k-steps s of four MFMAs (kk = input
+// channel): lane slot g holds tap 4s + g, so one float4 load of x0 (NHWC, channel 3 = 0) feeds the
+// four MFMAs.  Tap 8 is one MFMA whose k slot g is the input channel.  27 real MFMA k-values (plus
+// the zero 4th channel), 9 MFMAs per 16x16 output tile.
+constexpr int C1_ROWS = 32;     // output pixels per wave iteration (two 16-row tiles)
+constexpr int C1_LD = 52;       // staging row stride (floats): 16-B aligned, rows on different banks
+__global__ void __launch_bounds__(256)
+k_conv1_fwd(const float* __restrict__ x0, const float* __restrict__ W, const float* __restrict__ bias,
+            float* __restrict__ a1, long units) {
+    __shared__ __attribute__((aligned(16))) float stage[4][C1_ROWS * C1_LD];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int i = lane & 15, g = lane >> 4;
+    float* st = stage[wv];
+    f32x4 wb[3][2];
+    float w8[3], bj[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const int co = 16 * j + i;
+#pragma unroll
+        for (int sx = 0; sx < 2; ++sx) {
+            const int tap = 4 * sx + g;
+            wb[j][sx] = f32x4{W[(co * 3 + 0) * 9 + tap], W[(co * 3 + 1) * 9 + tap],
+                              W[(co * 3 + 2) * 9 + tap], 0.f};
+        }
+        w8[j] = g < 3 ? W[(co * 3 + g) * 9 + 8] : 0.f;
+        bj[j] = bias[co];
+    }
+    auto load = [&](long u, f32x4 (&xa)[2][2], float (&x8)[2]) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const long m = u * C1_ROWS + 16 * t + i;
+            const long smp = m / 1156;
+            const int rem = (int)(m - smp * 1156);
+            const int oh = rem / 34, ow = rem - (rem / 34) * 34;
+            const float* xs = x0 + smp * 4096;
+#pragma unroll
+            for (int sx = 0; sx < 2; ++sx) {
+                const int tap = 4 * sx + g;
+                const int ih = oh + tap / 3 - 2, iw = ow + tap % 3 - 2;
+                xa[t][sx] = ((unsigned)ih < 32u && (unsigned)iw < 32u)
+                                ? *reinterpret_cast<const f32x4*>(xs + (ih * 32 + iw) * 4) : zero4();
+            }
+            x8[t] = (oh < 32 && ow < 32) ? xs[(oh * 32 + ow) * 4 + g] : 0.f;   // tap 8: (ih, iw) = (oh, ow)
+        }
+    };
+    const long nw = (long)gridDim.x * 4;
+    long u = (long)blockIdx.x * 4 + wv;
+    f32x4 xa[2][2];
+    float x8[2];
+    if (u < units) load(u, xa, x8);
+    for (; u < units; u += nw) {
+        f32x4 acc[2][3];
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                f32x4 c = zero4();
+#pragma unroll
+                for (int sx = 0; sx < 2; ++sx)
+#pragma unroll
+                    for (int kk = 0; kk < 4; ++kk) c = mfma16(xa[t][sx][kk], wb[j][sx][kk], c);
+                acc[t][j] = mfma16(x8[t], w8[j], c);
+            }
+        if (u + nw < units) load(u + nw, xa, x8);     // next unit's loads fly during the stores
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    st[(16 * t + 4 * g + r) * C1_LD + 16 * j + i] = fmaxf(acc[t][j][r] + bj[j], 0.f);
+        __builtin_amdgcn_wave_barrier();
+        f32x4* dst = reinterpret_cast<f32x4*>(a1 + u * C1_ROWS * 48);
+#pragma unroll
+        for (int q0 = 0; q0 < C1_ROWS * 12; q0 += 64) {
+            const int q = q0 + lane, row = q / 12, c4 = q - (q / 12) * 12;
+            st_nt4(reinterpret_cast<float*>(dst + q), *reinterpret_cast<const f32x4*>(st + row * C1_LD + 4 * c4));
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+static int conv1_fwd(const float* x0, const float* W, const float* bias, float* a1, int S,
+                     hipStream_t st) {
+    const long M = (long)S * 34 * 34;
+    if (M % C1_ROWS) return 1;             // S is a multiple of 128 (whole sample groups)
+    const long units = M / C1_ROWS;
+    const int grid = (int)(units / 4 < 2048 ? (units + 3) / 4 : 2048);
+    const ProbeSlot ps = probe_begin();
+    hipExtLaunchKernelGGL(k_conv1_fwd, dim3(grid), dim3(256), 0, st, ps.start, ps.stop, 0, x0, W,
+                          bias, a1, units);
+    FLSIM_LAUNCH_CHECK();
+    return probe_end(ps, K_FWD1, 2.0 * M * 48 * 27);
+}
+
 static int forward(const GradState& g, const WS& w, const float* theta, int S,
                    const WorkerRec* workers, uint64_t seed, int dropout, hipStream_t st) {
     // conv1, conv2 (+ReLU)  models.py:29-30
-    RC((conv_like<32, 32, 4, 2, 2, 3, 4, 1>(w.x0, S, g.wf[0], 48, 48,
-        EpiBiasReluRows<48>{w.a1, theta + P_OFF[1], S * 34 * 34}, st, K_FWD1, 27)));
+    RC(conv1_fwd(w.x0, theta + P_OFF[0], theta + P_OFF[1], w.a1, S, st));
     // conv2 + ReLU + pool1 + dropout1 (models.py:30-32), one fused launch
     RC((conv_pool_fwd<34, 34, 48, 48, 2, 2, 3, 8, 1, false>(w.a1, S, g.wf[1], 432, w.d1, w.i1,
         theta + P_OFF[3], workers, seed, SITE_DROP1, THR_P25, SCALE_P25, dropout, st, K_FWD2,

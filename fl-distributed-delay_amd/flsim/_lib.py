@@ -11,7 +11,8 @@ import os
 
 import torch  # noqa: F401  (must be loaded before libflsim.so, see module docstring)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libflsim.so")
+LIB_PATH = os.environ.get("FLSIM_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                        "_lib", "libflsim.so")
 
 EXPORTS = [
     "flsim_last_error", "flsim_sched_create", "flsim_sched_destroy", "flsim_sched_epoch",

@@ -4,7 +4,8 @@ VGG11Ref, itself pinned to the reference's own vgg11() by tests/golden/vgg.npz).
 
 Tolerances (as tests/test_gpu_parity.py):
   * one worker-step gradient: per-tensor rel-L2 vs fp64 <= 5e-3; whole gradient within
-    2.5e-4 of |g64| (or 4x the CPU's own fp32 error);
+    2.5e-4 of |g64| (or 4x the CPU's own fp32 error), or else at most 8 knife-edge decisions
+    that fp64 takes the other way, with the teacher-forced gradient exact to 2e-5;
   * teacher-forced (the GPU's own ReLU / argmax / dropout decisions in an fp64 reference):
     per-tensor rel-L2 <= 2e-5, losses to 1e-5;
   * losses |dloss| <= 1e-4 on the first step, <= 1e-3 over the first epochs; trace bit-exact.
@@ -48,41 +49,18 @@ def _run(theta_np, items, dropout, pool, n_total=4):
     return eng, S.cpu().numpy().astype(np.float64), loss.cpu().numpy()
 
 
-@pytest.mark.parametrize("dropout", [False, True])
-def test_vgg_single_worker_step_gradient(pool, dropout):
-    from flsim.engine import VGG11_SHAPES
-    from oracle import model_ref as MR
-    sim = MR.OracleSim(4, delay=2, pool=pool, dropout=dropout, model=M)
-    items = [(0, 0, 0)]
-    g32, l32 = sim.grad_of(sim.theta, items)
-    g64, l64 = sim.grad_of(sim.theta, items, dtype=torch.float64)
-    _, g, loss = _run(sim.theta, items, dropout, pool)
-    assert abs(float(loss[0]) - l64[0]) <= 1e-4, (loss[0], l64[0])
-    off = 0
-    for (name, shp) in VGG11_SHAPES:
-        n = int(np.prod(shp))
-        r = _rel_l2(g[off:off + n], g64[off:off + n])
-        off += n
-        assert r <= 5e-3, (name, r)
-    e_gpu = np.linalg.norm(g - g64)
-    e_cpu = np.linalg.norm(g32.astype(np.float64) - g64)
-    assert e_gpu <= max(2.5e-4 * np.linalg.norm(g64), 4 * e_cpu), (e_gpu, e_cpu)
-
-
-@pytest.mark.parametrize("dropout,items", [
-    (False, [(0, 1, 2)]), (True, [(0, 1, 2)]), (True, [(1, 0, 3), (1, 2, 0)])])
-def test_vgg_gradient_teacher_forced_decisions(pool, dropout, items):
-    """Every backward kernel checked tightly: an fp64 reference that takes the GPU's own forward
-    decisions (ReLU signs, max-pool argmax, dropout masks, read back from the workspace) must give
-    the GPU's gradient to fp32 accumulation accuracy.  The two-item case is ONE chunk of 256
-    samples whose gradient must be the sum of the per-worker mean-CE gradients (agents.py:35)."""
+def _teacher_forced(sim, eng, items, dropout):
+    """fp64 VGG-11 forward + backward that takes the GPU's own forward decisions (ReLU signs, max-
+    pool argmax, dropout masks, read back from the workspace).  Returns the per-tensor gradient,
+    the per-worker losses, and the number of GPU decisions that the fp64 pre-activations computed
+    on the way disagree with (a ReLU sign, a pool argmax among live windows, a kept unit whose
+    fp64 pre-activation is <= 0): knife-edge decisions any fp32 order can take either way."""
     import torch.nn.functional as F
-    from flsim.engine import VGG11_SHAPES, VGG11Engine
+    import _flips
+    from flsim.engine import VGG11Engine
     from oracle import model_ref as MR
     from test_gpu_parity import _gather_pool
     NS = 128 * len(items)
-    sim = MR.OracleSim(4, delay=2, pool=pool, dropout=dropout, model=M)
-    eng, g, loss = _run(sim.theta, items, dropout, pool)
     ids = {name: j for j, name in enumerate(VGG11Engine.WORKSPACE)}
 
     def W(name, shp, dt=torch.float32):
@@ -104,6 +82,7 @@ def test_vgg_gradient_teacher_forced_decisions(pool, dropout, items):
          for a in MR.split_flat(sim.theta.astype(np.float64), M)]
     cw, cb = P[0:16:2], P[1:16:2]
     l1w, l1b, l2w, l2b, l3w, l3b = P[16:]
+    flips = [0]
 
     def m(t):
         return (t > 0).to(torch.float64)
@@ -111,52 +90,124 @@ def test_vgg_gradient_teacher_forced_decisions(pool, dropout, items):
     def conv(h, j):
         return F.conv2d(h, cw[j], cb[j], padding=1)
 
+    def pool(z, idx, mask, kept_only=False):
+        zd = z.detach()
+        own = _flips.pool_idx(F.relu(zd))
+        gidx = torch.from_numpy(idx.astype(np.int64)).permute(0, 3, 1, 2)
+        pz = _gather_pool(zd, idx)
+        live = (pz > 0) | (mask > 0)
+        flips[0] += int(((own != gidx) & live).sum())
+        flips[0] += int(((mask > 0) & (pz <= 0)).sum()) if kept_only else int(((pz > 0) != (mask > 0)).sum())
+        return _gather_pool(z, idx) * m(mask)
+
+    def relu(z, mask, kept_only=False):
+        zd = z.detach()
+        flips[0] += int(((mask > 0) & (zd <= 0)).sum()) if kept_only else int(((zd > 0) != (mask > 0)).sum())
+        return z * m(mask)
+
     s50 = 2.0 if dropout else 1.0
     lrefs = []
     for wi, it in enumerate(items):
         sl = slice(128 * wi, 128 * (wi + 1))
         a = {k: v[sl] for k, v in A.items()}
         x, y = sim.batch(*it, dtype=torch.float64)
-        h = _gather_pool(conv(x, 0), a["i1"]) * m(a["d1"])
-        h = _gather_pool(conv(h, 1), a["i2"]) * m(a["d2"])
-        h = conv(h, 2) * m(a["a3"])
-        h = _gather_pool(conv(h, 3), a["i4"]) * m(a["d4"])
-        h = conv(h, 4) * m(a["a5"])
-        h = _gather_pool(conv(h, 5), a["i6"]) * m(a["d6"])
-        h = conv(h, 6) * m(a["a7"])
-        h = _gather_pool(conv(h, 7), a["i8"]).reshape(128, 512) * m(a["f0"]) * s50
-        h = F.linear(h, l1w, l1b) * m(a["e1"]) * s50
-        h = F.linear(h, l2w, l2b) * m(a["e2"])
+        h = pool(conv(x, 0), a["i1"], a["d1"])
+        h = pool(conv(h, 1), a["i2"], a["d2"])
+        h = relu(conv(h, 2), a["a3"])
+        h = pool(conv(h, 3), a["i4"], a["d4"])
+        h = relu(conv(h, 4), a["a5"])
+        h = pool(conv(h, 5), a["i6"], a["d6"])
+        h = relu(conv(h, 6), a["a7"])
+        h = pool(conv(h, 7), a["i8"], a["f0"].reshape(128, 512, 1, 1), kept_only=dropout)
+        h = h.reshape(128, 512) * s50
+        h = relu(F.linear(h, l1w, l1b), a["e1"], kept_only=dropout) * s50
+        h = relu(F.linear(h, l2w, l2b), a["e2"])
         lref = F.cross_entropy(F.linear(h, l3w, l3b), y)
         lref.backward()
         lrefs.append(lref.item())
+    g = np.concatenate([p.grad.reshape(-1).numpy() for p in P])
+    return g, lrefs, flips[0]
+
+
+@pytest.mark.parametrize("dropout", [False, True])
+def test_vgg_single_worker_step_gradient(pool, dropout):
+    """The GPU gradient of one worker-step against the fp64 oracle with its OWN decisions.  A
+    knife-edge decision (ReLU sign / argmax within rounding) taken the other way moves a gradient
+    by ~1e-4 of |g|; so beyond the flat bound the excess must come with a handful of such
+    decisions (counted against the fp64 pre-activations, at most FLIPS of ~2e6) while the
+    teacher-forced gradient (same decisions) stays at fp32 accuracy."""
+    from flsim.engine import VGG11_SHAPES
+    from oracle import model_ref as MR
+    FLIPS = 8
+    sim = MR.OracleSim(4, delay=2, pool=pool, dropout=dropout, model=M)
+    items = [(0, 0, 0)]
+    g32, l32 = sim.grad_of(sim.theta, items)
+    g64, l64 = sim.grad_of(sim.theta, items, dtype=torch.float64)
+    eng, g, loss = _run(sim.theta, items, dropout, pool)
+    assert abs(float(loss[0]) - l64[0]) <= 1e-4, (loss[0], l64[0])
+    off = 0
+    for (name, shp) in VGG11_SHAPES:
+        n = int(np.prod(shp))
+        r = _rel_l2(g[off:off + n], g64[off:off + n])
+        off += n
+        assert r <= 5e-3, (name, r)
+    e_gpu = np.linalg.norm(g - g64)
+    e_cpu = np.linalg.norm(g32.astype(np.float64) - g64)
+    if e_gpu > max(2.5e-4 * np.linalg.norm(g64), 4 * e_cpu):
+        g_tf, _, flips = _teacher_forced(sim, eng, items, dropout)
+        assert 1 <= flips <= FLIPS, (e_gpu, e_cpu, flips)
+        assert _rel_l2(g, g_tf) <= 2e-5, (e_gpu, flips, _rel_l2(g, g_tf))
+
+
+@pytest.mark.parametrize("dropout,items", [
+    (False, [(0, 1, 2)]), (True, [(0, 1, 2)]), (True, [(1, 0, 3), (1, 2, 0)])])
+def test_vgg_gradient_teacher_forced_decisions(pool, dropout, items):
+    """Every backward kernel checked tightly: an fp64 reference that takes the GPU's own forward
+    decisions (ReLU signs, max-pool argmax, dropout masks, read back from the workspace) must give
+    the GPU's gradient to fp32 accumulation accuracy.  The two-item case is ONE chunk of 256
+    samples whose gradient must be the sum of the per-worker mean-CE gradients (agents.py:35)."""
+    from flsim.engine import VGG11_SHAPES
+    from oracle import model_ref as MR
+    sim = MR.OracleSim(4, delay=2, pool=pool, dropout=dropout, model=M)
+    eng, g, loss = _run(sim.theta, items, dropout, pool)
+    g_tf, lrefs, flips = _teacher_forced(sim, eng, items, dropout)
     off = 0
     worst = {}
-    for (name, _), p in zip(VGG11_SHAPES, P):
-        n = p.numel()
-        worst[name] = _rel_l2(g[off:off + n], p.grad.reshape(-1).numpy())
+    for (name, shp) in VGG11_SHAPES:
+        n = int(np.prod(shp))
+        worst[name] = _rel_l2(g[off:off + n], g_tf[off:off + n])
         off += n
     np.testing.assert_allclose(loss, lrefs, atol=1e-5)
     assert max(worst.values()) <= 2e-5, worst
+    assert flips <= 8 * len(items), flips
 
 
 def test_vgg_simulation_matches_oracle_trajectory(pool):
     """The batched server loop with vgg11 (FLSimulation(model='vgg11')) against the oracle loop:
-    bit-exact staleness trace, losses within the fp32 tolerance."""
+    bit-exact staleness trace, each epoch's loss within the fp32 forward tolerance.  The oracle
+    starts every epoch from the GPU's theta / Adam moments: Adam's first steps turn any fp32
+    difference in a near-zero gradient (a knife-edge decision taken the other way, see
+    test_vgg_single_worker_step_gradient) into a parameter change of ~lr, so free-running
+    trajectories part by more than the forward tolerance within a few epochs.  The update itself
+    (rule() + Adam) is bit-exact with the oracle in tests/test_gpu_server_step.py."""
     from flsim.sim import FLSimulation
     from oracle import model_ref as MR
     n, d, ep = 3, 2, 4
     osim = MR.OracleSim(n, delay=d, throttle=True, pool=pool, model=M)
     gsim = FLSimulation(n, delay=d, throttle=True, device=DEV, chunk_workers=2, pool=pool, model=M)
     assert np.array_equal(gsim.theta.cpu().numpy(), osim.theta)
+    P = osim.theta.size
     for t in range(ep):
+        osim.theta = gsim.theta[:P].cpu().numpy().copy()
+        osim.m = gsim.m[:P].cpu().numpy().copy()
+        osim.v = gsim.v[:P].cpu().numpy().copy()
         lo = osim.epoch()
         lg = gsim.epoch()
         tr_o = osim.trace[-1]
         plan = gsim.trace[-1]
         assert [i for (_, i, _) in tr_o["items"]] == list(np.nonzero(plan.computes)[0])
         assert [s for (k, s) in tr_o["appended"] if k == "stale"] == [s for (_, s) in plan.stale]
-        assert abs(lg - lo) <= (1e-4 if t == 0 else 1e-3), (t, lg, lo)
+        assert abs(lg - lo) <= 1e-4, (t, lg, lo)
 
 
 def test_vgg_eval_predictions_match_oracle(pool):

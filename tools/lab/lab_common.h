@@ -19,6 +19,10 @@ struct Im2colKCo : Im2colKC<IH, IW, CI, PAD, TR, NT> {
     using Base = Im2colKC<IH, IW, CI, PAD, TR, NT>;
     static_assert(CI % 16 == 0, "");
     __device__ void load(int ks, f32x4 (&r)[Base::UNITS]) const {
+        if constexpr (ORD == 1) {      // the product's order (loaders.h)
+            Base::load(ks, r);
+            return;
+        }
         int khkw, ci0;
         if constexpr (ORD == 0) {
             khkw = ks * GK / CI;
@@ -40,22 +44,7 @@ struct Im2colKCo : Im2colKC<IH, IW, CI, PAD, TR, NT> {
 
 template <int IH, int IW, int CI, int PAD, int TR, int NT, int ORD, int VO = 0>
 struct Im2colKMo : Im2colKM<IH, IW, CI, PAD, TR, NT, VO> {
-    using Base = Im2colKM<IH, IW, CI, PAD, TR, NT, VO>;
-    __device__ void setup(int c0, int tid) {
-        Base::setup(c0, tid);
-        if constexpr (ORD == 1) {
-#pragma unroll
-            for (int j = 0; j < Base::UNITS; ++j) {
-                const int u = tid + j * NT;
-                const int kk = c0 + 4 * (u % Base::C4);
-                const int cs = kk / 144, rem = kk - 144 * cs;
-                const int tap = rem >> 4;
-                this->kh[j] = (short)(tap / 3);
-                this->kw[j] = (short)(tap % 3);
-                this->coff[j] = (u < Base::TOTAL && cs < CI / 16) ? cs * 16 + (rem & 15) : -1;
-            }
-        }
-    }
+    static_assert(ORD == 0, "the product's column order only");
 };
 
 static float* dalloc(size_t n, float scale) {
