@@ -277,7 +277,7 @@ static int forward(const GradState& g, const WS& w, const float* theta, int S,
     // conv1, conv2 (+ReLU)  models.py:29-30
     RC(conv1_fwd(w.x0, theta + P_OFF[0], theta + P_OFF[1], w.a1, S, st));
     // conv2 + ReLU + pool1 + dropout1 (models.py:30-32), one fused launch
-    RC((conv_pool_fwd<34, 34, 48, 48, 2, 2, 3, 8, 1, false>(w.a1, S, g.wf[1], 432, w.d1, w.i1,
+    RC((conv_pool_fwd<34, 34, 48, 48, 2, 2, 3, 4, 1, false>(w.a1, S, g.wf[1], 432, w.d1, w.i1,
         theta + P_OFF[3], workers, seed, SITE_DROP1, THR_P25, SCALE_P25, dropout, st, K_FWD2,
         432)));
     RC((conv_like<18, 18, 48, 2, 4, 3, 4, 2>(w.d1, S, g.wf[2], 96, 432,
@@ -343,7 +343,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
         EpiMask<true>{w.gx, w.a3, S * 20 * 20, 96}, st, K_DG4, 864)));
     float* dz3 = w.gx;
     // ---- conv3: wgrad (input d1), bias, dgrad -> grad wrt d1 (site 1) into gy ----
-    RC((conv_wgrad<18, 18, 48, 2, 3, 3, 2, 2>(dz3, w.d1, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW,
+    RC((conv_wgrad<18, 18, 48, 2, 3, 3, 2, 1>(dz3, w.d1, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW,
                                              st, K_WG3, 432)));
     RC((conv_like<20, 20, 96, 0, 2, 3, 8, 1>(dz3, S, g.wd[2], 48, 864,
         EpiDropMask{w.gy, w.d1, s25, S * 18 * 18, 48}, st, K_DG3, 864)));
