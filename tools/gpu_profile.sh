@@ -14,7 +14,7 @@ echo "trace pass ok"
 # HBM bytes of the aggregation kernel and the heaviest GEMMs, one counter group per pass
 for PMC in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 300 rocprofv3 --pmc $PMC --output-format csv -d "$OUT/pmc_$PMC" -o run \
-        --kernel-include-regex "k_slab_step|k_agg_stream|gemm_kernel" \
+        --kernel-include-regex "k_slab_step|k_agg_stream|gemm_kernel|k_conv1_fwd|k_pool_scatter" \
         -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-probe \
         > "$OUT/bench_$PMC.log" 2>&1 || { echo "pmc $PMC failed $?"; exit 1; }
     echo "pmc $PMC ok"

@@ -26,6 +26,11 @@ def probe_name(kname):
         if m.group(1) == "false":
             return "slab_sum"
         return "slab_step" if m.group(2) == "true" else "slab_step_seq"
+    if "k_conv1_fwd" in kname:
+        return "conv1_fwd"
+    m = re.search(r"k_pool_scatter(_nchw)?<(\d+), (\d+), (\d+)", kname)
+    if m:
+        return f"pool_scatter_{m.group(2)}x{m.group(3)}x{m.group(4)}"
     m = re.search(r"k_agg_stream<(true|false)>", kname)
     if m:
         return "aggregate_adam" if m.group(1) == "true" else "aggregate_adam_seq"
