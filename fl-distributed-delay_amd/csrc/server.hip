@@ -322,7 +322,9 @@ __device__ __forceinline__ bool col_to_param(const SlabSeg& g, long col, long& t
 template <bool ADAM, bool INL>
 __device__ __forceinline__ void slab_step_wide(const StepArgs& A, const SlabSeg& g, int u, int ul,
                                                float* lds) {
-    constexpr int NYW = 2;          // entry arrays held in registers (the rest load on demand)
+    // entry arrays held in registers (the rest load on demand): all of a general-order program's
+    // arrays up to 8 (configs[3] uses 6), so no Y word of the interpreter waits on a global load
+    constexpr int NYW = 8;
     const int tid = threadIdx.x;
     const float* slab = A.base + g.slab_off;
     const ProgRef<INL> prog{A.R};
@@ -421,8 +423,14 @@ __device__ __forceinline__ void slab_step_wide(const StepArgs& A, const SlabSeg&
         if (A.S_out) *reinterpret_cast<f32x4*>(A.S_out + e) = a0;
         if constexpr (ADAM) {
             auto yf = [&](int q) -> f32x4 {
-                if (q < NYW) return ys[q];
-                return A.R.arr[q] ? ld(A.R.arr[q] + e) : f32x4{0.f, 0.f, 0.f, 0.f};
+                // q is uniform: a scalar branch chain picks the register, no indexed access
+                f32x4 r = f32x4{0.f, 0.f, 0.f, 0.f};
+                bool hit = false;
+#pragma unroll
+                for (int k = 0; k < NYW; ++k)
+                    if (q == k) { r = ys[k]; hit = true; }
+                if (!hit && A.R.arr[q]) r = ld(A.R.arr[q] + e);
+                return r;
             };
             const f32x4 sum = casc_run<INL ? 1 : CASC_PAD, true>(
                 prog, 0, casc_values(a0, A.R.info.need, A.R.info.lp), yf);

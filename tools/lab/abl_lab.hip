@@ -1,11 +1,15 @@
 // Ablation lab: 0 full, 1 no barrier, 2 no LDS stores, 3 no global loads, 4 no staging, 5 no staging
-// and no barrier, 6 A operand not loaded, 7 B operand not loaded (timing only: 1-5 compute wrong sums).  From the pipeline lab (development tool, not part of libflsim.so): the product's GEMM pipeline with
+// and no barrier, 6 A operand not loaded, 7 B operand not loaded, 9 no bias-gradient column sum (timing only: 1-5 compute wrong sums).  From the pipeline lab (development tool, not part of libflsim.so): the product's GEMM pipeline with
 // KSUB 16-deep sub-steps per LDS stage and barrier (fewer barriers per MFMA), and PIN = keep the
 // k-step's MFMAs ahead of the barrier (sched_barrier; the compiler otherwise hoists the barrier
 // above them).  Conv shapes of PerformantNet1 at S = 16384 samples, channel-slice-major K order.
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -I include
 //         -I fl-distributed-delay_amd/csrc tools/lab/ks_lab.hip -o tools/lab/ks_lab
 #include "lab_common.h"
+
+struct EpiSlabAccNoSum : EpiSlabAcc {
+    static constexpr bool ASUM = false;
+};
 
 template <int FM, int FN, int WAVES_M, int WAVES_N, int KSUB, int PIN, class AL, class BL, class EPI>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N)
@@ -196,6 +200,10 @@ static void conv_wgrad(const char* tag, const float* dz, const float* X, float* 
     using BL = Im2colKMo<IH, IH, CI, 2, BN, NT, 0, VO>;
     const int M = S * BL::OH * BL::OW;
     const int KP = 9 * CI;
+    if ((size_t)Z * CO * KP > (size_t)4096 * 48 * 432 || (size_t)Z * CO > (size_t)4096 * 192) {
+        printf("%-24s skipped: Z * CO * KP exceeds the lab's slab capacity\n", tag);
+        return;
+    }
     AL al;
     al.P = dz;
     al.ld = CO;
@@ -204,6 +212,12 @@ static void conv_wgrad(const char* tag, const float* dz, const float* X, float* 
     BL bl;
     bl.X = X;
     bl.M = M;
+    if (PIN == 9) {
+        EpiSlabAccNoSum epi;
+        epi.S = slab; epi.M = CO; epi.N = KP; epi.zstride = (long)CO * KP; epi.Bsl = bslab;
+        time_ks<FM, FN, WM, WN, KSUB, 0>(tag, al, bl, epi, CO, KP, ceil_div(M, GK), Z, 2.0 * M * CO * KP);
+        return;
+    }
     EpiSlabAcc epi{slab, CO, KP, (long)CO * KP, bslab};
     time_ks<FM, FN, WM, WN, KSUB, PIN>(tag, al, bl, epi, CO, KP, ceil_div(M, GK), Z, 2.0 * M * CO * KP);
 }
@@ -224,33 +238,21 @@ int main(int argc, char** argv) {
     if (want(tag)) conv_fwd<IH, CI, PAD, CO, FM, FN, WM, WN, KS, PIN>(tag, X, W, b, Y, S);
 #define G(tag, IH, CI, CO, Z, FM, FN, WM, WN, KS, PIN, VO) \
     if (want(tag)) conv_wgrad<IH, CI, CO, FM, FN, WM, WN, KS, PIN, VO>(tag, Y, X, slab, bsl, S, Z);
-    F("fwd6 abl0", 13, 192, 2, 192, 2, 6, 4, 2, 1, 0)
-    F("fwd6 abl3", 13, 192, 2, 192, 2, 6, 4, 2, 1, 3)
-    F("dg4 abl0", 22, 96, 0, 96, 4, 3, 4, 2, 1, 0)
-    F("dg4 abl3", 22, 96, 0, 96, 4, 3, 4, 2, 1, 3)
-    F("fwd2 abl0", 34, 48, 2, 48, 2, 3, 8, 1, 1, 0)
-    F("fwd2 abl3", 34, 48, 2, 48, 2, 3, 8, 1, 1, 3)
-    F("dg2 abl0", 36, 48, 0, 48, 2, 3, 8, 1, 1, 0)
-    F("dg2 abl3", 36, 48, 0, 48, 2, 3, 8, 1, 1, 3)
     G("wg6 abl0", 13, 192, 192, 256, 6, 3, 2, 2, 1, 0, 14)
-    G("wg6 abl3", 13, 192, 192, 256, 6, 3, 2, 2, 1, 3, 14)
-    G("wg6 abl6", 13, 192, 192, 256, 6, 3, 2, 2, 1, 6, 14)
-    G("wg6 abl7", 13, 192, 192, 256, 6, 3, 2, 2, 1, 7, 14)
+    G("wg6 abl9", 13, 192, 192, 256, 6, 3, 2, 2, 1, 9, 14)
     G("wg5 abl0", 11, 96, 192, 512, 6, 3, 2, 2, 1, 0, 0)
-    G("wg5 abl3", 11, 96, 192, 512, 6, 3, 2, 2, 1, 3, 0)
-    G("wg5 abl6", 11, 96, 192, 512, 6, 3, 2, 2, 1, 6, 0)
-    G("wg5 abl7", 11, 96, 192, 512, 6, 3, 2, 2, 1, 7, 0)
+    G("wg5 abl9", 11, 96, 192, 512, 6, 3, 2, 2, 1, 9, 0)
     G("wg4 abl0", 20, 96, 96, 1024, 3, 3, 2, 2, 1, 0, 0)
-    G("wg4 abl3", 20, 96, 96, 1024, 3, 3, 2, 2, 1, 3, 0)
-    G("wg4 abl6", 20, 96, 96, 1024, 3, 3, 2, 2, 1, 6, 0)
-    G("wg4 abl7", 20, 96, 96, 1024, 3, 3, 2, 2, 1, 7, 0)
-    G("wg3 abl0", 18, 48, 96, 2048, 3, 3, 2, 2, 1, 0, 0)
-    G("wg3 abl3", 18, 48, 96, 2048, 3, 3, 2, 2, 1, 3, 0)
-    G("wg3 abl6", 18, 48, 96, 2048, 3, 3, 2, 2, 1, 6, 0)
-    G("wg3 abl7", 18, 48, 96, 2048, 3, 3, 2, 2, 1, 7, 0)
+    G("wg4 abl9", 20, 96, 96, 1024, 3, 3, 2, 2, 1, 9, 0)
+    G("wg3 abl0", 18, 48, 96, 2048, 3, 3, 2, 1, 1, 0, 0)
+    G("wg3 abl9", 18, 48, 96, 2048, 3, 3, 2, 1, 1, 9, 0)
     G("wg2 abl0", 34, 48, 48, 4096, 3, 3, 1, 3, 1, 0, 0)
-    G("wg2 abl3", 34, 48, 48, 4096, 3, 3, 1, 3, 1, 3, 0)
-    G("wg2 abl6", 34, 48, 48, 4096, 3, 3, 1, 3, 1, 6, 0)
-    G("wg2 abl7", 34, 48, 48, 4096, 3, 3, 1, 3, 1, 7, 0)
+    G("wg2 abl9", 34, 48, 48, 4096, 3, 3, 1, 3, 1, 9, 0)
+    G("wg4 96x96 2w fm6", 20, 96, 96, 1024, 6, 3, 1, 2, 1, 0, 0)
+    G("wg4 96x192 4w fm6", 20, 96, 96, 1024, 6, 3, 1, 4, 1, 0, 0)
+    G("wg3 96x48 1w fm6", 18, 48, 96, 2048, 6, 3, 1, 1, 1, 0, 0)
+    G("wg3 96x144 3w fm6", 18, 48, 96, 2048, 6, 3, 1, 3, 1, 0, 0)
+    G("wg5 192x96 4w z256", 11, 96, 192, 256, 6, 3, 2, 2, 1, 0, 0)
+    G("wg5 96x96 2w", 11, 96, 192, 512, 6, 3, 1, 2, 1, 0, 0)
     return 0;
 }

@@ -230,7 +230,7 @@ static void conv_wgrad(const char* tag, const float* dz, const float* X, float* 
     constexpr int NT = 64 * WM * WN, BM = 16 * FM * WM, BN = 16 * FN * WN;
     constexpr int OFULL = IH + 2;
     using AL = RowsKM<BM, NT, (VO > 0 ? OFULL : 0), VO>;
-    using BL = Im2colKMo<IH, IH, CI, 2, BN, NT, 1, VO>;
+    using BL = Im2colKMo<IH, IH, CI, 2, BN, NT, 0, VO>;
     const int M = S * BL::OH * BL::OW;
     const int KP = 9 * CI;
     AL al;

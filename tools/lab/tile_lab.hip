@@ -196,6 +196,10 @@ static void conv_wgrad(const char* tag, const float* dz, const float* X, float* 
     using BL = Im2colKMo<IH, IH, CI, 2, BN, NT, 0, VO>;
     const int M = S * BL::OH * BL::OW;
     const int KP = 9 * CI;
+    if ((size_t)Z * CO * KP > (size_t)4096 * 48 * 432 || (size_t)Z * CO > (size_t)4096 * 192) {
+        printf("%-24s skipped: Z * CO * KP exceeds the lab's slab capacity\n", tag);
+        return;
+    }
     AL al;
     al.P = dz;
     al.ld = CO;
