@@ -49,12 +49,15 @@ struct SmallDiv {
 // WIN = true: output rows in max-pool window order, m = ((n * PH + ph) * PW + pw) * 4 + 2 dy + dx
 // with (oh, ow) = (2 ph + dy, 2 pw + dx); the floor-mode border rows/columns a 2x2 pool drops
 // are not computed at all (PerformantNet1 discards them: models.py:31,35,39).
-template <int IH, int IW, int CI, int PAD, int TR, int NT, bool WIN = false>
+// OHX > 0: output OHX x OHX instead of IH + 2 PAD - 2, i.e. taps past the bottom/right edge of X
+// read as zero (conv6's data gradient over the compact 14x14 dZ, whose 15th row/column would be
+// zero: the floor-mode pool never reads conv6's row/column 14).
+template <int IH, int IW, int CI, int PAD, int TR, int NT, bool WIN = false, int OHX = 0>
 struct Im2colKC {
     static constexpr int ROWS = TR;
     static constexpr bool KC = true;
-    static constexpr int OH = IH + 2 * PAD - 2;
-    static constexpr int OW = IW + 2 * PAD - 2;
+    static constexpr int OH = OHX > 0 ? OHX : IH + 2 * PAD - 2;
+    static constexpr int OW = OHX > 0 ? OHX : IW + 2 * PAD - 2;
     static constexpr int PH = OH / 2, PW = OW / 2;
     static constexpr int ROWS_PER_IMG = WIN ? 4 * PH * PW : OH * OW;
     static constexpr int TOTAL = ROWS * 4;

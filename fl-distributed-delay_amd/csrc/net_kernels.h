@@ -604,12 +604,13 @@ static int launch_gemm(const AL& al, const BL& bl, const EPI& epi, int M, int N,
 }
 
 // forward conv (also the data-gradient conv): out[m][n] for m < S*OH*OW, n < N
-template <int IH, int IW, int CI, int PAD, int FM, int FN, int WM, int WN, class EPI>
+// (OHX > 0: explicit output size, see Im2colKC)
+template <int IH, int IW, int CI, int PAD, int FM, int FN, int WM, int WN, class EPI, int OHX = 0>
 static int conv_like(const float* X, int S, const float* Wpk, int N, int KP, const EPI& epi,
                      hipStream_t st, int kid, int kreal) {
     constexpr int NT = 64 * WM * WN;
     constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
-    using AL = Im2colKC<IH, IW, CI, PAD, BM, NT>;
+    using AL = Im2colKC<IH, IW, CI, PAD, BM, NT, false, OHX>;
     using BL = RowsKC<BN, NT>;
     AL al;
     al.X = X;
@@ -624,14 +625,17 @@ static int conv_like(const float* X, int S, const float* Wpk, int N, int KP, con
 
 // weight gradient: slab[z][co][kk] += sum_p dz[p][co] * im2col(X)[p][kk]  (conv padding PAD)
 // VO > 0: only the top-left VO x VO window of the output pixels (dz is zero outside it)
-template <int IH, int IW, int CI, int PAD, int FM, int FN, int WM, int WN, int VO = 0>
+// DZC: dz is already stored compact over that window ([S][VO][VO][CO]), so its rows are the
+// reduction index as they stand
+template <int IH, int IW, int CI, int PAD, int FM, int FN, int WM, int WN, int VO = 0,
+          bool DZC = false>
 static int conv_wgrad(const float* dz, const float* X, int S, int CO, int KP, float* slab,
                       float* bslab, int Z, hipStream_t st, int kid, int kreal) {
     constexpr int NT = 64 * WM * WN;
     constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
     constexpr int OFULL = IH + 2 * PAD - 2;
     static_assert(IH == IW && VO <= OFULL, "square maps only");
-    using AL = RowsKM<BM, NT, (VO > 0 ? OFULL : 0), VO>;
+    using AL = RowsKM<BM, NT, (VO > 0 && !DZC ? OFULL : 0), (DZC ? 0 : VO)>;
     using BL = Im2colKM<IH, IW, CI, PAD, BN, NT, VO>;
     const int M = S * BL::OH * BL::OW;
     AL al;

@@ -320,13 +320,15 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC((linear_dgrad<4, 4, 2, 2>(w.dh1, theta + P_OFF[12], w.gy, w.d3, s25, S, 512, 9408, st,
                                  K_L1D)));
     // ---- pool3 backward -> dz6 (a6 buffer: conv6 fwd no longer writes it) ----
-    RC((pool_scatter<15, 15, 192, true>(w.gy, w.i3, w.a6, S, st)));
+    // Row/column 14 of conv6's 15x15 output is never pooled (floor mode), so its dz is zero: dz6
+    // is stored compact as [S][14][14][192].  The weight gradient then runs over those rows as
+    // they stand, and the data gradient reads the missing 15th row/column as zero padding.
+    RC((pool_scatter<14, 14, 192, true>(w.gy, w.i3, w.a6, S, st)));
     float* dz6 = w.a6;
     // ---- conv6: wgrad (input a5), bias, dgrad -> dz5 = . * (a5 > 0) into gx ----
-    // (row/column 14 of conv6's 15x15 output is never pooled: its dz is zero, skip those pixels)
-    RC((conv_wgrad<13, 13, 192, 2, 6, 3, 2, 2, 14>(dz6, w.a5, S, 192, 1728, g.sw[5], g.sb[5],
-                                                  GEO[5].ZW, st, K_WG6, 1728)));
-    RC((conv_like<15, 15, 192, 0, 2, 6, 4, 2>(dz6, S, g.wd[5], 192, 1728,
+    RC((conv_wgrad<13, 13, 192, 2, 6, 3, 2, 2, 14, true>(dz6, w.a5, S, 192, 1728, g.sw[5],
+                                                        g.sb[5], GEO[5].ZW, st, K_WG6, 1728)));
+    RC((conv_like<14, 14, 192, 0, 2, 6, 4, 2, EpiMask<true>, 13>(dz6, S, g.wd[5], 192, 1728,
         EpiMask<true>{w.gx, w.a5, S * 13 * 13, 192}, st, K_DG6, 1728)));
     float* dz5 = w.gx;
     // ---- conv5: wgrad (input d2), bias, dgrad -> grad wrt d2 (dropout site 2) into gy ----

@@ -13,6 +13,7 @@ struct EpiSlabAccNoSum : EpiSlabAcc {
 
 template <int FM, int FN, int WAVES_M, int WAVES_N, int KSUB, int PIN, class AL, class BL, class EPI>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N)
+__attribute__((amdgpu_waves_per_eu(PIN >= 10 ? PIN - 10 : 1)))
 gemm_ks(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, int tiles_m, int tiles_n) {
     constexpr int BM = 16 * FM * WAVES_M;
     constexpr int BN = 16 * FN * WAVES_N;
@@ -238,21 +239,26 @@ int main(int argc, char** argv) {
     if (want(tag)) conv_fwd<IH, CI, PAD, CO, FM, FN, WM, WN, KS, PIN>(tag, X, W, b, Y, S);
 #define G(tag, IH, CI, CO, Z, FM, FN, WM, WN, KS, PIN, VO) \
     if (want(tag)) conv_wgrad<IH, CI, CO, FM, FN, WM, WN, KS, PIN, VO>(tag, Y, X, slab, bsl, S, Z);
-    G("wg6 abl0", 13, 192, 192, 256, 6, 3, 2, 2, 1, 0, 14)
-    G("wg6 abl9", 13, 192, 192, 256, 6, 3, 2, 2, 1, 9, 14)
-    G("wg5 abl0", 11, 96, 192, 512, 6, 3, 2, 2, 1, 0, 0)
-    G("wg5 abl9", 11, 96, 192, 512, 6, 3, 2, 2, 1, 9, 0)
-    G("wg4 abl0", 20, 96, 96, 1024, 3, 3, 2, 2, 1, 0, 0)
-    G("wg4 abl9", 20, 96, 96, 1024, 3, 3, 2, 2, 1, 9, 0)
-    G("wg3 abl0", 18, 48, 96, 2048, 3, 3, 2, 1, 1, 0, 0)
-    G("wg3 abl9", 18, 48, 96, 2048, 3, 3, 2, 1, 1, 9, 0)
-    G("wg2 abl0", 34, 48, 48, 4096, 3, 3, 1, 3, 1, 0, 0)
-    G("wg2 abl9", 34, 48, 48, 4096, 3, 3, 1, 3, 1, 9, 0)
-    G("wg4 96x96 2w fm6", 20, 96, 96, 1024, 6, 3, 1, 2, 1, 0, 0)
-    G("wg4 96x192 4w fm6", 20, 96, 96, 1024, 6, 3, 1, 4, 1, 0, 0)
-    G("wg3 96x48 1w fm6", 18, 48, 96, 2048, 6, 3, 1, 1, 1, 0, 0)
-    G("wg3 96x144 3w fm6", 18, 48, 96, 2048, 6, 3, 1, 3, 1, 0, 0)
-    G("wg5 192x96 4w z256", 11, 96, 192, 256, 6, 3, 2, 2, 1, 0, 0)
-    G("wg5 96x96 2w", 11, 96, 192, 512, 6, 3, 1, 2, 1, 0, 0)
+    F("fwd6 wpe0", 13, 192, 2, 192, 2, 6, 4, 2, 1, 0)
+    F("fwd6 wpe15", 13, 192, 2, 192, 2, 6, 4, 2, 1, 15)
+    F("fwd6 wpe16", 13, 192, 2, 192, 2, 6, 4, 2, 1, 16)
+    F("dg4 wpe0", 22, 96, 0, 96, 4, 3, 4, 2, 1, 0)
+    F("dg4 wpe15", 22, 96, 0, 96, 4, 3, 4, 2, 1, 15)
+    F("dg4 wpe16", 22, 96, 0, 96, 4, 3, 4, 2, 1, 16)
+    G("wg6 wpe0", 13, 192, 192, 256, 6, 3, 2, 2, 1, 0, 14)
+    G("wg6 wpe14", 13, 192, 192, 256, 6, 3, 2, 2, 1, 14, 14)
+    G("wg6 wpe15", 13, 192, 192, 256, 6, 3, 2, 2, 1, 15, 14)
+    G("wg5 wpe0", 11, 96, 192, 512, 6, 3, 2, 2, 1, 0, 0)
+    G("wg5 wpe14", 11, 96, 192, 512, 6, 3, 2, 2, 1, 14, 0)
+    G("wg5 wpe15", 11, 96, 192, 512, 6, 3, 2, 2, 1, 15, 0)
+    G("wg4 wpe0", 20, 96, 96, 1024, 3, 3, 2, 2, 1, 0, 0)
+    G("wg4 wpe14", 20, 96, 96, 1024, 3, 3, 2, 2, 1, 14, 0)
+    G("wg4 wpe15", 20, 96, 96, 1024, 3, 3, 2, 2, 1, 15, 0)
+    G("wg2 wpe0", 34, 48, 48, 4096, 3, 3, 1, 3, 1, 0, 0)
+    G("wg2 wpe14", 34, 48, 48, 4096, 3, 3, 1, 3, 1, 14, 0)
+    G("wg2 wpe15", 34, 48, 48, 4096, 3, 3, 1, 3, 1, 15, 0)
+    G("wg3 wpe0", 18, 48, 96, 2048, 3, 3, 2, 1, 1, 0, 0)
+    G("wg3 wpe14", 18, 48, 96, 2048, 3, 3, 2, 1, 1, 14, 0)
+    G("wg3 wpe15", 18, 48, 96, 2048, 3, 3, 2, 1, 1, 15, 0)
     return 0;
 }

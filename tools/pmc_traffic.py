@@ -17,7 +17,8 @@ import sys
 
 FWD = {(32, 32, 4): 1, (34, 34, 48): 2, (18, 18, 48): 3, (20, 20, 96): 4, (11, 11, 96): 5,
        (13, 13, 192): 6}
-DGRAD = {(36, 36, 48): 2, (20, 20, 96): 3, (22, 22, 96): 4, (13, 13, 192): 5, (15, 15, 192): 6}
+DGRAD = {(36, 36, 48): 2, (20, 20, 96): 3, (22, 22, 96): 4, (13, 13, 192): 5, (15, 15, 192): 6,
+         (14, 14, 192): 6}
 
 
 def probe_name(kname):
