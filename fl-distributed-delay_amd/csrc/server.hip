@@ -75,7 +75,8 @@ __device__ __forceinline__ void adam_elem(const AdamConst& A, float s, float& p,
     v = vi;
 }
 
-// Program access.  The interpreter reads one word per op at a uniform address, so the words must
+// Program access.  The interpreter reads one macro word (two dwords) per step at a uniform address,
+// so the words must
 // come through the scalar cache: the reference-order program rides in the kernel arguments; a
 // general-order program is copied (device to device, stream-ordered, right before the launch)
 // into this constant-address-space buffer.  A plain global buffer would be read with vector loads
@@ -86,20 +87,24 @@ __constant__ int32_t g_casc_prog[CASC_CONST_WORDS];
 template <bool INL>
 struct ProgRef {
     const RuleProg& R;
-    __device__ __forceinline__ int32_t operator[](int i) const {
-        if constexpr (INL) return R.iprog[i];
-        else return g_casc_prog[i];
+    __device__ __forceinline__ uint32_t lo(int i) const {
+        if constexpr (INL) return (uint32_t)R.iprog[2 * i];
+        else return (uint32_t)g_casc_prog[2 * i];
+    }
+    __device__ __forceinline__ uint32_t hi(int i) const {
+        if constexpr (INL) return (uint32_t)R.iprog[2 * i + 1];
+        else return (uint32_t)g_casc_prog[2 * i + 1];
     }
 };
 
 // stage a general-order program into g_casc_prog on `stream` (no-op for inline programs)
 static int stage_program(const RuleProg& R, hipStream_t stream) {
     if (R.prog == nullptr) return 0;
-    FLSIM_REQUIRE(R.info.len + CASC_PAD <= CASC_CONST_WORDS, "rule program of %d words (max %d)",
-                  R.info.len, CASC_CONST_WORDS - CASC_PAD);
+    FLSIM_REQUIRE(2 * (R.info.len + 1) <= CASC_CONST_WORDS, "rule program of %d macro words (max %d)",
+                  R.info.len, CASC_CONST_WORDS / 2 - 1);
     static void* dst = nullptr;
     if (!dst) FLSIM_CHECK_HIP(hipGetSymbolAddress(&dst, HIP_SYMBOL(g_casc_prog)));
-    FLSIM_CHECK_HIP(hipMemcpyAsync(dst, R.prog, (size_t)(R.info.len + CASC_PAD) * 4,
+    FLSIM_CHECK_HIP(hipMemcpyAsync(dst, R.prog, (size_t)(R.info.len + 1) * 8,
                                    hipMemcpyDeviceToDevice, stream));
     return 0;
 }
@@ -160,8 +165,8 @@ __global__ void __launch_bounds__(256) k_agg_stream(AggArgs A) {
         const CascVals<float> cv = casc_values(x, A.R.info.need, A.R.info.lp);
         const bool tail = in_tail(A, e);
         float s = 0.f;
-        if (!tail) s = casc_run<INL ? 1 : CASC_PAD>(prog, 0, cv, yf);
-        if (tail) s = casc_run<INL ? 1 : CASC_PAD>(prog, A.R.info.tail_off, cv, yf);
+        if (!tail) s = casc_run_macro(prog, 0, cv, yf);
+        if (tail) s = casc_run_macro(prog, A.R.info.tail_off, cv, yf);
         adam_elem(A.ac, s, p, m, v);
         A.p[e] = p;
         A.m[e] = m;
@@ -190,7 +195,7 @@ __global__ void __launch_bounds__(256) k_agg_stream(AggArgs A) {
         if (q < NYR) return ys_lds[q * 256 + tid];
         return A.R.arr[q] ? ld(A.R.arr[q] + e0) : f32x4{0.f, 0.f, 0.f, 0.f};
     };
-    const f32x4 sum = casc_run<INL ? 1 : CASC_PAD, true>(
+    const f32x4 sum = casc_run_macro<true>(
         prog, 0, casc_values(x, A.R.info.need, A.R.info.lp), yf);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -217,6 +222,7 @@ struct StepArgs {
     float* v;
     int nseg, units;
     int u_lo;                       // first unit of this launch (block b runs unit u_lo + b)
+    int il_lo, il_w, il_n;          // interleave units [il_lo, il_lo + il_n): il_w wide, then conv
     AdamConst ac;
     RuleProg R;
     SlabSeg seg[STEP_MAX_SEG];
@@ -226,6 +232,9 @@ static_assert(sizeof(StepArgs) <= 4096, "kernel argument block");
 // LDS map (ONE __shared__ array, cdna_hip_programming.md §5 item 4(a)): z-lane partials f32x4[256]
 // at 0, the tile's 256 sums at 1024, the last-arriver flag at 1280, staged entry arrays at 1536
 constexpr int L_RED = 0, L_SUM = 1024, L_FLAG = 1280, L_Y = 1536;
+// general-order tiles also stage x, p, m, v for the one-wave interpreter
+constexpr int L_S = L_Y + NYR * 256, L_P = L_S + 256, L_M = L_P + 256, L_V = L_M + 256,
+              L_END = L_V + 256;
 
 // one unit's z-range of 256 slab columns -> this thread's column sum (thread t owns column t)
 __device__ __forceinline__ float reduce_cols(const float* slab, const SlabSeg& g, int tile, int z0,
@@ -356,7 +365,11 @@ __device__ __forceinline__ void slab_step_wide(const StepArgs& A, const SlabSeg&
             m = ld(A.m + e);
             v = ld(A.v + e);
         };
-        if (ADAM && valid && g.nz == 1) load_param_side();
+        // reference order: the parameter side is loaded ahead of the slab rows (both round trips
+        // overlap); general order: after them, so the registers are free during the reduction and
+        // more waves fit (the interpreter that follows hides the exposed load behind the other
+        // resident waves)
+        if (ADAM && INL && valid && g.nz == 1) load_param_side();
         f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
         if (valid) {
             const float* pz = slab + c;
@@ -389,6 +402,7 @@ __device__ __forceinline__ void slab_step_wide(const StepArgs& A, const SlabSeg&
         a0 += a1;
         a0 += a2;
         a0 += a3;
+        if (ADAM && !INL && valid && g.nz == 1) load_param_side();
         if (g.nz > 1) {
             // the conv path's hand-off with 1024 floats per unit (sc1 stores / loads)
             float* part = A.base + A.part_off;
@@ -423,16 +437,22 @@ __device__ __forceinline__ void slab_step_wide(const StepArgs& A, const SlabSeg&
         if (A.S_out) *reinterpret_cast<f32x4*>(A.S_out + e) = a0;
         if constexpr (ADAM) {
             auto yf = [&](int q) -> f32x4 {
-                // q is uniform: a scalar branch chain picks the register, no indexed access
-                f32x4 r = f32x4{0.f, 0.f, 0.f, 0.f};
-                bool hit = false;
-#pragma unroll
-                for (int k = 0; k < NYW; ++k)
-                    if (q == k) { r = ys[k]; hit = true; }
-                if (!hit && A.R.arr[q]) r = ld(A.R.arr[q] + e);
-                return r;
+                // q is uniform: a scalar switch picks the register, no indexed access
+                static_assert(NYW == 8, "one case per register-held entry array");
+                switch (q) {
+                    case 0: return ys[0];
+                    case 1: return ys[1];
+                    case 2: return ys[2];
+                    case 3: return ys[3];
+                    case 4: return ys[4];
+                    case 5: return ys[5];
+                    case 6: return ys[6];
+                    case 7: return ys[7];
+                    default:
+                        return A.R.arr[q] ? ld(A.R.arr[q] + e) : f32x4{0.f, 0.f, 0.f, 0.f};
+                }
             };
-            const f32x4 sum = casc_run<INL ? 1 : CASC_PAD, true>(
+            const f32x4 sum = casc_run_macro<true>(
                 prog, 0, casc_values(a0, A.R.info.need, A.R.info.lp), yf);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -455,8 +475,7 @@ __device__ __forceinline__ void slab_step_wide(const StepArgs& A, const SlabSeg&
 // parameter-side loads (p, m, v, staged entry arrays) are issued before the slab reduction (whole
 // tiles) or together with the partial loads (split tiles), so the two memory round trips overlap.
 template <bool ADAM, bool INL>
-__global__ void __launch_bounds__(256) k_slab_step(StepArgs A) {
-    __shared__ float lds[L_Y + NYR * 256];
+__device__ __forceinline__ void slab_step_body(const StepArgs& A, float* lds) {
     const int tid = threadIdx.x;
     // runs of XG consecutive units (a tile's z-units, neighbouring tiles: one parameter region)
     // share an XCD (blocks b and b + 8 do), the runs themselves go round-robin over the XCDs so
@@ -466,8 +485,15 @@ __global__ void __launch_bounds__(256) k_slab_step(StepArgs A) {
     const int b = (int)blockIdx.x;
     const int nfull = nb / (8 * XG) * (8 * XG);
     const int lb = b < nfull ? ((b >> 3) / XG * 8 + (b & 7)) * XG + (b >> 3) % XG : b;
-    const int u = A.u_lo + lb;
+    int u = A.u_lo + lb;
     if (u >= A.units) return;
+    if (u >= A.il_lo && A.il_n > 0) {
+        // position i of the interleaved run: wide unit f(i) when f steps, else conv unit i - f(i),
+        // f(i) = floor(i * W / N) (the wide units spread evenly over the run)
+        const long i = u - A.il_lo;
+        const long f0 = i * A.il_w / A.il_n, f1 = (i + 1) * A.il_w / A.il_n;
+        u = A.il_lo + (f1 > f0 ? (int)f0 : A.il_w + (int)(i - f0));
+    }
     int si = 0;
     while (si + 1 < A.nseg && A.seg[si + 1].unit0 <= u) ++si;
     const SlabSeg& g = A.seg[si];
@@ -546,8 +572,52 @@ __global__ void __launch_bounds__(256) k_slab_step(StepArgs A) {
             }
             if (tid == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        if constexpr (ADAM && !INL) {
+            // general order: the tile's 256 elements go through the program as float4 lanes of
+            // ONE wave (a quarter of the interpreter's scalar work per element); the tile is
+            // staged in LDS (x, p, m, v, entry arrays) and written back by its owning threads.
+            // Tiles holding row_sum tail elements, or more arrays than NYR, take the per-element
+            // path below.
+            if (valid && A.S_out) A.S_out[e] = s;
+            const bool tail = valid && tl >= (long)(g.numel / 32) * 32;
+            lds[L_S + tid] = valid ? s : 0.f;
+            lds[L_P + tid] = p;
+            lds[L_M + tid] = m;
+            lds[L_V + tid] = v;
+#pragma unroll
+            for (int q = 0; q < NYR; ++q)
+                if (q < nst) lds[L_Y + q * 256 + tid] = valid ? ys[q] : 0.f;
+            if (!__syncthreads_or(tail) && A.R.narr <= NYR) {
+                if (tid < 64) {
+                    const f32x4* l4 = reinterpret_cast<const f32x4*>(lds);
+                    auto yf4 = [&](int q) -> f32x4 { return l4[(L_Y + q * 256) / 4 + tid]; };
+                    const f32x4 sum = casc_run_macro<true>(
+                        prog, 0, casc_values(l4[L_S / 4 + tid], A.R.info.need, A.R.info.lp), yf4);
+                    f32x4 pp = l4[L_P / 4 + tid], mm = l4[L_M / 4 + tid], vv = l4[L_V / 4 + tid];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        float p1 = pp[k], m1 = mm[k], v1 = vv[k];
+                        adam_elem(A.ac, sum[k], p1, m1, v1);
+                        pp[k] = p1;
+                        mm[k] = m1;
+                        vv[k] = v1;
+                    }
+                    f32x4* w4 = reinterpret_cast<f32x4*>(lds);
+                    w4[L_P / 4 + tid] = pp;
+                    w4[L_M / 4 + tid] = mm;
+                    w4[L_V / 4 + tid] = vv;
+                }
+                __syncthreads();
+                if (valid) {
+                    A.p[e] = lds[L_P + tid];
+                    A.m[e] = lds[L_M + tid];
+                    A.v[e] = lds[L_V + tid];
+                }
+                continue;
+            }
+        }
         if (!valid) continue;
-        if (A.S_out) A.S_out[e] = s;
+        if (A.S_out && (INL || !ADAM)) A.S_out[e] = s;
         if constexpr (ADAM) {
 #pragma unroll
             for (int q = 0; q < NYR; ++q)
@@ -559,14 +629,31 @@ __global__ void __launch_bounds__(256) k_slab_step(StepArgs A) {
             const CascVals<float> cv = casc_values(s, A.R.info.need, A.R.info.lp);
             const bool tail = tl >= (long)(g.numel / 32) * 32;
             float sum = 0.f;
-            if (!tail) sum = casc_run<INL ? 1 : CASC_PAD>(prog, 0, cv, yf);
-            if (tail) sum = casc_run<INL ? 1 : CASC_PAD>(prog, A.R.info.tail_off, cv, yf);
+            if (!tail) sum = casc_run_macro(prog, 0, cv, yf);
+            if (tail) sum = casc_run_macro(prog, A.R.info.tail_off, cv, yf);
             adam_elem(A.ac, sum, p, m, v);
             A.p[e] = p;
             A.m[e] = m;
             A.v[e] = v;
         }
     }
+}
+
+template <bool ADAM, bool INL>
+__global__ void __launch_bounds__(256) k_slab_step(StepArgs A) {
+    __shared__ float lds[L_Y + NYR * 256];
+    slab_step_body<ADAM, INL>(A, lds);
+}
+
+// General-order programs: the interpreter's chains of dependent adds want many resident waves to
+// hide their latency, so this instantiation is held to SEQ_WAVES waves per SIMD (register budget)
+#ifndef SEQ_WAVES
+#define SEQ_WAVES 4
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEQ_WAVES, 8)))
+k_slab_step_seq(StepArgs A) {
+    __shared__ float lds[L_END];
+    slab_step_body<true, false>(A, lds);
 }
 
 // ================================================================================================
@@ -620,9 +707,13 @@ int make_rule(const flsim_rule* r, RuleProg* R) {
             pos[q] = r->c + q;
             arr[q] = q;
         }
-        const int len = build_cascade_program(k, pos, arr, r->n_arrays, R->iprog, RULE_INL_PROG,
-                                              &R->info);
+        int32_t ops[RULE_INL_PROG];
+        CascInfo oi;
+        int len = build_cascade_program(k, pos, arr, r->n_arrays, ops, RULE_INL_PROG, &oi);
         FLSIM_REQUIRE(len > 0, "rule program for k = %d entries failed (%d)", k, len);
+        len = build_macro_program(ops, oi, reinterpret_cast<uint32_t*>(R->iprog),
+                                  RULE_INL_PROG / 2, &R->info);
+        FLSIM_REQUIRE(len > 0, "rule macro program for k = %d entries failed (%d)", k, len);
         R->prog = nullptr;
     } else {
         R->prog = r->prog;
@@ -656,13 +747,21 @@ int slab_step_launch(float* gradstate, const StepPlan& plan, long cnt_off, long 
     // segments, so every split tile completes and resets its counter
     A.u_lo = 0;
     int u_hi = plan.units;
+    // general order only: interleave the wide and conv units (measured: reference order and
+    // reduce-only steps are faster in plan order, profiles/r02f/step_bench_*.txt)
+    A.il_lo = plan.u_wide;
+    A.il_w = plan.u_conv - plan.u_wide;
+    A.il_n = (rule && rule->prog != nullptr) ? plan.units - plan.u_wide : 0;
     if (const char* env = getenv("FLSIM_STEP_UNITS")) {
         int lo = 0, hi = 0;
         if (sscanf(env, "%d,%d", &lo, &hi) == 2 && 0 <= lo && lo < hi && hi <= plan.units) {
             A.u_lo = lo;
             u_hi = hi;
+            A.il_n = 0;             // measurement of a unit range: plan order, no interleave
         }
     }
+    if (const char* env = getenv("FLSIM_STEP_NO_INTERLEAVE"))
+        if (atoi(env)) A.il_n = 0;
     const unsigned nblk = (unsigned)(u_hi - A.u_lo);
     // algorithmic HBM bytes: every slab byte once; S_out written; p, m, v read + written; each
     // distinct entry array read once
@@ -677,7 +776,7 @@ int slab_step_launch(float* gradstate, const StepPlan& plan, long cnt_off, long 
                               ps.stop, 0, A);
     } else {
         RC(stage_program(*rule, stream));
-        hipExtLaunchKernelGGL(k_slab_step<true, false>, dim3(nblk), dim3(256), 0, stream, ps.start,
+        hipExtLaunchKernelGGL(k_slab_step_seq, dim3(nblk), dim3(256), 0, stream, ps.start,
                               ps.stop, 0, A);
     }
     FLSIM_LAUNCH_CHECK();
@@ -807,34 +906,46 @@ int flsim_aggregate_adam_sum(const float* S, int k, float* p, float* m, float* v
 }
 
 // host: rule()'s summation program for k entries with the non-S entries at pos[] (increasing)
-// holding array arr[]; info[4] = {len, tail_off, need, lp}.  Returns 0 or 1 (bad input / cap).
+// holding array arr[], in the device's macro-word form (cascade.h): prog[cap] int32 = pairs (lo,
+// hi) + one fetch-pad pair; info[4] = {pairs, pair index of the row_sum part, need, lp}.
 int flsim_cascade_program(int k, const int32_t* pos, const int32_t* arr, int n_events,
                           int32_t* prog, int cap, int32_t* info) {
     FLSIM_REQUIRE(prog && info && (n_events == 0 || (pos && arr)), "null pointer");
+    FLSIM_REQUIRE(n_events >= 0 && n_events <= CASC_MAX_K, "n_events = %d", n_events);
+    const int ocap = 72 + 40 * (n_events + 8);
+    int32_t* ops = new int32_t[ocap];
     CascInfo ci{};
-    const int len = build_cascade_program(k, pos, arr, n_events, prog, cap, &ci);
+    int len = build_cascade_program(k, pos, arr, n_events, ops, ocap, &ci);
+    CascInfo mi{};
+    if (len > 0) len = build_macro_program(ops, ci, reinterpret_cast<uint32_t*>(prog), cap / 2, &mi);
+    delete[] ops;
     FLSIM_REQUIRE(len != -3, "k = %d entries: supported 1 .. %d", k, CASC_MAX_K);
     FLSIM_REQUIRE(len != -1, "events must have increasing positions in [0, k) and arrays >= 0");
-    FLSIM_REQUIRE(len != -2, "program longer than %d words", cap);
-    info[0] = ci.len;
-    info[1] = ci.tail_off;
-    info[2] = ci.need;
-    info[3] = ci.lp;
+    FLSIM_REQUIRE(len > 0, "program longer than %d words (or an array index past 63)", cap);
+    info[0] = mi.len;
+    info[1] = mi.tail_off;
+    info[2] = mi.need;
+    info[3] = mi.lp;
     return 0;
 }
 
-// host interpreter of a program (testing): out[e] = the cascade sum of element e, x = S[e],
+// host interpreter of a macro program (testing): out[e] = the cascade sum of element e, x = S[e],
 // entry arrays ys[q][e]; tail[e] != 0 selects the row_sum program
 int flsim_cascade_eval_host(const int32_t* prog, const int32_t* info, const float* S,
                             const float* const* ys, int n_arrays, const uint8_t* tail, long n,
                             float* out) {
     FLSIM_REQUIRE(prog && info && S && out, "null pointer");
+    struct HostPairs {
+        const int32_t* w;
+        uint32_t lo(int i) const { return (uint32_t)w[2 * i]; }
+        uint32_t hi(int i) const { return (uint32_t)w[2 * i + 1]; }
+    } hp{prog};
     for (long e = 0; e < n; ++e) {
         const CascVals<float> cv = casc_values(S[e], info[2], info[3]);
         auto yf = [&](int q) -> float {
             return (q < n_arrays && ys[q]) ? ys[q][e] : 0.f;
         };
-        out[e] = casc_run<CASC_PAD>(prog, (tail && tail[e]) ? info[1] : 0, cv, yf);
+        out[e] = casc_run_macro(hp, (tail && tail[e]) ? info[1] : 0, cv, yf);
     }
     return 0;
 }

@@ -48,6 +48,7 @@ struct StepPlan {
     SlabSeg seg[STEP_MAX_SEG];
     int nseg, units, ctiles;
     long slab_floats;     // sum of Z * n (the slab bytes the step streams / 4)
+    int u_wide, u_conv;   // first unit of the wide (class 1) and packed conv (class 2) segments
 };
 
 // wide (float4) tiles: identity layout, 16-B aligned, no row_sum tail, a real weight matrix
@@ -56,8 +57,10 @@ inline bool seg_wide(const SegSpec& s) {
 }
 
 // Dispatch order of the units: small tensors first (biases, the head, conv1: few units, each a
-// long serial z-reduction), then the wide segments (the linear layers: many short units), then
-// the packed conv segments (uniform 256 KB streaming units), so the launch ends on uniform work.
+// long serial z-reduction), then the wide segments (the linear layers: many short units) and the
+// packed conv segments (uniform 256 KB streaming units) interleaved in proportion (the kernel
+// maps block positions onto the two runs), so the units that carry most of the rule() program's
+// arithmetic (the linear layers' elements) run beside the ones that carry most of the slab bytes.
 inline int seg_class(const SegSpec& s) { return s.n < 4096 ? 0 : (seg_wide(s) ? 1 : 2); }
 
 inline int plan_step(const SegSpec* s_in, int nseg, StepPlan* P) {
@@ -70,8 +73,11 @@ inline int plan_step(const SegSpec* s_in, int nseg, StepPlan* P) {
     P->nseg = nseg;
     int u = 0, ct = 0;
     long sf = 0;
+    P->u_wide = P->u_conv = -1;
     for (int i = 0; i < nseg; ++i) {
         SlabSeg& g = P->seg[i];
+        if (P->u_wide < 0 && seg_class(s[i]) >= 1) P->u_wide = u;
+        if (P->u_conv < 0 && seg_class(s[i]) == 2) P->u_conv = u;
         g.slab_off = s[i].slab_off;
         g.Z = s[i].Z;
         g.n = (int)s[i].n;
@@ -110,6 +116,8 @@ inline int plan_step(const SegSpec* s_in, int nseg, StepPlan* P) {
         sf += (long)s[i].Z * s[i].n;
     }
     P->units = u;
+    if (P->u_wide < 0) P->u_wide = u;
+    if (P->u_conv < 0) P->u_conv = u;
     P->ctiles = ct;
     P->slab_floats = sf;
     return 0;

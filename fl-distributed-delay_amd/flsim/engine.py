@@ -308,18 +308,18 @@ def aggregate_adam_sum(S, k, theta, m, v, step, sizes, lr=1e-3, betas=(0.9, 0.99
 def cascade_program(k, events):
     """rule()'s summation program (host, flsim_cascade_program) for k entries whose non-S_t
     entries are events = [(position, array index)] (positions increasing).  -> (int32 words,
-    info[4])."""
+    info[4]).  The words are the device's macro form (csrc/cascade.h): (lo, hi) pairs."""
     ev = np.asarray(events, np.int32).reshape(-1, 2)
     pos = np.ascontiguousarray(ev[:, 0])
     arr = np.ascontiguousarray(ev[:, 1])
-    cap = 72 + 40 * (len(ev) + 8)          # + the interpreter's fetch padding (CASC_PAD)
+    cap = 2 * (72 + 40 * (len(ev) + 8))    # macro pairs (lo, hi) + the fetch-pad pair
     prog = np.zeros(cap, np.int32)
     info = np.zeros(4, np.int32)
     vp = ctypes.c_void_p
     check(lib().flsim_cascade_program(int(k), pos.ctypes.data_as(vp), arr.ctypes.data_as(vp),
                                       len(ev), prog.ctypes.data_as(vp), cap,
                                       info.ctypes.data_as(vp)))
-    return prog[:info[0] + 8].copy(), info      # with the 8 padding words
+    return prog[:2 * (info[0] + 1)].copy(), info      # with the padding pair
 
 
 class Rule:

@@ -79,8 +79,10 @@ def test_program_is_compact():
     words, so it fits the kernel arguments (RULE_INL_PROG = 192)."""
     from flsim.engine import cascade_program
     words, info = cascade_program(1024, [(1023, 0)])
-    assert info[0] + 8 == len(words) and info[0] < 184    # + the fetch padding
+    assert 2 * (info[0] + 1) == len(words) and info[0] < 96 - 1   # pairs + the fetch-pad pair
     assert info[3] == 4
+    words, info = cascade_program(8100, [(p, p % 6) for p in range(50, 8100, 113)])
+    assert info[1] <= 2 * 72           # main part: one or two macro words per stale entry
 
 
 def test_program_errors():

@@ -2,7 +2,8 @@
 the whole plan and each segment alone (FLSIM_STEP_UNITS), reduce-only and with rule() + Adam.
 
   python tools/step_bench.py
-Prints per segment: units, slab MB, time (us), algorithmic GB/s.
+Prints per segment: units, slab MB, time (us), algorithmic GB/s.  Modes: ref (reference order,
+k = 513), seq (k = 8100 with 72 stale entries among 6 arrays), c3 [T] (configs[3]'s epoch T).
 """
 import os
 import sys
@@ -78,6 +79,25 @@ def main():
         ev = list(zip(pos.tolist(), rs.randint(0, 6, 72).tolist()))
         rule = Rule(8100, arrs, events=ev, stager=ProgramStager(dev))
         print("seq program words", int(rule.c_rule.info[0]))
+    elif mode == "c3":         # configs[3]'s own programs: the heterogeneous schedule's epoch T
+        import numpy as np
+        from flsim.engine import ProgramStager
+        from flsim.schedule import Schedule, heterogeneous_delays
+        T = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+        n = 16384
+        sch = Schedule(n, heterogeneous_delays(n), True)
+        for _ in range(T + 1):
+            plan_t = sch.next_epoch()
+        fast = np.nonzero(plan_t.fast)[0]
+        sw = np.asarray([w for (w, _) in plan_t.stale])
+        pos = np.searchsorted(fast, sw) + np.arange(len(sw))
+        srcs = sorted({src for (_, src) in plan_t.stale})
+        arr = [srcs.index(src) for (_, src) in plan_t.stale]
+        arrs = [torch.randn(P + 64, device=dev) * 1e-3 for _ in srcs]
+        rule = Rule(plan_t.c_t + plan_t.s_t, arrs, events=list(zip(pos.tolist(), arr)),
+                    stager=ProgramStager(dev))
+        print(f"configs[3] epoch {T}: k {plan_t.c_t + plan_t.s_t}, {len(arr)} stale entries, "
+              f"{len(srcs)} arrays, {int(rule.c_rule.info[0])} macro words")
     else:
         rule = Rule(513, [stale], c=512)
 
@@ -98,6 +118,10 @@ def main():
     print(f"plan: {total} units, slabs {slab / 1e6:.1f} MB")
     print(f"FULL reduce-only {full_red:8.1f} us  {(slab + 4 * P) / full_red / 1e3:7.1f} GB/s")
     print(f"FULL step        {full_step:8.1f} us  {(slab + 4 * P * 7) / full_step / 1e3:7.1f} GB/s")
+    os.environ["FLSIM_STEP_NO_INTERLEAVE"] = "1"
+    t = timeit(lambda: eng.server_step(None, rule, theta, m, v, 5))
+    os.environ.pop("FLSIM_STEP_NO_INTERLEAVE")
+    print(f"FULL step, plan order (no interleave) {t:8.1f} us")
     for name, u0, u1, sb, numel in segs:
         os.environ["FLSIM_STEP_UNITS"] = f"{u0},{u1}"
         t = timeit(lambda: eng.server_step(None, rule, theta, m, v, 5))
