@@ -53,6 +53,15 @@ template <> struct Lane<float> {
     __device__ static float ld(const float* p) { return __builtin_nontemporal_load(p); }
     __device__ static void st(float* p, float v) { __builtin_nontemporal_store(v, p); }
 };
+template <> struct Lane<f32x4> {
+    static constexpr int EPL = 4;
+    __device__ static f32x4 ld(const float* p) {
+        return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+    }
+    __device__ static void st(float* p, f32x4 v) {
+        __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+    }
+};
 template <int W> struct Lane<vecw<W>> {
     static constexpr int EPL = 4 * W;
     __device__ static vecw<W> ld(const float* p) {
@@ -190,7 +199,8 @@ int main() {
     run<vecw<1>, 0, true>("ops   epl 4", A, want, hout.data());
     run<vecw<2>, 0, true>("ops   epl 8", A, want, hout.data());
     run<float, 1, true>("macro epl 1", A, want, hout.data());
-    run<vecw<1>, 1, true>("macro epl 4", A, want, hout.data());
+    run<vecw<1>, 1, true>("macro epl 4 (vecw)", A, want, hout.data());
+    run<f32x4, 1, true>("macro epl 4 (f32x4)", A, want, hout.data());
     run<vecw<2>, 1, true>("macro epl 8", A, want, hout.data());
     run<vecw<4>, 1, true>("macro epl 16", A, want, hout.data());
     return 0;
