@@ -22,6 +22,8 @@ DGRAD = {(36, 36, 48): 2, (20, 20, 96): 3, (22, 22, 96): 4, (13, 13, 192): 5, (1
 
 
 def probe_name(kname):
+    if "k_slab_step_seq" in kname:
+        return "slab_step_seq"
     m = re.search(r"k_slab_step<(true|false), (true|false)>", kname)
     if m:
         if m.group(1) == "false":
