@@ -197,11 +197,13 @@ typedef struct flsim_rule {
 } flsim_rule;
 
 /* host: the summation program of rule() over k entries whose non-S_t entries sit at positions
- * pos[0 .. n_events) (increasing) and hold arrays arr[] (indices into flsim_rule.arrays);
- * info[4] = {length, row_sum offset, flags, level power}.  k <= 524288. */
+ * pos[0 .. n_events) (increasing) and hold arrays arr[] (indices into flsim_rule.arrays; at most
+ * 64), in the device's macro-word form: prog[0 .. cap) receives (lo, hi) int32 pairs plus one
+ * padding pair; info[4] = {pairs, pair index of the row_sum part, flags, level power}.
+ * k <= 524288. */
 int flsim_cascade_program(int k, const int32_t* pos, const int32_t* arr, int n_events,
                           int32_t* prog, int cap, int32_t* info);
-/* host (testing): run a program on the host, out[e] = cascade sum for element e (x = S[e],
+/* host (testing): run a macro program on the host, out[e] = cascade sum for element e (x = S[e],
  * entry arrays ys[q][e]; tail[e] != 0 selects the row_sum part) */
 int flsim_cascade_eval_host(const int32_t* prog, const int32_t* info, const float* S,
                             const float* const* ys, int n_arrays, const uint8_t* tail, long n,
