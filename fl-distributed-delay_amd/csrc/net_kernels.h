@@ -603,6 +603,26 @@ static int launch_gemm(const AL& al, const BL& bl, const EPI& epi, int M, int N,
     return probe_end(ps, kid, alg_flops);
 }
 
+// Splits of a slab-accumulating GEMM (weight gradients: the reduction runs over the chunk's
+// pixels or samples).  The slab has Z rows; a small chunk (configs[1]: 5 workers = 640 samples)
+// would leave each split a handful of k-steps, so the per-block prologue and the slab
+// read-modify-write dominate.  Such launches use only the first max(ceil(ksteps / KMIN),
+// ceil(1024 / tiles)) rows (>= 32 k-steps per split, >= 1024 blocks); the other rows keep what
+// earlier chunks accumulated, and the epoch's slab sum reads every row.  KMIN = 32 measured on
+// n = 10: 617 -> 645 worker-steps/s, headline unchanged (profiles/r02f/wsplit.txt).
+static int wsplit(int ksteps, int Z, int tiles) {
+    static int kmin = -1;
+    if (kmin < 0) {
+        const char* e = getenv("FLSIM_WSPLIT_KMIN");     // measurement override (0: always Z)
+        kmin = e ? atoi(e) : 32;
+    }
+    if (kmin <= 0) return Z;
+    int z = (ksteps + kmin - 1) / kmin;
+    const int zb = (1024 + tiles - 1) / tiles;
+    if (z < zb) z = zb;
+    return z < Z ? z : Z;
+}
+
 // forward conv (also the data-gradient conv): out[m][n] for m < S*OH*OW, n < N
 // (OHX > 0: explicit output size, see Im2colKC)
 template <int IH, int IW, int CI, int PAD, int FM, int FN, int WM, int WN, class EPI, int OHX = 0>
@@ -647,7 +667,9 @@ static int conv_wgrad(const float* dz, const float* X, int S, int CO, int KP, fl
     bl.X = X;
     bl.M = M;
     EpiSlabAcc epi{slab, CO, KP, (long)CO * KP, bslab};
-    return launch_gemm<FM, FN, WM, WN>(al, bl, epi, CO, KP, ceil_div(M, GK), Z, st, kid,
+    const int tiles = ceil_div(CO, BM) * ceil_div(KP, BN);
+    return launch_gemm<FM, FN, WM, WN>(al, bl, epi, CO, KP, ceil_div(M, GK),
+                                       wsplit(ceil_div(M, GK), Z, tiles), st, kid,
                                        2.0 * M * CO * kreal);
 }
 
@@ -698,7 +720,9 @@ static int linear_wgrad(const float* dy, const float* x, float* slab, float* bsl
     RowsKM<16 * FN * WN, NT> bl{};
     bl.P = x; bl.ld = K; bl.NK = S; bl.NC = K;
     EpiSlabAcc epi{slab, N, K, (long)N * K, bslab};
-    return launch_gemm<FM, FN, WM, WN>(al, bl, epi, N, K, ceil_div(S, GK), Z, st, kid,
+    const int tiles = ceil_div(N, 16 * FM * WM) * ceil_div(K, 16 * FN * WN);
+    return launch_gemm<FM, FN, WM, WN>(al, bl, epi, N, K, ceil_div(S, GK),
+                                       wsplit(ceil_div(S, GK), Z, tiles), st, kid,
                                        2.0 * S * N * K);
 }
 
