@@ -483,21 +483,32 @@ struct EpiDropMask {
 
 // split-K partial slab, accumulated across chunks: S[z][m][n] += acc   (one owner per element);
 // with Bsl != nullptr also the bias gradient Bsl[z][m] += column sum of the dZ tile (ASUM)
+// zinit: slab rows z >= zinit have not been written yet this epoch (begin_epoch does not clear
+// the slabs): those blocks store instead of accumulating
 struct EpiSlabAcc {
     static constexpr bool ASUM = true;
     float* S;
     int M, N;
     long zstride;
     float* Bsl;
+    int zinit = 0x7fffffff;
     __device__ void asum(int m, int z, float v) const {
-        if (Bsl && m < M) Bsl[(long)z * M + m] += v;
+        if (!Bsl || m >= M) return;
+        if (z < zinit) Bsl[(long)z * M + m] += v;
+        else Bsl[(long)z * M + m] = v;
     }
     __device__ void apply4(int m, int n, int z, f32x4 v) const {
         if (n >= N) return;
         float* base = S + z * zstride;
+        if (z < zinit) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-            if (m + r < M) base[(long)(m + r) * N + n] += v[r];
+            for (int r = 0; r < 4; ++r)
+                if (m + r < M) base[(long)(m + r) * N + n] += v[r];
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (m + r < M) base[(long)(m + r) * N + n] = v[r];
+        }
     }
 };
 

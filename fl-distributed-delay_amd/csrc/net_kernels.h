@@ -650,7 +650,8 @@ static int conv_like(const float* X, int S, const float* Wpk, int N, int KP, con
 template <int IH, int IW, int CI, int PAD, int FM, int FN, int WM, int WN, int VO = 0,
           bool DZC = false>
 static int conv_wgrad(const float* dz, const float* X, int S, int CO, int KP, float* slab,
-                      float* bslab, int Z, hipStream_t st, int kid, int kreal) {
+                      float* bslab, int Z, hipStream_t st, int kid, int kreal,
+                      int zinit = 0x7fffffff, int* zused = nullptr) {
     constexpr int NT = 64 * WM * WN;
     constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
     constexpr int OFULL = IH + 2 * PAD - 2;
@@ -666,10 +667,11 @@ static int conv_wgrad(const float* dz, const float* X, int S, int CO, int KP, fl
     BL bl;
     bl.X = X;
     bl.M = M;
-    EpiSlabAcc epi{slab, CO, KP, (long)CO * KP, bslab};
+    EpiSlabAcc epi{slab, CO, KP, (long)CO * KP, bslab, zinit};
     const int tiles = ceil_div(CO, BM) * ceil_div(KP, BN);
-    return launch_gemm<FM, FN, WM, WN>(al, bl, epi, CO, KP, ceil_div(M, GK),
-                                       wsplit(ceil_div(M, GK), Z, tiles), st, kid,
+    const int zu = wsplit(ceil_div(M, GK), Z, tiles);
+    if (zused) *zused = zu;
+    return launch_gemm<FM, FN, WM, WN>(al, bl, epi, CO, KP, ceil_div(M, GK), zu, st, kid,
                                        2.0 * M * CO * kreal);
 }
 
@@ -713,16 +715,18 @@ static int linear_fwd(const float* x, const float* W, float* part, int M, int N,
 // linear weight gradient: slab[z][n][k] += sum_s dy[s][n] x[s][k]; bias slab[z][n] += sum_s dy
 template <int FM, int FN, int WM, int WN>
 static int linear_wgrad(const float* dy, const float* x, float* slab, float* bslab, int S, int N,
-                        int K, int Z, hipStream_t st, int kid) {
+                        int K, int Z, hipStream_t st, int kid, int zinit = 0x7fffffff,
+                        int* zused = nullptr) {
     constexpr int NT = 64 * WM * WN;
     RowsKM<16 * FM * WM, NT> al{};
     al.P = dy; al.ld = N; al.NK = S; al.NC = N;
     RowsKM<16 * FN * WN, NT> bl{};
     bl.P = x; bl.ld = K; bl.NK = S; bl.NC = K;
-    EpiSlabAcc epi{slab, N, K, (long)N * K, bslab};
+    EpiSlabAcc epi{slab, N, K, (long)N * K, bslab, zinit};
     const int tiles = ceil_div(N, 16 * FM * WM) * ceil_div(K, 16 * FN * WN);
-    return launch_gemm<FM, FN, WM, WN>(al, bl, epi, N, K, ceil_div(S, GK),
-                                       wsplit(ceil_div(S, GK), Z, tiles), st, kid,
+    const int zu = wsplit(ceil_div(S, GK), Z, tiles);
+    if (zused) *zused = zu;
+    return launch_gemm<FM, FN, WM, WN>(al, bl, epi, N, K, ceil_div(S, GK), zu, st, kid,
                                        2.0 * S * N * K);
 }
 

@@ -13,6 +13,9 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <mutex>
+#include <unordered_map>
+
 #include "net_kernels.h"
 #include "slabstep.h"
 
@@ -82,13 +85,13 @@ static int pn1_segments(const GradState& g, const float* base, SegSpec* s) {
     for (int l = 0; l < 6; ++l) {
         const ConvGeo& c = GEO[l];
         s[i++] = SegSpec{g.sw[l] - base, c.ZW, (long)c.CO * c.KP, P_OFF[2 * l],
-                         (long)c.CO * c.CI * 9, c.CO, c.CI, c.CIP, c.KP};
-        s[i++] = SegSpec{g.sb[l] - base, c.ZW, c.CO, P_OFF[2 * l + 1], c.CO, 0, 0, 1, 1};
+                         (long)c.CO * c.CI * 9, c.CO, c.CI, c.CIP, c.KP, l};
+        s[i++] = SegSpec{g.sb[l] - base, c.ZW, c.CO, P_OFF[2 * l + 1], c.CO, 0, 0, 1, 1, l};
     }
-    s[i++] = SegSpec{g.l1w - base, ZL1W, 512L * 9408, P_OFF[12], 512L * 9408, 0, 0, 1, 1};
-    s[i++] = SegSpec{g.l1b - base, ZL1W, 512, P_OFF[13], 512, 0, 0, 1, 1};
-    s[i++] = SegSpec{g.l2w - base, ZL2W, 256L * 512, P_OFF[14], 256L * 512, 0, 0, 1, 1};
-    s[i++] = SegSpec{g.l2b - base, ZL2W, 256, P_OFF[15], 256, 0, 0, 1, 1};
+    s[i++] = SegSpec{g.l1w - base, ZL1W, 512L * 9408, P_OFF[12], 512L * 9408, 0, 0, 1, 1, 6};
+    s[i++] = SegSpec{g.l1b - base, ZL1W, 512, P_OFF[13], 512, 0, 0, 1, 1, 6};
+    s[i++] = SegSpec{g.l2w - base, ZL2W, 256L * 512, P_OFF[14], 256L * 512, 0, 0, 1, 1, 7};
+    s[i++] = SegSpec{g.l2b - base, ZL2W, 256, P_OFF[15], 256, 0, 0, 1, 1, 7};
     s[i++] = SegSpec{g.l3w - base, ZH, 2560, P_OFF[16], 2560, 0, 0, 1, 1};
     s[i++] = SegSpec{g.l3b - base, ZH, 10, P_OFF[17], 10, 0, 0, 1, 1};
     return i;
@@ -305,18 +308,54 @@ static int forward(const GradState& g, const WS& w, const float* theta, int S,
     return 0;
 }
 
+// Slab rows written so far this epoch, per slab group (conv1..6, linear1, linear2), host side.
+// begin_epoch does not clear the 1.9 GB of slabs: the weight-gradient GEMMs store into rows not
+// yet written this epoch and accumulate into the others (EpiSlabAcc::zinit), and the epoch's
+// slab sum reads only the written rows (SlabSeg::zlim).  Small chunks use fewer rows (wsplit), so
+// an n = 10 epoch no longer pays a 0.3 ms clear and a full 1.9 GB read.  Keyed by the gradstate
+// address; a gradstate whose epoch was not begun in this process falls back to "every row".
+struct EpochRows {
+    int z[8];
+};
+static std::mutex g_rows_mu;
+static std::unordered_map<const void*, EpochRows> g_rows;
+
+static EpochRows* epoch_rows(const void* gradstate) {
+    std::lock_guard<std::mutex> lk(g_rows_mu);
+    auto it = g_rows.find(gradstate);
+    return it == g_rows.end() ? nullptr : &it->second;
+}
+
+// the plan with each tracked segment limited to its rows written this epoch
+static StepPlan plan_in_use(const GradState& g, const void* gradstate) {
+    StepPlan p = g.plan;
+    const EpochRows* er = epoch_rows(gradstate);
+    if (!er) return p;
+    for (int i = 0; i < p.nseg; ++i)
+        if (p.seg[i].group >= 0) {
+            const int z = er->z[p.seg[i].group];
+            p.seg[i].zlim = z < p.seg[i].Z ? z : p.seg[i].Z;
+        }
+    return p;
+}
+
 static int backward(const GradState& g, const WS& w, const float* theta, int S, int dropout,
-                    hipStream_t st) {
+                    hipStream_t st, EpochRows* er) {
+    constexpr int ALL = 0x7fffffff;
+    auto zi = [&](int grp) { return er ? er->z[grp] : ALL; };
+    int zu[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const float s25 = dropout ? SCALE_P25 : 1.f;
     const float s50 = dropout ? SCALE_P50 : 1.f;
     // ---- linear3 weight/bias (head already produced dlog, dh2) ----
     RC(head_wgrad<256>(w.dlog, w.e2, g.l3w, g.l3b, S, ZH, st));
     // ---- linear2: wgrad, bias, dgrad (-> dh1 through dropout/relu of linear1) ----
-    RC((linear_wgrad<4, 4, 2, 2>(w.dh2, w.e1, g.l2w, g.l2b, S, 256, 512, ZL2W, st, K_L2W)));
+    RC((linear_wgrad<4, 4, 2, 2>(w.dh2, w.e1, g.l2w, g.l2b, S, 256, 512, ZL2W, st, K_L2W, zi(7),
+                                 &zu[7])));
     RC((linear_dgrad<2, 2, 2, 2>(w.dh2, theta + P_OFF[14], w.dh1, w.e1, s50, S, 256, 512, st,
                                  K_L2D)));
     // ---- linear1: wgrad, bias, dgrad (-> gradient wrt d3 through dropout1 site 3) ----
-    RC((linear_wgrad<4, 4, 2, 2>(w.dh1, w.d3, g.l1w, g.l1b, S, 512, 9408, ZL1W, st, K_L1W)));
+    RC((linear_wgrad<4, 4, 2, 2>(w.dh1, w.d3, g.l1w, g.l1b, S, 512, 9408, ZL1W, st, K_L1W, zi(6),
+                                 &zu[6])));
     RC((linear_dgrad<4, 4, 2, 2>(w.dh1, theta + P_OFF[12], w.gy, w.d3, s25, S, 512, 9408, st,
                                  K_L1D)));
     // ---- pool3 backward -> dz6 (a6 buffer: conv6 fwd no longer writes it) ----
@@ -327,40 +366,48 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     float* dz6 = w.a6;
     // ---- conv6: wgrad (input a5), bias, dgrad -> dz5 = . * (a5 > 0) into gx ----
     RC((conv_wgrad<13, 13, 192, 2, 6, 3, 2, 2, 14, true>(dz6, w.a5, S, 192, 1728, g.sw[5],
-                                                        g.sb[5], GEO[5].ZW, st, K_WG6, 1728)));
+                                                        g.sb[5], GEO[5].ZW, st, K_WG6, 1728, zi(5),
+                                             &zu[5])));
     RC((conv_like<14, 14, 192, 0, 2, 6, 4, 2, EpiMask<true>, 13>(dz6, S, g.wd[5], 192, 1728,
         EpiMask<true>{w.gx, w.a5, S * 13 * 13, 192}, st, K_DG6, 1728)));
     float* dz5 = w.gx;
     // ---- conv5: wgrad (input d2), bias, dgrad -> grad wrt d2 (dropout site 2) into gy ----
     RC((conv_wgrad<11, 11, 96, 2, 6, 3, 2, 2>(dz5, w.d2, S, 192, 864, g.sw[4], g.sb[4], GEO[4].ZW,
-                                             st, K_WG5, 864)));
+                                             st, K_WG5, 864, zi(4),
+                                             &zu[4])));
     RC((conv_like<13, 13, 192, 0, 4, 3, 4, 2>(dz5, S, g.wd[4], 96, 1728,
         EpiDropMask{w.gy, w.d2, s25, S * 11 * 11, 96}, st, K_DG5, 1728)));
     RC((pool_scatter<22, 22, 96, false>(w.gy, w.i2, w.a4, S, st)));
     float* dz4 = w.a4;
     // ---- conv4: wgrad (input a3), bias, dgrad -> dz3 = . * (a3 > 0) into gx ----
     RC((conv_wgrad<20, 20, 96, 2, 3, 3, 2, 2>(dz4, w.a3, S, 96, 864, g.sw[3], g.sb[3], GEO[3].ZW,
-                                             st, K_WG4, 864)));
+                                             st, K_WG4, 864, zi(3),
+                                             &zu[3])));
     RC((conv_like<22, 22, 96, 0, 4, 3, 4, 2>(dz4, S, g.wd[3], 96, 864,
         EpiMask<true>{w.gx, w.a3, S * 20 * 20, 96}, st, K_DG4, 864)));
     float* dz3 = w.gx;
     // ---- conv3: wgrad (input d1), bias, dgrad -> grad wrt d1 (site 1) into gy ----
     RC((conv_wgrad<18, 18, 48, 2, 3, 3, 2, 1>(dz3, w.d1, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW,
-                                             st, K_WG3, 432)));
+                                             st, K_WG3, 432, zi(2),
+                                             &zu[2])));
     RC((conv_like<20, 20, 96, 0, 2, 3, 8, 1>(dz3, S, g.wd[2], 48, 864,
         EpiDropMask{w.gy, w.d1, s25, S * 18 * 18, 48}, st, K_DG3, 864)));
     RC((pool_scatter<36, 36, 48, false>(w.gy, w.i1, w.a2, S, st)));
     float* dz2 = w.a2;
     // ---- conv2: wgrad (input a1), bias, dgrad -> dz1 = . * (a1 > 0) into gx ----
     RC((conv_wgrad<34, 34, 48, 2, 3, 3, 1, 3>(dz2, w.a1, S, 48, 432, g.sw[1], g.sb[1], GEO[1].ZW,
-                                             st, K_WG2, 432)));
+                                             st, K_WG2, 432, zi(1),
+                                             &zu[1])));
     RC((conv_like<36, 36, 48, 0, 2, 3, 8, 1>(dz2, S, g.wd[1], 48, 432,
         EpiMaskRows<48>{w.gx, w.a1, S * 34 * 34}, st, K_DG2, 432)));
     float* dz1 = w.gx;
     // ---- conv1: wgrad (input x0), bias ----
     // (3 waves of 16 rows each: 0.272 vs 0.325 ms for one 48x48 wave, profiles/r01c/lab_conv1.txt)
     RC((conv_wgrad<32, 32, 4, 2, 1, 3, 3, 1>(dz1, w.x0, S, 48, 48, g.sw[0], g.sb[0], GEO[0].ZW, st,
-                                            K_WG1, 27)));
+                                            K_WG1, 27, zi(0), &zu[0])));
+    if (er)
+        for (int i = 0; i < 8; ++i)
+            if (zu[i] > er->z[i]) er->z[i] = zu[i];
     return 0;
 }
 
@@ -396,7 +443,13 @@ int flsim_pn1_begin_epoch(void* gradstate, const float* theta, hipStream_t strea
     FLSIM_REQUIRE(gradstate && theta, "null pointer");
     GradState g = gs_layout((float*)gradstate);
     RC(pack_weights(g, theta, stream));
-    FLSIM_CHECK_HIP(hipMemsetAsync(g.slab_begin, 0, g.slab_floats * 4, stream));
+    // only the head's slabs (k_head_wgrad accumulates) and the step's tile counters are cleared;
+    // the other slabs are overwritten by their first writer this epoch (EpochRows)
+    FLSIM_CHECK_HIP(hipMemsetAsync(g.l3w, 0, (g.l3b + ZH * 10 - g.l3w) * 4, stream));
+    FLSIM_CHECK_HIP(hipMemsetAsync((float*)gradstate + g.cnt_off, 0,
+                                   step_counter_floats(g.plan) * 4, stream));
+    std::lock_guard<std::mutex> lk(g_rows_mu);
+    g_rows[gradstate] = EpochRows{{0, 0, 0, 0, 0, 0, 0, 0}};
     return 0;
 }
 
@@ -411,7 +464,7 @@ static int run_chunk(void* gradstate, const WS& w, const float* theta, const Wor
     RC(head_and_loss<256>(w.e2, theta + P_OFF[16], theta + P_OFF[17], w.y, w.loss_s, w.dlog, w.dh2,
                           S, backward_pass, dropout ? SCALE_P50 : 1.f, gscale, worker_loss,
                           stream));
-    if (backward_pass) RC(backward(g, w, theta, S, dropout, stream));
+    if (backward_pass) RC(backward(g, w, theta, S, dropout, stream, epoch_rows(gradstate)));
     return 0;
 }
 
@@ -514,8 +567,8 @@ int flsim_pn1_eval_pool(void* gradstate, void* workspace, int max_samples, const
 int flsim_pn1_end_epoch(void* gradstate, float* grad_out, hipStream_t stream) {
     FLSIM_REQUIRE(gradstate && grad_out, "null pointer");
     GradState g = gs_layout((float*)gradstate);
-    return slab_step_launch((float*)gradstate, g.plan, g.cnt_off, g.part_off, grad_out, nullptr,
-                            nullptr, nullptr, nullptr, nullptr, P_TOTAL, stream);
+    return slab_step_launch((float*)gradstate, plan_in_use(g, gradstate), g.cnt_off, g.part_off,
+                            grad_out, nullptr, nullptr, nullptr, nullptr, nullptr, P_TOTAL, stream);
 }
 
 // the same reduction fused with rule() + Adam (world = 1)
@@ -528,8 +581,8 @@ int flsim_pn1_server_step(void* gradstate, float* S_out, const flsim_rule* rule,
     RC(make_rule(rule, &R));
     AdamConst ac;
     RC(make_adam_const(rule->k, step, lr, beta1, beta2, eps, &ac));
-    return slab_step_launch((float*)gradstate, g.plan, g.cnt_off, g.part_off, S_out, &R, &ac, p,
-                            m, v, P_TOTAL, stream);
+    return slab_step_launch((float*)gradstate, plan_in_use(g, gradstate), g.cnt_off, g.part_off,
+                            S_out, &R, &ac, p, m, v, P_TOTAL, stream);
 }
 
 }  // extern "C"

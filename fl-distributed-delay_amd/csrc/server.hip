@@ -348,7 +348,8 @@ __device__ __forceinline__ void slab_step_wide(const StepArgs& A, const SlabSeg&
         t_end = tile + 1;
     }
     const int z0 = j * g.zc;
-    const int z1 = z0 + g.zc < g.Z ? z0 + g.zc : g.Z;
+    int z1 = z0 + g.zc < g.Z ? z0 + g.zc : g.Z;
+    if (z1 > g.zlim) z1 = g.zlim > z0 ? g.zlim : z0;     // rows past zlim are stale this epoch
     auto ld = [](const float* ptr) -> f32x4 {
         return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(ptr));
     };
@@ -514,7 +515,8 @@ __device__ __forceinline__ void slab_step_body(const StepArgs& A, float* lds) {
     }
     const float* slab = A.base + g.slab_off;
     const int z0 = j * g.zc;
-    const int z1 = z0 + g.zc < g.Z ? z0 + g.zc : g.Z;
+    int z1 = z0 + g.zc < g.Z ? z0 + g.zc : g.Z;
+    if (z1 > g.zlim) z1 = g.zlim > z0 ? g.zlim : z0;     // rows past zlim are stale this epoch
     const ProgRef<INL> prog{A.R};
     const int nst = A.R.narr < NYR ? A.R.narr : NYR;
     for (; tile < t_end; ++tile) {
@@ -765,7 +767,11 @@ int slab_step_launch(float* gradstate, const StepPlan& plan, long cnt_off, long 
     const unsigned nblk = (unsigned)(u_hi - A.u_lo);
     // algorithmic HBM bytes: every slab byte once; S_out written; p, m, v read + written; each
     // distinct entry array read once
-    double bytes = 4.0 * (double)plan.slab_floats + (S_out ? 4.0 * P : 0.0);
+    double slab_read = 0.0;
+    for (int i = 0; i < plan.nseg; ++i)
+        slab_read += (double)(plan.seg[i].zlim < plan.seg[i].Z ? plan.seg[i].zlim : plan.seg[i].Z) *
+                     plan.seg[i].n;
+    double bytes = 4.0 * slab_read + (S_out ? 4.0 * P : 0.0);
     if (rule) bytes += 4.0 * (double)P * (6 + rule->distinct);
     const ProbeSlot ps = probe_begin();
     if (!rule) {

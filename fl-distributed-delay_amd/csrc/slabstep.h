@@ -34,6 +34,7 @@ struct SegSpec {
     long n;
     long toff, numel;  // the tensor in the flat named_parameters vector
     int CO, CI, CIP, KP;   // packed conv layout n = CO * KP, column = co*KP + khkw*CIP + ci; CO = 0: identity
+    int group = -1;        // slab-row group whose rows in use this epoch are tracked (-1: all Z)
 };
 
 // planned segment (kernel argument)
@@ -42,6 +43,8 @@ struct SlabSeg {
     int Z, n, zc, nz, tiles, tpu, unit0, tile0, toff, numel;
     uint16_t CO, CI, CIP, KP;
     uint16_t wide;   // identity layout, 16-B aligned, no row_sum tail: 1024-element float4 tiles
+    int16_t group;   // SegSpec::group
+    int zlim;        // rows [0, zlim) hold this epoch's sums (set per launch; the rest are stale)
 };
 
 struct StepPlan {
@@ -88,6 +91,8 @@ inline int plan_step(const SegSpec* s_in, int nseg, StepPlan* P) {
         g.CIP = (uint16_t)s[i].CIP;
         g.KP = (uint16_t)s[i].KP;
         g.wide = seg_wide(s[i]);
+        g.group = (int16_t)s[i].group;
+        g.zlim = g.Z;
         g.tiles = (int)((s[i].n + (g.wide ? 1023 : 255)) / (g.wide ? 1024 : 256));
         const long tile_f = (g.wide ? 1024L : 256L) * s[i].Z;
         // wide tiles: 64 KB units (one tile of a few rows per block: many blocks in flight)
