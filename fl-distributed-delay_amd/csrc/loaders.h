@@ -20,6 +20,31 @@ __device__ __forceinline__ f32x4 ldg4_or0(const float* p, const float* /*safe*/,
     return ok ? ldg4(p) : zero4();
 }
 
+// Buffer-resource loads (FLSIM_BUFLOAD, default on): the operand tensor is one buffer of `bytes`
+// bytes (< 4 GB, every activation at the 16,384-sample chunk is), addressed by 32-bit byte offsets.
+// A masked unit (padding tap, row or column past the matrix) passes the out-of-range offset
+// BUF_OOB and the hardware returns zeros: no exec-mask branch around the load, no zeroing of the
+// destination registers, no 64-bit address arithmetic per unit.
+#ifndef FLSIM_BUFLOAD
+#define FLSIM_BUFLOAD 1
+#endif
+constexpr unsigned BUF_OOB = 0xfffffff0u;
+struct BufSrc {
+    __amdgpu_buffer_rsrc_t r;
+    __device__ __forceinline__ void init(const float* base, unsigned long bytes) {
+        // raw buffer (stride 0): num_records in bytes; dword 3 = the gfx9 raw-buffer format word
+        const unsigned n = bytes < (unsigned long)BUF_OOB ? (unsigned)bytes : BUF_OOB;
+        r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, (int)n,
+                                              0x00020000);
+    }
+    __device__ __forceinline__ f32x4 ld(unsigned byte_off) const {
+        return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+    }
+    __device__ __forceinline__ f32x4 ld_or0(unsigned byte_off, bool ok) const {
+        return ld(ok ? byte_off : BUF_OOB);
+    }
+};
+
 // r / D for 0 <= r < R by one 24-bit multiply and a shift (exact on that range, checked at
 // compile time): the per-unit pixel -> (row, column) split of the k-major loaders
 template <unsigned D, unsigned R>
@@ -74,9 +99,12 @@ struct Im2colKC {
     short tapmask[UNITS];   // bit kh*3+kw set iff that tap of this output pixel is inside X
     short row[UNITS];
     int q;
+    BufSrc buf;
 
     __device__ void setup(int m0, int tid) {
         q = tid & 3;
+        if constexpr (FLSIM_BUFLOAD)
+            buf.init(X, (unsigned long)((M + ROWS_PER_IMG - 1) / ROWS_PER_IMG) * IH * IW * CI * 4);
 #pragma unroll
         for (int j = 0; j < UNITS; ++j) {
             const int u = tid + j * NT;
@@ -123,7 +151,10 @@ struct Im2colKC {
 #pragma unroll
             for (int j = 0; j < UNITS; ++j) {
                 const bool ok = (tapmask[j] >> khkw) & 1;
-                r[j] = ldg4_or0(X + base[j] + off, X, ok);
+                if constexpr (FLSIM_BUFLOAD)
+                    r[j] = buf.ld_or0((unsigned)base[j] * 4u + (unsigned)off * 4u, ok);
+                else
+                    r[j] = ldg4_or0(X + base[j] + off, X, ok);
             }
         } else {
             const int k = ks * GK + 4 * q;          // CI == 4: one tap per lane quad
@@ -133,7 +164,10 @@ struct Im2colKC {
 #pragma unroll
             for (int j = 0; j < UNITS; ++j) {
                 const bool ok = khkw < 9 && ((tapmask[j] >> khkw) & 1);
-                r[j] = ldg4_or0(X + base[j] + off, X, ok);
+                if constexpr (FLSIM_BUFLOAD)
+                    r[j] = buf.ld_or0((unsigned)base[j] * 4u + (unsigned)off * 4u, ok);
+                else
+                    r[j] = ldg4_or0(X + base[j] + off, X, ok);
             }
         }
     }
@@ -159,21 +193,31 @@ struct RowsKC {
     long ld;
     int NR;
     const float* rowp[UNITS];
+    unsigned rowb[UNITS];   // byte offset of the unit's row chunk, BUF_OOB past the matrix
     short row[UNITS];
     int q;
+    BufSrc buf;
     __device__ void setup(int r0, int tid) {
         q = tid & 3;
+        if constexpr (FLSIM_BUFLOAD) buf.init(P, (unsigned long)NR * ld * 4);
 #pragma unroll
         for (int j = 0; j < UNITS; ++j) {
             const int u = tid + j * NT;
             const int r = u >> 2;
             row[j] = (short)r;
-            rowp[j] = (u < TOTAL && r0 + r < NR) ? P + (long)(r0 + r) * ld + 4 * q : nullptr;
+            const bool ok = u < TOTAL && r0 + r < NR;
+            rowp[j] = ok ? P + (long)(r0 + r) * ld + 4 * q : nullptr;
+            rowb[j] = ok ? (unsigned)(((long)(r0 + r) * ld + 4 * q) * 4) : BUF_OOB;
         }
     }
     __device__ void load(int ks, f32x4 (&r)[UNITS]) const {
 #pragma unroll
-        for (int j = 0; j < UNITS; ++j) r[j] = ldg4_or0(rowp[j] + ks * GK, P, rowp[j] != nullptr);
+        for (int j = 0; j < UNITS; ++j) {
+            if constexpr (FLSIM_BUFLOAD)
+                r[j] = buf.ld(rowb[j] == BUF_OOB ? BUF_OOB : rowb[j] + (unsigned)(ks * GK * 4));
+            else
+                r[j] = ldg4_or0(rowp[j] + ks * GK, P, rowp[j] != nullptr);
+        }
     }
     __device__ void store(float* lds, const f32x4 (&r)[UNITS]) const {
 #pragma unroll
@@ -206,8 +250,13 @@ struct RowsKM {
     int krow;
     int c_off[UNITS];
     short c4[UNITS];
+    BufSrc buf;
     __device__ void setup(int c0, int tid) {
         krow = tid / TPR;
+        if constexpr (FLSIM_BUFLOAD) {
+            const long rows = PO > 0 ? (long)((NK + PV * PV - 1) / (PV * PV)) * PO * PO : NK;
+            buf.init(P, (unsigned long)rows * ld * 4);
+        }
 #pragma unroll
         for (int j = 0; j < UNITS; ++j) {
             const int c = tid % TPR + TPR * j;
@@ -229,10 +278,17 @@ struct RowsKM {
             const unsigned oh = SmallDiv<PV, PV * PV + GK>::div(rem);
             row = (long)img * (PO * PO) + oh * PO + (rem - oh * PV);
         }
-        const float* rp = P + row * ld;
         const bool rok = k < NK;
+        if constexpr (FLSIM_BUFLOAD) {
+            const unsigned rb = (unsigned)(row * ld) * 4u;
 #pragma unroll
-        for (int j = 0; j < UNITS; ++j) r[j] = ldg4_or0(rp + c_off[j], P, rok && c_off[j] >= 0);
+            for (int j = 0; j < UNITS; ++j)
+                r[j] = buf.ld_or0(rb + (unsigned)c_off[j] * 4u, rok && c_off[j] >= 0);
+        } else {
+            const float* rp = P + row * ld;
+#pragma unroll
+            for (int j = 0; j < UNITS; ++j) r[j] = ldg4_or0(rp + c_off[j], P, rok && c_off[j] >= 0);
+        }
     }
     __device__ void store(float* lds, const f32x4 (&r)[UNITS]) const {
 #pragma unroll
@@ -265,8 +321,11 @@ struct Im2colKM {
     int coff[UNITS];   // ((kh - PAD) * IW + kw - PAD) * CI + ci: the column's offset from pixel (oh, ow)
     short kh[UNITS], kw[UNITS];   // tap of the column; kh = -64 when it is padding
     short c4[UNITS];
+    BufSrc buf;
     __device__ void setup(int c0, int tid) {
         krow = tid / TPR;
+        if constexpr (FLSIM_BUFLOAD)
+            buf.init(X, (unsigned long)((M + OH * OW - 1) / (OH * OW)) * IH * IW * CI * 4);
 #pragma unroll
         for (int j = 0; j < UNITS; ++j) {
             const int c = tid % TPR + TPR * j;
@@ -293,13 +352,16 @@ struct Im2colKM {
         }
         const int oh = (int)SmallDiv<OW, OH * OW + GK>::div(rem);
         const int ow = (int)rem - oh * OW;
-        const float* xp = X + ((long)img * IH * IW + oh * IW + ow) * CI;
+        const long xo = ((long)img * IH * IW + oh * IW + ow) * CI;
         const bool pok = p < M;
 #pragma unroll
         for (int j = 0; j < UNITS; ++j) {
             const int ih = oh + kh[j] - PAD, iw = ow + kw[j] - PAD;
             const bool ok = pok && (unsigned)ih < (unsigned)IH && (unsigned)iw < (unsigned)IW;
-            r[j] = ldg4_or0(xp + coff[j], X, ok);
+            if constexpr (FLSIM_BUFLOAD)
+                r[j] = buf.ld_or0((unsigned)xo * 4u + (unsigned)coff[j] * 4u, ok);
+            else
+                r[j] = ldg4_or0(X + xo + coff[j], X, ok);
         }
     }
     __device__ void store(float* lds, const f32x4 (&r)[UNITS]) const {
