@@ -207,22 +207,26 @@ k_conv1_fwd(const float* __restrict__ x0, const float* __restrict__ W, const flo
         w8[j] = g < 3 ? W[(co * 3 + g) * 9 + 8] : 0.f;
         bj[j] = bias[co];
     }
+    // x0 as one buffer (S * 16 KB < 4 GB): 32-bit index math, out-of-range taps read zeros from
+    // the hardware's bounds check instead of an exec-masked branch
+    BufSrc xb;
+    xb.init(x0, (unsigned long)(units * C1_ROWS / 1156) * 4096 * 4);
     auto load = [&](long u, f32x4 (&xa)[2][2], float (&x8)[2]) {
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-            const long m = u * C1_ROWS + 16 * t + i;
-            const long smp = m / 1156;
-            const int rem = (int)(m - smp * 1156);
+            const unsigned m = (unsigned)u * C1_ROWS + 16 * t + i;
+            const unsigned smp = m / 1156u;
+            const int rem = (int)(m - smp * 1156u);
             const int oh = rem / 34, ow = rem - (rem / 34) * 34;
-            const float* xs = x0 + smp * 4096;
+            const unsigned xs = smp * 4096u;
 #pragma unroll
             for (int sx = 0; sx < 2; ++sx) {
                 const int tap = 4 * sx + g;
                 const int ih = oh + tap / 3 - 2, iw = ow + tap % 3 - 2;
-                xa[t][sx] = ((unsigned)ih < 32u && (unsigned)iw < 32u)
-                                ? *reinterpret_cast<const f32x4*>(xs + (ih * 32 + iw) * 4) : zero4();
+                xa[t][sx] = xb.ld_or0((xs + (unsigned)(ih * 32 + iw) * 4u) * 4u,
+                                      (unsigned)ih < 32u && (unsigned)iw < 32u);
             }
-            x8[t] = (oh < 32 && ow < 32) ? xs[(oh * 32 + ow) * 4 + g] : 0.f;   // tap 8: (ih, iw) = (oh, ow)
+            x8[t] = (oh < 32 && ow < 32) ? x0[xs + (oh * 32 + ow) * 4 + g] : 0.f;   // tap 8: (ih, iw) = (oh, ow)
         }
     };
     const long nw = (long)gridDim.x * 4;
