@@ -293,7 +293,7 @@ struct RowsKM {
     __device__ void store(float* lds, const f32x4 (&r)[UNITS]) const {
 #pragma unroll
         for (int j = 0; j < UNITS; ++j)
-            if (C4 % TPR == 0 || c4[j] < C4) store_unit<false, ROWS>(lds, krow, c4[j], r[j]);
+            store_km_or_spare<ROWS>(lds, C4 % TPR == 0 || c4[j] < C4, krow, c4[j], r[j]);
     }
 };
 
@@ -367,7 +367,7 @@ struct Im2colKM {
     __device__ void store(float* lds, const f32x4 (&r)[UNITS]) const {
 #pragma unroll
         for (int j = 0; j < UNITS; ++j)
-            if (C4 % TPR == 0 || c4[j] < C4) store_unit<false, ROWS>(lds, krow, c4[j], r[j]);
+            store_km_or_spare<ROWS>(lds, C4 % TPR == 0 || c4[j] < C4, krow, c4[j], r[j]);
     }
 };
 
