@@ -96,6 +96,7 @@ struct Im2colKC {
     const float* X;
     int M;
     long base[UNITS];       // element offset of input pixel (oh - PAD, ow - PAD), channel 4q
+    unsigned vb[UNITS];     // the same in bytes, mod 2^32 (buffer loads)
     short tapmask[UNITS];   // bit kh*3+kw set iff that tap of this output pixel is inside X
     short row[UNITS];
     int q;
@@ -135,6 +136,7 @@ struct Im2colKC {
                 }
                 tapmask[j] = (short)msk;
             }
+            vb[j] = (unsigned)base[j] * 4u;
         }
     }
     __device__ void load(int ks, f32x4 (&r)[UNITS]) const {
@@ -152,7 +154,7 @@ struct Im2colKC {
             for (int j = 0; j < UNITS; ++j) {
                 const bool ok = (tapmask[j] >> khkw) & 1;
                 if constexpr (FLSIM_BUFLOAD)
-                    r[j] = buf.ld_or0((unsigned)base[j] * 4u + (unsigned)off * 4u, ok);
+                    r[j] = buf.ld_or0(vb[j] + (unsigned)off * 4u, ok);
                 else
                     r[j] = ldg4_or0(X + base[j] + off, X, ok);
             }
@@ -165,7 +167,7 @@ struct Im2colKC {
             for (int j = 0; j < UNITS; ++j) {
                 const bool ok = khkw < 9 && ((tapmask[j] >> khkw) & 1);
                 if constexpr (FLSIM_BUFLOAD)
-                    r[j] = buf.ld_or0((unsigned)base[j] * 4u + (unsigned)off * 4u, ok);
+                    r[j] = buf.ld_or0(vb[j] + (unsigned)off * 4u, ok);
                 else
                     r[j] = ldg4_or0(X + base[j] + off, X, ok);
             }
@@ -280,7 +282,7 @@ struct RowsKM {
         }
         const bool rok = k < NK;
         if constexpr (FLSIM_BUFLOAD) {
-            const unsigned rb = (unsigned)(row * ld) * 4u;
+            const unsigned rb = (unsigned)row * ((unsigned)ld * 4u);
 #pragma unroll
             for (int j = 0; j < UNITS; ++j)
                 r[j] = buf.ld_or0(rb + (unsigned)c_off[j] * 4u, rok && c_off[j] >= 0);
@@ -352,16 +354,23 @@ struct Im2colKM {
         }
         const int oh = (int)SmallDiv<OW, OH * OW + GK>::div(rem);
         const int ow = (int)rem - oh * OW;
-        const long xo = ((long)img * IH * IW + oh * IW + ow) * CI;
         const bool pok = p < M;
+        if constexpr (FLSIM_BUFLOAD) {
+            const unsigned xb = (img * (unsigned)(IH * IW) + (unsigned)(oh * IW + ow)) * (CI * 4u);
 #pragma unroll
-        for (int j = 0; j < UNITS; ++j) {
-            const int ih = oh + kh[j] - PAD, iw = ow + kw[j] - PAD;
-            const bool ok = pok && (unsigned)ih < (unsigned)IH && (unsigned)iw < (unsigned)IW;
-            if constexpr (FLSIM_BUFLOAD)
-                r[j] = buf.ld_or0((unsigned)xo * 4u + (unsigned)coff[j] * 4u, ok);
-            else
+            for (int j = 0; j < UNITS; ++j) {
+                const int ih = oh + kh[j] - PAD, iw = ow + kw[j] - PAD;
+                const bool ok = pok && (unsigned)ih < (unsigned)IH && (unsigned)iw < (unsigned)IW;
+                r[j] = buf.ld_or0(xb + (unsigned)coff[j] * 4u, ok);
+            }
+        } else {
+            const long xo = ((long)img * IH * IW + oh * IW + ow) * CI;
+#pragma unroll
+            for (int j = 0; j < UNITS; ++j) {
+                const int ih = oh + kh[j] - PAD, iw = ow + kw[j] - PAD;
+                const bool ok = pok && (unsigned)ih < (unsigned)IH && (unsigned)iw < (unsigned)IW;
                 r[j] = ldg4_or0(X + xo + coff[j], X, ok);
+            }
         }
     }
     __device__ void store(float* lds, const f32x4 (&r)[UNITS]) const {
