@@ -369,7 +369,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC((pool_scatter<14, 14, 192, true>(w.gy, w.i3, w.a6, S, st)));
     float* dz6 = w.a6;
     // ---- conv6: wgrad (input a5), bias, dgrad -> dz5 = . * (a5 > 0) into gx ----
-    RC((conv_wgrad<13, 13, 192, 2, 6, 3, 2, 2, 14, true>(dz6, w.a5, S, 192, 1728, g.sw[5],
+    RC((conv_wgrad<13, 13, 192, 2, 6, 3, 2, 4, 14, true>(dz6, w.a5, S, 192, 1728, g.sw[5],
                                                         g.sb[5], GEO[5].ZW, st, K_WG6, 1728, zi(5),
                                              &zu[5])));
     RC((conv_like<14, 14, 192, 0, 2, 6, 4, 2, EpiMask<true>, 13>(dz6, S, g.wd[5], 192, 1728,
@@ -399,7 +399,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC((pool_scatter<36, 36, 48, false>(w.gy, w.i1, w.a2, S, st)));
     float* dz2 = w.a2;
     // ---- conv2: wgrad (input a1), bias, dgrad -> dz1 = . * (a1 > 0) into gx ----
-    RC((conv_wgrad<34, 34, 48, 2, 3, 3, 1, 3>(dz2, w.a1, S, 48, 432, g.sw[1], g.sb[1], GEO[1].ZW,
+    RC((conv_wgrad<34, 34, 48, 2, 3, 3, 1, 1>(dz2, w.a1, S, 48, 432, g.sw[1], g.sb[1], GEO[1].ZW,
                                              st, K_WG2, 432, zi(1),
                                              &zu[1])));
     RC((conv_like<36, 36, 48, 0, 2, 3, 8, 1>(dz2, S, g.wd[1], 48, 432,

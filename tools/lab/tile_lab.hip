@@ -245,5 +245,20 @@ int main(int argc, char** argv) {
     G("wg2 48x48 1w", 34, 48, 48, 4096, 3, 3, 1, 1, 1, 0, 0)
     G("wg2 48x144 1w", 34, 48, 48, 4096, 3, 9, 1, 1, 1, 0, 0)
     G("wg2 48x96 2w", 34, 48, 48, 4096, 3, 3, 1, 2, 1, 0, 0)
+    // round 2, after the buffer-resource loads: the largest weight gradients and forwards
+    G("wg6 192x96 4w", 13, 192, 192, 256, 6, 3, 2, 2, 1, 0, 0)
+    G("wg6 192x192 8w", 13, 192, 192, 256, 6, 3, 2, 4, 1, 0, 0)
+    G("wg6 96x192 4w", 13, 192, 192, 256, 3, 6, 2, 2, 1, 0, 0)
+    G("wg6 192x96 4w m4", 13, 192, 192, 256, 3, 6, 4, 1, 1, 0, 0)
+    G("wg6 192x144 6w", 13, 192, 192, 256, 6, 3, 2, 3, 1, 0, 0)
+    G("wg5 192x96 4w", 11, 96, 192, 512, 6, 3, 2, 2, 1, 0, 0)
+    G("wg5 192x192 8w", 11, 96, 192, 512, 6, 3, 2, 4, 1, 0, 0)
+    G("wg4 96x96 4w", 20, 96, 96, 1024, 3, 3, 2, 2, 1, 0, 0)
+    G("wg4 96x192 8w", 20, 96, 96, 1024, 3, 3, 2, 4, 1, 0, 0)
+    G("wg4 96x144 6w", 20, 96, 96, 1024, 3, 3, 2, 3, 1, 0, 0)
+    G("wg3b 96x48 2w", 18, 48, 96, 2048, 3, 3, 2, 1, 1, 0, 0)
+    G("wg3b 96x144 6w", 18, 48, 96, 2048, 3, 3, 2, 3, 1, 0, 0)
+    G("wg2b 48x144 3w", 34, 48, 48, 4096, 3, 3, 1, 3, 1, 0, 0)
+    G("wg2b 48x144 6w", 34, 48, 48, 4096, 3, 3, 1, 3, 1, 0, 0)
     return 0;
 }
