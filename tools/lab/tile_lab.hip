@@ -260,5 +260,22 @@ int main(int argc, char** argv) {
     G("wg3b 96x144 6w", 18, 48, 96, 2048, 3, 3, 2, 3, 1, 0, 0)
     G("wg2b 48x144 3w", 34, 48, 48, 4096, 3, 3, 1, 3, 1, 0, 0)
     G("wg2b 48x144 6w", 34, 48, 48, 4096, 3, 3, 1, 3, 1, 0, 0)
+    F("fwd6 128x192 8w", 13, 192, 2, 192, 2, 6, 4, 2, 1, 0)
+    F("fwd6 256x192 8w", 13, 192, 2, 192, 4, 6, 4, 2, 1, 0)
+    F("fwd6 128x192 4w", 13, 192, 2, 192, 4, 6, 2, 2, 1, 0)
+    F("fwd6 256x96 8w", 13, 192, 2, 192, 4, 3, 4, 2, 1, 0)
+    F("fwd6 128x96 4w", 13, 192, 2, 192, 2, 3, 4, 2, 1, 0)
+    F("dg6 128x192 8w", 15, 192, 0, 192, 2, 6, 4, 2, 1, 0)
+    F("dg6 256x192 8w", 15, 192, 0, 192, 4, 6, 4, 2, 1, 0)
+    F("dg6 256x96 8w", 15, 192, 0, 192, 4, 3, 4, 2, 1, 0)
+    F("fwd4 256x96 8w", 20, 96, 2, 96, 4, 3, 4, 2, 1, 0)
+    F("fwd4 128x96 4w", 20, 96, 2, 96, 4, 3, 2, 2, 1, 0)
+    F("fwd4 256x96 4w", 20, 96, 2, 96, 8, 3, 2, 2, 1, 0)
+    F("dg4 256x96 8w", 22, 96, 0, 96, 4, 3, 4, 2, 1, 0)
+    F("dg4 128x96 4w", 22, 96, 0, 96, 4, 3, 2, 2, 1, 0)
+    F("fwd5 128x192 8w", 11, 96, 2, 192, 2, 6, 4, 2, 1, 0)
+    F("fwd5 256x192 8w", 11, 96, 2, 192, 4, 6, 4, 2, 1, 0)
+    F("dg5 256x96 8w", 13, 192, 0, 96, 4, 3, 4, 2, 1, 0)
+    F("dg5 128x96 4w", 13, 192, 0, 96, 4, 3, 2, 2, 1, 0)
     return 0;
 }
