@@ -287,13 +287,13 @@ static int forward(const GradState& g, const WS& w, const float* theta, int S,
     RC((conv_pool_fwd<34, 34, 48, 48, 2, 2, 3, 4, 1, false>(w.a1, S, g.wf[1], 432, w.d1, w.i1,
         theta + P_OFF[3], workers, seed, SITE_DROP1, THR_P25, SCALE_P25, dropout, st, K_FWD2,
         432)));
-    RC((conv_like<18, 18, 48, 2, 4, 3, 4, 2>(w.d1, S, g.wf[2], 96, 432,
+    RC((conv_like<18, 18, 48, 2, 2, 3, 4, 2>(w.d1, S, g.wf[2], 96, 432,
         EpiBiasRelu{w.a3, theta + P_OFF[5], S * 20 * 20, 96}, st, K_FWD3, 432)));
     // conv4 + ReLU + pool2 + dropout1 (models.py:34-36)
     RC((conv_pool_fwd<20, 20, 96, 96, 2, 4, 3, 2, 2, false>(w.a3, S, g.wf[3], 864, w.d2, w.i2,
         theta + P_OFF[7], workers, seed, SITE_DROP2, THR_P25, SCALE_P25, dropout, st, K_FWD4,
         864)));
-    RC((conv_like<11, 11, 96, 2, 2, 6, 4, 2>(w.d2, S, g.wf[4], 192, 864,
+    RC((conv_like<11, 11, 96, 2, 2, 3, 4, 2>(w.d2, S, g.wf[4], 192, 864,
         EpiBiasRelu{w.a5, theta + P_OFF[9], S * 13 * 13, 192}, st, K_FWD5, 864)));
     // conv6 + ReLU + pool3 + dropout1 (models.py:38-40), written in torch's flatten order
     // (models.py:41) so linear1 keeps the torch weight layout; the floor-mode border row/column
@@ -394,7 +394,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC((conv_wgrad<18, 18, 48, 2, 3, 3, 2, 1>(dz3, w.d1, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW,
                                              st, K_WG3, 432, zi(2),
                                              &zu[2])));
-    RC((conv_like<20, 20, 96, 0, 2, 3, 8, 1>(dz3, S, g.wd[2], 48, 864,
+    RC((conv_like<20, 20, 96, 0, 4, 3, 4, 1>(dz3, S, g.wd[2], 48, 864,
         EpiDropMask{w.gy, w.d1, s25, S * 18 * 18, 48}, st, K_DG3, 864)));
     RC((pool_scatter<36, 36, 48, false>(w.gy, w.i1, w.a2, S, st)));
     float* dz2 = w.a2;
@@ -402,7 +402,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC((conv_wgrad<34, 34, 48, 2, 3, 3, 1, 1>(dz2, w.a1, S, 48, 432, g.sw[1], g.sb[1], GEO[1].ZW,
                                              st, K_WG2, 432, zi(1),
                                              &zu[1])));
-    RC((conv_like<36, 36, 48, 0, 2, 3, 8, 1>(dz2, S, g.wd[1], 48, 432,
+    RC((conv_like<36, 36, 48, 0, 2, 3, 4, 1>(dz2, S, g.wd[1], 48, 432,
         EpiMaskRows<48>{w.gx, w.a1, S * 34 * 34}, st, K_DG2, 432)));
     float* dz1 = w.gx;
     // ---- conv1: wgrad (input x0), bias ----

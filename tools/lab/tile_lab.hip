@@ -277,5 +277,17 @@ int main(int argc, char** argv) {
     F("fwd5 256x192 8w", 11, 96, 2, 192, 4, 6, 4, 2, 1, 0)
     F("dg5 256x96 8w", 13, 192, 0, 96, 4, 3, 4, 2, 1, 0)
     F("dg5 128x96 4w", 13, 192, 0, 96, 4, 3, 2, 2, 1, 0)
+    F("fwd5b 128x96 8w", 11, 96, 2, 192, 2, 3, 4, 2, 1, 0)
+    F("fwd5b 128x192 8w", 11, 96, 2, 192, 2, 6, 4, 2, 1, 0)
+    F("fwd3 256x96 8w", 18, 48, 2, 96, 4, 3, 4, 2, 1, 0)
+    F("fwd3 128x96 4w", 18, 48, 2, 96, 4, 3, 2, 2, 1, 0)
+    F("fwd3 128x96 8w", 18, 48, 2, 96, 2, 3, 4, 2, 1, 0)
+    F("dg3 256x48 8w", 20, 96, 0, 48, 2, 3, 8, 1, 1, 0)
+    F("dg3 128x48 4w", 20, 96, 0, 48, 2, 3, 4, 1, 1, 0)
+    F("dg3 256x48 4w", 20, 96, 0, 48, 4, 3, 4, 1, 1, 0)
+    F("dg2b 256x48 8w", 36, 48, 0, 48, 2, 3, 8, 1, 1, 0)
+    F("dg2b 128x48 4w", 36, 48, 0, 48, 2, 3, 4, 1, 1, 0)
+    F("fwd2b 128x48 4w", 34, 48, 2, 48, 2, 3, 4, 1, 1, 0)
+    F("fwd2b 128x48 2w", 34, 48, 2, 48, 4, 3, 2, 1, 1, 0)
     return 0;
 }
