@@ -217,7 +217,7 @@ int main(int argc, char** argv) {
     const size_t big = (size_t)S * 36 * 36 * 48;
     float* X = dalloc(big, 1.f);
     float* Y = dalloc(big, 0.f);
-    float* W = dalloc(192 * 1728 + 64, 0.05f);
+    float* W = dalloc(512 * 4608 + 64, 0.05f);    // up to vgg11's 512 x 4608
     float* b = dalloc(256, 0.01f);
     const size_t slabn = (size_t)4096 * 48 * 432;
     float* slab = dalloc(slabn, 0.f);
@@ -289,5 +289,20 @@ int main(int argc, char** argv) {
     F("dg2b 128x48 4w", 36, 48, 0, 48, 2, 3, 4, 1, 1, 0)
     F("fwd2b 128x48 4w", 34, 48, 2, 48, 2, 3, 4, 1, 1, 0)
     F("fwd2b 128x48 2w", 34, 48, 2, 48, 4, 3, 2, 1, 1, 0)
+    // vgg11 (padding 1), the product's 128x128 4-wave tile against others
+    F("vfwd2 128x128 4w", 16, 64, 1, 128, 4, 4, 2, 2, 1, 0)
+    F("vfwd2 128x128 8w", 16, 64, 1, 128, 2, 4, 4, 2, 1, 0)
+    F("vfwd2 256x128 8w", 16, 64, 1, 128, 4, 4, 4, 2, 1, 0)
+    F("vfwd2 128x64 4w", 16, 64, 1, 128, 4, 2, 2, 2, 1, 0)
+    F("vfwd4 128x128 4w", 8, 256, 1, 256, 4, 4, 2, 2, 1, 0)
+    F("vfwd4 128x128 8w", 8, 256, 1, 256, 2, 4, 4, 2, 1, 0)
+    F("vfwd4 256x128 8w", 8, 256, 1, 256, 4, 4, 4, 2, 1, 0)
+    F("vfwd4 128x256 8w", 8, 256, 1, 256, 4, 4, 2, 4, 1, 0)
+    F("vfwd4 128x64 4w", 8, 256, 1, 256, 4, 2, 2, 2, 1, 0)
+    F("vfwd6 128x128 4w", 4, 512, 1, 512, 4, 4, 2, 2, 1, 0)
+    F("vfwd6 128x128 8w", 4, 512, 1, 512, 2, 4, 4, 2, 1, 0)
+    F("vfwd6 256x128 8w", 4, 512, 1, 512, 4, 4, 4, 2, 1, 0)
+    F("vfwd6 128x256 8w", 4, 512, 1, 512, 4, 4, 2, 4, 1, 0)
+    F("vfwd6 128x64 4w", 4, 512, 1, 512, 4, 2, 2, 2, 1, 0)
     return 0;
 }
