@@ -187,16 +187,17 @@ static void conv_fwd(const char* tag, const float* X, const float* W, const floa
     time_ks<FM, FN, WM, WN, KSUB, PIN>(tag, al, bl, epi, al.M, CO, KP / GK, 1, 2.0 * al.M * CO * KP);
 }
 
-template <int IH, int CI, int CO, int FM, int FN, int WM, int WN, int KSUB, int PIN, int VO = 0>
+template <int IH, int CI, int CO, int FM, int FN, int WM, int WN, int KSUB, int PIN, int VO = 0,
+          int PAD = 2>
 static void conv_wgrad(const char* tag, const float* dz, const float* X, float* slab, float* bslab,
                        int S, int Z) {
     constexpr int NT = 64 * WM * WN, BM = 16 * FM * WM, BN = 16 * FN * WN;
-    constexpr int OFULL = IH + 2;
+    constexpr int OFULL = IH + 2 * PAD - 2;
     using AL = RowsKM<BM, NT, (VO > 0 ? OFULL : 0), VO>;
-    using BL = Im2colKMo<IH, IH, CI, 2, BN, NT, 0, VO>;
+    using BL = Im2colKMo<IH, IH, CI, PAD, BN, NT, 0, VO>;
     const int M = S * BL::OH * BL::OW;
     const int KP = 9 * CI;
-    if ((size_t)Z * CO * KP > (size_t)4096 * 48 * 432 || (size_t)Z * CO > (size_t)4096 * 192) {
+    if ((size_t)Z * CO * KP > (size_t)8192 * 48 * 432 || (size_t)Z * CO > (size_t)4096 * 192) {
         printf("%-24s skipped: Z * CO * KP exceeds the lab's slab capacity\n", tag);
         return;
     }
@@ -219,7 +220,7 @@ int main(int argc, char** argv) {
     float* Y = dalloc(big, 0.f);
     float* W = dalloc(512 * 4608 + 64, 0.05f);    // up to vgg11's 512 x 4608
     float* b = dalloc(256, 0.01f);
-    const size_t slabn = (size_t)4096 * 48 * 432;
+    const size_t slabn = (size_t)8192 * 48 * 432;
     float* slab = dalloc(slabn, 0.f);
     float* bsl = dalloc(4096 * 192, 0.f);
     const char* only = argc > 1 ? argv[1] : "";
@@ -228,6 +229,8 @@ int main(int argc, char** argv) {
     if (want(tag)) conv_fwd<IH, CI, PAD, CO, FM, FN, WM, WN, KS, PIN>(tag, X, W, b, Y, S);
 #define G(tag, IH, CI, CO, Z, FM, FN, WM, WN, KS, PIN, VO) \
     if (want(tag)) conv_wgrad<IH, CI, CO, FM, FN, WM, WN, KS, PIN, VO>(tag, Y, X, slab, bsl, S, Z);
+#define GV(tag, IH, CI, CO, Z, FM, FN, WM, WN) \
+    if (want(tag)) conv_wgrad<IH, CI, CO, FM, FN, WM, WN, 1, 0, 0, 1>(tag, Y, X, slab, bsl, S, Z);
     F("fwd2 256x48 8w", 34, 48, 2, 48, 2, 3, 8, 1, 1, 0)
     F("fwd2 256x48 4w", 34, 48, 2, 48, 4, 3, 4, 1, 1, 0)
     F("fwd2 512x48 8w", 34, 48, 2, 48, 4, 3, 8, 1, 1, 0)
@@ -304,5 +307,16 @@ int main(int argc, char** argv) {
     F("vfwd6 256x128 8w", 4, 512, 1, 512, 4, 4, 4, 2, 1, 0)
     F("vfwd6 128x256 8w", 4, 512, 1, 512, 4, 4, 2, 4, 1, 0)
     F("vfwd6 128x64 4w", 4, 512, 1, 512, 4, 2, 2, 2, 1, 0)
+    // vgg11 weight gradients (ZW from vgg_net.hip VG[])
+    GV("vwg2 128x128 4w", 16, 64, 128, 512, 4, 4, 2, 2)
+    GV("vwg2 128x192 6w", 16, 64, 128, 512, 4, 4, 2, 3)
+    GV("vwg2 128x64 2w", 16, 64, 128, 512, 4, 4, 2, 1)
+    GV("vwg2 128x128 8w", 16, 64, 128, 512, 2, 4, 4, 2)
+    GV("vwg4 128x128 4w", 8, 256, 256, 128, 4, 4, 2, 2)
+    GV("vwg4 128x256 8w", 8, 256, 256, 128, 4, 4, 2, 4)
+    GV("vwg4 256x128 8w", 8, 256, 256, 128, 4, 4, 4, 2)
+    GV("vwg6 128x128 4w", 4, 512, 512, 32, 4, 4, 2, 2)
+    GV("vwg6 128x256 8w", 4, 512, 512, 32, 4, 4, 2, 4)
+    GV("vwg6 256x128 8w", 4, 512, 512, 32, 4, 4, 4, 2)
     return 0;
 }
