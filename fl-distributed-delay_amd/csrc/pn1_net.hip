@@ -375,13 +375,13 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC((conv_like<14, 14, 192, 0, 4, 3, 4, 2, EpiMask<true>, 13>(dz6, S, g.wd[5], 192, 1728,
         EpiMask<true>{w.gx, w.a5, S * 13 * 13, 192}, st, K_DG6, 1728)));
     float* dz5 = w.gx;
-    // ---- conv5: wgrad (input d2), bias, dgrad -> grad wrt d2 (dropout site 2) into gy ----
+    // ---- conv5: wgrad (input d2), bias, dgrad -> grad wrt d2 (dropout site 2), scattered through
+    //      pool2 straight into dz4 (a4 buffer; EpiDropScatter, no gy round trip) ----
     RC((conv_wgrad<11, 11, 96, 2, 6, 3, 2, 2>(dz5, w.d2, S, 192, 864, g.sw[4], g.sb[4], GEO[4].ZW,
                                              st, K_WG5, 864, zi(4),
                                              &zu[4])));
     RC((conv_like<13, 13, 192, 0, 4, 3, 2, 2>(dz5, S, g.wd[4], 96, 1728,
-        EpiDropMask{w.gy, w.d2, s25, S * 11 * 11, 96}, st, K_DG5, 1728)));
-    RC((pool_scatter<22, 22, 96, false>(w.gy, w.i2, w.a4, S, st)));
+        EpiDropScatter<11, 11>{w.a4, w.d2, w.i2, s25, S * 11 * 11, 96}, st, K_DG5, 1728)));
     float* dz4 = w.a4;
     // ---- conv4: wgrad (input a3), bias, dgrad -> dz3 = . * (a3 > 0) into gx ----
     RC((conv_wgrad<20, 20, 96, 2, 3, 3, 2, 2>(dz4, w.a3, S, 96, 864, g.sw[3], g.sb[3], GEO[3].ZW,
@@ -390,13 +390,13 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC((conv_like<22, 22, 96, 0, 4, 3, 2, 2>(dz4, S, g.wd[3], 96, 864,
         EpiMask<true>{w.gx, w.a3, S * 20 * 20, 96}, st, K_DG4, 864)));
     float* dz3 = w.gx;
-    // ---- conv3: wgrad (input d1), bias, dgrad -> grad wrt d1 (site 1) into gy ----
+    // ---- conv3: wgrad (input d1), bias, dgrad -> grad wrt d1 (site 1), scattered through pool1
+    //      straight into dz2 (a2 buffer) ----
     RC((conv_wgrad<18, 18, 48, 2, 3, 3, 2, 1>(dz3, w.d1, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW,
                                              st, K_WG3, 432, zi(2),
                                              &zu[2])));
     RC((conv_like<20, 20, 96, 0, 4, 3, 4, 1>(dz3, S, g.wd[2], 48, 864,
-        EpiDropMask{w.gy, w.d1, s25, S * 18 * 18, 48}, st, K_DG3, 864)));
-    RC((pool_scatter<36, 36, 48, false>(w.gy, w.i1, w.a2, S, st)));
+        EpiDropScatter<18, 18>{w.a2, w.d1, w.i1, s25, S * 18 * 18, 48}, st, K_DG3, 864)));
     float* dz2 = w.a2;
     // ---- conv2: wgrad (input a1), bias, dgrad -> dz1 = . * (a1 > 0) into gx ----
     RC((conv_wgrad<34, 34, 48, 2, 3, 3, 1, 1>(dz2, w.a1, S, 48, 432, g.sw[1], g.sb[1], GEO[1].ZW,
