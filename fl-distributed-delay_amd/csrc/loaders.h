@@ -587,6 +587,54 @@ struct EpiDropScatter {
     }
 };
 
+// EpiDropScatter staged through LDS (gemm_core.h STAGED, the block covers all NC channels): a
+// thread takes (pooled row, 4 channels) and writes the four positions of its 2x2 window as float4
+// pieces of whole dZ pixel rows, instead of 16 scalar stores per lane
+template <int PH, int PW, int NC>
+struct EpiDropScatterRows {
+    static constexpr bool ASUM = false;
+    static constexpr bool STAGED = true;
+    static constexpr int NCOL = NC;
+    static_assert(NC % 4 == 0, "float4 rows");
+    float* dZ;
+    const float* act;
+    const uint8_t* idx;
+    float scale;
+    int M;
+    __device__ float value(int, float v) const { return v; }
+    __device__ void store_rows(const float* tile, int ld, int m0, int bm, int tid, int nt) const {
+        const int rows = M - m0 < bm ? M - m0 : bm;
+        constexpr int N4 = NC / 4;
+        const f32x4* a4 = reinterpret_cast<const f32x4*>(act + (long)m0 * NC);
+        const uint32_t* i4 = reinterpret_cast<const uint32_t*>(idx + (long)m0 * NC);
+        for (int q = tid; q < rows * N4; q += nt) {
+            const int r = q / N4, c = q - r * N4;
+            const f32x4 t = *reinterpret_cast<const f32x4*>(tile + r * ld + 4 * c);
+            const f32x4 a = a4[q];
+            const uint32_t id = i4[q];
+            f32x4 g;
+            g.x = a.x > 0.f ? t.x * scale : 0.f;
+            g.y = a.y > 0.f ? t.y * scale : 0.f;
+            g.z = a.z > 0.f ? t.z * scale : 0.f;
+            g.w = a.w > 0.f ? t.w * scale : 0.f;
+            const unsigned mm = (unsigned)(m0 + r);
+            const unsigned img = mm / (PH * PW);
+            const unsigned rem = mm - img * (PH * PW);
+            const unsigned ph = rem / PW, pw = rem - ph * PW;
+            float* base = dZ + (((long)img * (2 * PH) + 2 * ph) * (2 * PW) + 2 * pw) * NC + 4 * c;
+#pragma unroll
+            for (int pos = 0; pos < 4; ++pos) {
+                f32x4 o;
+                o.x = (id & 0xffu) == (uint32_t)pos ? g.x : 0.f;
+                o.y = ((id >> 8) & 0xffu) == (uint32_t)pos ? g.y : 0.f;
+                o.z = ((id >> 16) & 0xffu) == (uint32_t)pos ? g.z : 0.f;
+                o.w = (id >> 24) == (uint32_t)pos ? g.w : 0.f;
+                st_nt4(base + ((pos >> 1) * (2 * PW) + (pos & 1)) * (long)NC, o);
+            }
+        }
+    }
+};
+
 // split-K partial slab, accumulated across chunks: S[z][m][n] += acc   (one owner per element);
 // with Bsl != nullptr also the bias gradient Bsl[z][m] += column sum of the dZ tile (ASUM)
 // zinit: slab rows z >= zinit have not been written yet this epoch (begin_epoch does not clear

@@ -381,7 +381,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
                                              st, K_WG5, 864, zi(4),
                                              &zu[4])));
     RC((conv_like<13, 13, 192, 0, 4, 3, 2, 2>(dz5, S, g.wd[4], 96, 1728,
-        EpiDropScatter<11, 11>{w.a4, w.d2, w.i2, s25, S * 11 * 11, 96}, st, K_DG5, 1728)));
+        EpiDropScatterRows<11, 11, 96>{w.a4, w.d2, w.i2, s25, S * 11 * 11}, st, K_DG5, 1728)));
     float* dz4 = w.a4;
     // ---- conv4: wgrad (input a3), bias, dgrad -> dz3 = . * (a3 > 0) into gx ----
     RC((conv_wgrad<20, 20, 96, 2, 3, 3, 2, 2>(dz4, w.a3, S, 96, 864, g.sw[3], g.sb[3], GEO[3].ZW,
@@ -396,7 +396,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
                                              st, K_WG3, 432, zi(2),
                                              &zu[2])));
     RC((conv_like<20, 20, 96, 0, 4, 3, 4, 1>(dz3, S, g.wd[2], 48, 864,
-        EpiDropScatter<18, 18>{w.a2, w.d1, w.i1, s25, S * 18 * 18, 48}, st, K_DG3, 864)));
+        EpiDropScatterRows<18, 18, 48>{w.a2, w.d1, w.i1, s25, S * 18 * 18}, st, K_DG3, 864)));
     float* dz2 = w.a2;
     // ---- conv2: wgrad (input a1), bias, dgrad -> dz1 = . * (a1 > 0) into gx ----
     RC((conv_wgrad<34, 34, 48, 2, 3, 3, 1, 1>(dz2, w.a1, S, 48, 432, g.sw[1], g.sb[1], GEO[1].ZW,
