@@ -292,6 +292,15 @@ int main(int argc, char** argv) {
     F("dg2b 128x48 4w", 36, 48, 0, 48, 2, 3, 4, 1, 1, 0)
     F("fwd2b 128x48 4w", 34, 48, 2, 48, 2, 3, 4, 1, 1, 0)
     F("fwd2b 128x48 2w", 34, 48, 2, 48, 4, 3, 2, 1, 1, 0)
+    F("fwd2c 256x48 4w", 34, 48, 2, 48, 4, 3, 4, 1, 1, 0)
+    F("fwd2c 192x48 4w", 34, 48, 2, 48, 3, 3, 4, 1, 1, 0)
+    F("fwd2c 128x48 4w", 34, 48, 2, 48, 2, 3, 4, 1, 1, 0)
+    F("fwd2c 256x48 8w", 34, 48, 2, 48, 2, 3, 8, 1, 1, 0)
+    F("fwd2c 192x48 6w", 34, 48, 2, 48, 2, 3, 6, 1, 1, 0)
+    F("dg2c 256x48 4w", 36, 48, 0, 48, 4, 3, 4, 1, 1, 0)
+    F("dg2c 192x48 4w", 36, 48, 0, 48, 3, 3, 4, 1, 1, 0)
+    F("dg2c 128x48 4w", 36, 48, 0, 48, 2, 3, 4, 1, 1, 0)
+    F("dg2c 192x48 6w", 36, 48, 0, 48, 2, 3, 6, 1, 1, 0)
     // vgg11 (padding 1), the product's 128x128 4-wave tile against others
     F("vfwd2 128x128 4w", 16, 64, 1, 128, 4, 4, 2, 2, 1, 0)
     F("vfwd2 128x128 8w", 16, 64, 1, 128, 2, 4, 4, 2, 1, 0)
