@@ -26,6 +26,10 @@
 #include "probe.h"
 #include "slabstep.h"
 
+#ifndef FLSIM_SEQ_EARLY_EXIT
+#define FLSIM_SEQ_EARLY_EXIT 1
+#endif
+
 namespace flsim {
 
 constexpr int NYR = 8;          // entry arrays staged per thread (LDS); the rest load on demand
@@ -590,6 +594,32 @@ __device__ __forceinline__ void slab_step_body(const StepArgs& A, float* lds) {
             for (int q = 0; q < NYR; ++q)
                 if (q < nst) lds[L_Y + q * 256 + tid] = valid ? ys[q] : 0.f;
             if (!__syncthreads_or(tail) && A.R.narr <= NYR) {
+#if FLSIM_SEQ_EARLY_EXIT
+                if (tile + 1 == t_end) {
+                    // the unit's last tile: waves 1..3 leave now (their slots go to the next
+                    // streaming blocks instead of idling at a barrier through the program); wave
+                    // 0 interprets and stores its four elements per lane itself
+                    if (tid >= 64) return;
+                    const f32x4* l4 = reinterpret_cast<const f32x4*>(lds);
+                    auto yf4 = [&](int q) -> f32x4 { return l4[(L_Y + q * 256) / 4 + tid]; };
+                    const f32x4 sum = casc_run_macro<true>(
+                        prog, 0, casc_values(l4[L_S / 4 + tid], A.R.info.need, A.R.info.lp), yf4);
+                    const f32x4 pp = l4[L_P / 4 + tid], mm = l4[L_M / 4 + tid],
+                                vv = l4[L_V / 4 + tid];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        long tk;
+                        if (!col_to_param(g, (long)tile * 256 + 4 * tid + k, tk)) continue;
+                        float p1 = pp[k], m1 = mm[k], v1 = vv[k];
+                        adam_elem(A.ac, sum[k], p1, m1, v1);
+                        const long ek = g.toff + tk;
+                        A.p[ek] = p1;
+                        A.m[ek] = m1;
+                        A.v[ek] = v1;
+                    }
+                    return;
+                }
+#endif
                 if (tid < 64) {
                     const f32x4* l4 = reinterpret_cast<const f32x4*>(lds);
                     auto yf4 = [&](int q) -> f32x4 { return l4[(L_Y + q * 256) / 4 + tid]; };
