@@ -557,39 +557,11 @@ struct EpiDropMask {
 // the full-resolution dZ at the position the forward's argmax recorded (idx, 2 dy + dx), zeros to
 // the other three, instead of being written as gy and scattered by k_pool_scatter.  The values
 // are the same floats; the pooled gradient never goes through HBM.  m = (img * PH + ph) * PW + pw;
-// dZ is [img][2 PH][2 PW][N] (no floor-mode border: both maps are even).
-template <int PH, int PW>
-struct EpiDropScatter {
-    static constexpr bool ASUM = false;
-    float* dZ;
-    const float* act;
-    const uint8_t* idx;
-    float scale;
-    int M, N;
-    __device__ void apply4(int m, int n, int z, f32x4 v) const {
-        if (n >= N) return;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int mm = m + r;
-            if (mm >= M) continue;
-            const long o = (long)mm * N + n;
-            const float g = act[o] > 0.f ? v[r] * scale : 0.f;
-            const int p = idx[o];
-            const unsigned img = (unsigned)mm / (PH * PW);
-            const unsigned rem = (unsigned)mm - img * (PH * PW);
-            const unsigned ph = rem / PW, pw = rem - ph * PW;
-            float* base = dZ + (((long)img * (2 * PH) + 2 * ph) * (2 * PW) + 2 * pw) * N + n;
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                __builtin_nontemporal_store(p == q ? g : 0.f,
-                                            base + ((q >> 1) * (2 * PW) + (q & 1)) * (long)N);
-        }
-    }
-};
-
-// EpiDropScatter staged through LDS (gemm_core.h STAGED, the block covers all NC channels): a
-// thread takes (pooled row, 4 channels) and writes the four positions of its 2x2 window as float4
-// pieces of whole dZ pixel rows, instead of 16 scalar stores per lane
+// dZ is [img][2 PH][2 PW][NC] (no floor-mode border: both maps are even).  The tile is staged
+// through LDS (gemm_core.h STAGED, the block covers all NC channels): a thread takes (pooled pixel,
+// 4 channels) and writes the four positions of its 2x2 window as float4 pieces of whole dZ pixel
+// rows (profiles/r02j: 16 scalar stores per lane from the accumulator layout were 10 % slower on
+// conv3's data gradient)
 template <int PH, int PW, int NC>
 struct EpiDropScatterRows {
     static constexpr bool ASUM = false;

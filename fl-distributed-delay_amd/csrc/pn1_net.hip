@@ -376,7 +376,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
         EpiMask<true>{w.gx, w.a5, S * 13 * 13, 192}, st, K_DG6, 1728)));
     float* dz5 = w.gx;
     // ---- conv5: wgrad (input d2), bias, dgrad -> grad wrt d2 (dropout site 2), scattered through
-    //      pool2 straight into dz4 (a4 buffer; EpiDropScatter, no gy round trip) ----
+    //      pool2 straight into dz4 (a4 buffer; EpiDropScatterRows, no gy round trip) ----
     RC((conv_wgrad<11, 11, 96, 2, 6, 3, 2, 2>(dz5, w.d2, S, 192, 864, g.sw[4], g.sb[4], GEO[4].ZW,
                                              st, K_WG5, 864, zi(4),
                                              &zu[4])));
