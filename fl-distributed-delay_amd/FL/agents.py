@@ -80,6 +80,7 @@ class _ModelContext:
         self.step = 0
         self.loss_buf = torch.zeros(64, device=dev)
         self.stager = ProgramStager(dev)
+        self.users = {}          # Worker.index -> id(Worker) of this epoch's fwd_bkwd calls
 
     def _alias_buffers(self, model):
         """BatchNorm running buffers become views of the engine's device buffer (loaded from the
@@ -115,8 +116,20 @@ class _ModelContext:
         if cw > self.loss_buf.numel():
             self.loss_buf = torch.zeros(cw, device=self.device)
 
+    def claim(self, worker):
+        """Dropout keys are (epoch, Worker.index): two different Worker objects computing with
+        the same index in one epoch would draw identical masks.  That happens only when the
+        indices were reset under live workers (a second Central built after them, or workers
+        built before the Central), so it is refused instead of silently correlating the masks."""
+        prev = self.users.setdefault(worker.index, id(worker))
+        if prev != id(worker):
+            raise ValueError(f"two Workers share index {worker.index} in one epoch (Worker "
+                             "indices restart at 0 when a Central is built: build the Central "
+                             "first, then the workers, as main.py:110-113 does)")
+
     def new_epoch(self):
         self.t += 1
+        self.users = {}
         self.G = None
         self.carry = None
         self.packed = False
@@ -238,6 +251,7 @@ class Worker:
                 getattr(self.loss, "reduction", "mean") != "mean":
             raise NotImplementedError("fused loss implements nn.CrossEntropyLoss(mean)")
         ctx = _context(self.model)
+        ctx.claim(self)
         n = int(inp.shape[0])
         if int(outp.shape[0]) != n:
             raise ValueError(f"Expected input batch_size ({n}) to match target batch_size "

@@ -40,8 +40,16 @@ def imshow(img):
 
 def print_test_accuracy(model, testloader):
     """util.py:31-45: top-1 accuracy (%) of `model` over `testloader` (batches of
-    (images NCHW float, labels)), predictions = first maximum of the logits."""
+    (images NCHW float, labels)), predictions = first maximum of the logits.
+
+    The device forward is the eval-mode one (dropout off, BatchNorm from the running buffers),
+    which is how main.py:190 calls it (central.model.eval() first).  The reference would run
+    model(images) in train mode too (random dropout masks, batch statistics); that is refused
+    here rather than silently evaluated in eval mode."""
     from FL.agents import _context
+    if model.training:
+        raise NotImplementedError("print_test_accuracy on the HIP engine evaluates in eval mode: "
+                                  "call model.eval() first (main.py:190)")
     ctx = _context(model)
     correct = 0
     total = 0

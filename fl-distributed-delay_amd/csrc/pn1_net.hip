@@ -317,7 +317,9 @@ static int forward(const GradState& g, const WS& w, const float* theta, int S,
 // yet written this epoch and accumulate into the others (EpiSlabAcc::zinit), and the epoch's
 // slab sum reads only the written rows (SlabSeg::zlim).  Small chunks use fewer rows (wsplit), so
 // an n = 10 epoch no longer pays a 0.3 ms clear and a full 1.9 GB read.  Keyed by the gradstate
-// address; a gradstate whose epoch was not begun in this process falls back to "every row".
+// address; the entry is created by begin_epoch and erased by flsim_pn1_release (engine teardown),
+// and a backward pass on a gradstate without one is refused: the slab rows would otherwise be
+// read or accumulated without ever having been written.
 struct EpochRows {
     int z[8];
 };
@@ -457,6 +459,13 @@ int flsim_pn1_begin_epoch(void* gradstate, const float* theta, hipStream_t strea
     return 0;
 }
 
+// forget the gradstate's slab-row table (the engine that owns the buffer is going away; the
+// caching allocator may hand the same address to a new engine)
+void flsim_pn1_release(void* gradstate) {
+    std::lock_guard<std::mutex> lk(g_rows_mu);
+    g_rows.erase(gradstate);
+}
+
 static int run_chunk(void* gradstate, const WS& w, const float* theta, const WorkerRec* workers,
                      int n_chunk_workers, uint64_t seed, int dropout, int backward_pass,
                      float* worker_loss, hipStream_t stream,
@@ -468,7 +477,11 @@ static int run_chunk(void* gradstate, const WS& w, const float* theta, const Wor
     RC(head_and_loss<256>(w.e2, theta + P_OFF[16], theta + P_OFF[17], w.y, w.loss_s, w.dlog, w.dh2,
                           S, backward_pass, dropout ? SCALE_P50 : 1.f, gscale, worker_loss,
                           stream));
-    if (backward_pass) RC(backward(g, w, theta, S, dropout, stream, epoch_rows(gradstate)));
+    if (backward_pass) {
+        EpochRows* er = epoch_rows(gradstate);
+        FLSIM_REQUIRE(er, "backward pass without flsim_pn1_begin_epoch on this gradstate");
+        RC(backward(g, w, theta, S, dropout, stream, er));
+    }
     return 0;
 }
 

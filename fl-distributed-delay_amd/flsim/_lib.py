@@ -32,7 +32,7 @@ EXPORTS = [
     "flsim_aggregate_adam", "flsim_aggregate_adam_rule", "flsim_aggregate_adam_sum",
     "flsim_cascade_program", "flsim_cascade_eval_host",
     "flsim_probe_enable", "flsim_probe_read", "flsim_probe_disable",
-    "flsim_probe_kernel_count", "flsim_probe_kernel_name",
+    "flsim_probe_kernel_count", "flsim_probe_kernel_name", "flsim_pn1_release",
 ]
 
 
@@ -97,6 +97,8 @@ def lib():
         f("eval_pool").argtypes = [vp, vp, ctypes.c_int, vp, vp, ctypes.c_int, ctypes.c_int,
                                    vp] + bn + [vp, vp]
     L.flsim_vgg11_bn_update_running.argtypes = [vp, vp, ctypes.c_int, vp]
+    L.flsim_pn1_release.argtypes = [vp]
+    L.flsim_pn1_release.restype = None
     L.flsim_aggregate_adam.argtypes = [
         vp, ctypes.c_int, vp, ctypes.c_int, vp, vp, vp, ctypes.c_long, vp, ctypes.c_int,
         ctypes.c_long, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp]

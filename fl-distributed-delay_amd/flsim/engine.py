@@ -102,6 +102,16 @@ class NetEngine:
     def _fn(self, name):
         return getattr(lib(), f"flsim_{self.PREFIX}_{name}")
 
+    def __del__(self):
+        # the caching allocator may give this gradstate's address to a later engine: the
+        # library's slab-row table for it must not outlive the buffer (flsim_pn1_release)
+        gs = getattr(self, "gradstate", None)
+        try:
+            if gs is not None and hasattr(lib(), f"flsim_{self.PREFIX}_release"):
+                self._fn("release")(ptr(gs))
+        except Exception:      # interpreter teardown: the library may already be gone
+            pass
+
     # -- per-epoch gradient --------------------------------------------------------------------
     def begin_epoch(self, theta):
         check(self._fn("begin_epoch")(ptr(self.gradstate), ptr(theta), stream_ptr()))

@@ -26,6 +26,9 @@ from .engine import PN1_SIZES, ProgramStager, Rule, engine_class, padded, split_
 from .schedule import Schedule, reference_delays
 
 SEMANTICS = ("reference", "torch1", "independent")
+# checkpoint format: 2 records the model, the optimizer hyper-parameters and the throttle cap, and
+# the reference's --delay 0 slow worker as DELAY_ZERO (restore() migrates format 1)
+CKPT_FORMAT = "flsim-checkpoint-2"
 
 
 def default_theta(seed=0, model="PerformantNet1"):
@@ -397,7 +400,7 @@ class FLSimulation:
         if self.semantics == "independent":
             raise NotImplementedError("checkpoint of the independent-entry semantics")
         return {
-            "format": "flsim-checkpoint-1",
+            "format": CKPT_FORMAT,
             "config": {"n": self.n, "delays": torch.from_numpy(self.delays.copy()),
                        "model": self.model,
                        "throttle": self.throttle, "seed": self.seed, "semantics": self.semantics,
@@ -420,17 +423,30 @@ class FLSimulation:
         weights_only=True).  The simulation must be fresh and built with the same config."""
         if isinstance(ck, (str, bytes)) or hasattr(ck, "__fspath__"):
             ck = torch.load(ck, map_location="cpu", weights_only=True)
-        if ck.get("format") != "flsim-checkpoint-1":
+        fmt = ck.get("format")
+        if fmt not in (CKPT_FORMAT, "flsim-checkpoint-1"):
             raise ValueError("not an flsim checkpoint")
-        cfg = ck["config"]
+        cfg = dict(ck["config"])
         mine = {"n": self.n, "throttle": self.throttle, "seed": self.seed,
                 "semantics": self.semantics, "dropout": self.dropout, "model": self.model,
                 "lr": self.lr, "betas": list(self.betas), "eps": self.eps,
                 "max_throttle": self.max_throttle}
+        delays = cfg["delays"].numpy().astype(np.int32)
+        if fmt == "flsim-checkpoint-1":
+            # format 1 (round 1) had no model / optimizer / throttle-cap keys (they were the
+            # defaults) and stored the slow worker of --delay 0 as 0 (now DELAY_ZERO)
+            import warnings
+            from .schedule import DELAY_ZERO
+            for k, v in (("model", "PerformantNet1"), ("lr", 1e-3), ("betas", [0.9, 0.999]),
+                         ("eps", 1e-8), ("max_throttle", 32)):
+                if k not in cfg:
+                    cfg[k] = v
+                    warnings.warn(f"format-1 checkpoint: {k} not recorded, taken as {v!r}")
+            delays = np.where((delays == 0) & (self.delays == DELAY_ZERO), DELAY_ZERO, delays)
         for k, v in mine.items():
-            if cfg.get(k, "PerformantNet1" if k == "model" else None) != v:
+            if cfg.get(k) != v:
                 raise ValueError(f"checkpoint {k}={cfg.get(k)!r} differs from this run ({v!r})")
-        if not np.array_equal(cfg["delays"].numpy(), self.delays):
+        if not np.array_equal(delays, self.delays):
             raise ValueError("checkpoint delays differ from this run")
         if self.trace:
             raise ValueError("restore() needs a fresh simulation")

@@ -82,6 +82,10 @@ int flsim_pn1_fwd_bwd_input(void* gradstate, void* workspace, int max_samples, c
                             const WorkerRec* workers, uint64_t seed, int dropout,
                             int backward_pass, float* worker_loss, flsim_stream_t stream);
 int flsim_pn1_end_epoch(void* gradstate, float* grad_out, flsim_stream_t stream);
+/* the gradstate's buffer is about to be freed: drop the library's per-gradstate bookkeeping (the
+ * slab rows written this epoch).  A backward pass on a gradstate with no flsim_pn1_begin_epoch
+ * since creation or release fails with status 1. */
+void flsim_pn1_release(void* gradstate);
 /* eval of an explicit batch (util.py:31-45 print_test_accuracy's model(images), dropout off):
  * x NCHW fp32 [n_images][3][32][32] -> pred (device int32[n_images]) */
 int flsim_pn1_eval_input(void* gradstate, void* workspace, int max_samples, const float* theta,

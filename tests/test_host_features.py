@@ -117,6 +117,33 @@ def test_restore_rejects_other_hyperparameters():
             b.restore(ck)
 
 
+def test_restore_migrates_format_1_checkpoints():
+    """A round-1 checkpoint (format 1: no model / optimizer / throttle-cap keys, the --delay 0
+    slow worker stored as delay 0) restores into a run with the defaults, with a warning."""
+    a = _sim(11, 3, True)
+    for _ in range(4):
+        a.epoch()
+    ck = a.checkpoint()
+    assert ck["format"] == "flsim-checkpoint-2"
+    old = dict(ck, format="flsim-checkpoint-1")
+    old["config"] = {k: v for k, v in ck["config"].items()
+                     if k not in ("model", "lr", "betas", "eps", "max_throttle")}
+    b = _sim(11, 3, True)
+    with pytest.warns(UserWarning, match="format-1"):
+        b.restore(old)
+    a.epoch()
+    b.epoch()
+    assert np.array_equal(a.theta.numpy().view(np.uint32), b.theta.numpy().view(np.uint32))
+    z = _sim(5, 0, False)
+    z.epoch()
+    ck0 = z.checkpoint()
+    old0 = dict(ck0, format="flsim-checkpoint-1")
+    old0["config"] = dict(ck0["config"], delays=torch.zeros(5, dtype=torch.int32))
+    _sim(5, 0, False).restore(old0)          # delay 0 maps onto DELAY_ZERO
+    with pytest.raises(ValueError):
+        _sim(5, 0, False).restore(dict(ck0, format="something-else"))
+
+
 def test_delay_zero_is_the_reference_slow_worker():
     """--delay 0 (main.py:150-158): worker n-1 is still the slow one -- it computes and pushes
     at t = 0 without an entry or a logged loss -- and t = 1 raises ZeroDivisionError (t % 0)."""
@@ -141,3 +168,29 @@ def test_fl_util_drop_in_names():
     exec("from FL.util import *", ns)
     for name in ("save_data", "plot_data", "imshow", "print_test_accuracy", "check_mem"):
         assert callable(ns[name]), name
+
+
+def test_print_test_accuracy_refuses_train_mode():
+    """The device evaluation is eval-mode only (main.py:190 calls model.eval() first)."""
+    from FL.models import PerformantNet1
+    from FL.util import print_test_accuracy
+    m = PerformantNet1()
+    m.train()
+    with pytest.raises(NotImplementedError):
+        print_test_accuracy(m, [])
+
+
+def test_worker_index_reuse_is_refused():
+    """Two Worker objects with one index in one epoch would share dropout keys: refused."""
+    from FL.agents import Worker, _ModelContext
+
+    class Ctx:
+        users = {}
+    claim = _ModelContext.claim
+    a, b = Worker(torch.nn.CrossEntropyLoss()), Worker(torch.nn.CrossEntropyLoss())
+    b.index = a.index
+    ctx = Ctx()
+    claim(ctx, a)
+    claim(ctx, a)                 # the same worker again is not a reuse
+    with pytest.raises(ValueError):
+        claim(ctx, b)
