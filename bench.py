@@ -81,6 +81,9 @@ def parse():
                     help="warm start (main.py:98-100): a models.py state_dict, e.g. configs[1]'s "
                          "warm_start.pt from tools/make_warm_start.py")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-stream", action="store_true",
+                    help="skip timing the post-all-reduce server step (k_agg_stream) after the "
+                         "timed window at N = 1")
     ap.add_argument("--no-probe", action="store_true")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI). gloo is for "
@@ -173,6 +176,48 @@ def cpu_baseline(n, delay, throttle, model="PerformantNet1", configs0_epochs=3):
                 host=info, configs0=c0)
 
 
+def stream_step_probe(sim, iters=20):
+    """The server step every N > 1 run ends its epochs with, timed on this GPU after the timed
+    window (untimed for `value`): rule() + Adam from S_t in a buffer, the stream that follows the
+    all-reduce (flsim_aggregate_adam_rule_push), on copies of the run's theta / m / v, for the
+    reference's two entry lists at n = 1024: a plain throttled epoch (k = c_t = 512) and the tick
+    epoch t = d (c_t = 512 + the stale S_{t-d}, the FIFO slot written in the same pass).  Bytes:
+    SURVEY 8(d) 4P (1 + stale + 6) (+ 4P for the slot write).  Launch times from the probe."""
+    from flsim._lib import KernelProbe
+    from flsim.engine import Rule
+    P, dev = sim.P, sim.device
+    S = torch.randn(sim.Ppad, device=dev, generator=torch.Generator(device=dev).manual_seed(1))
+    S.mul_(1e-3)
+    st = S.flip(0).contiguous()
+    slot = torch.empty_like(S)
+    p, m, v = sim.theta.clone(), sim.m.clone(), sim.v.clone()
+    out = {}
+    for name, rule, so, nbytes in (
+            ("plain_k512", Rule(512, [], c=512), None, 4 * P * 7),
+            ("tick_k513_fifo", Rule(513, [st], c=512), slot, 4 * P * 9)):
+        for _ in range(3):
+            sim.engine.aggregate_rule(S, rule, p, m, v, max(sim.step, 1), S_out=so)
+        torch.cuda.synchronize()
+        pr = KernelProbe(capacity=4096)
+        for _ in range(iters):
+            sim.engine.aggregate_rule(S, rule, p, m, v, max(sim.step, 1), S_out=so)
+        torch.cuda.synchronize()
+        rec = pr.read().get("aggregate_adam")
+        pr.close()
+        if not rec:
+            continue
+        cnt, ms, _ = rec
+        us = ms / cnt * 1e3
+        out[name] = dict(avg_launch_us=round(us, 2), bytes=nbytes,
+                         bytes_8d=4 * P * (7 + (1 if so is not None else 0)),
+                         achieved=round(nbytes / us / 1e3, 1), unit="GB/s",
+                         frac=round(nbytes / us / 1e3 / HBM_PEAK_GBPS, 4),
+                         frac_8d=round(4 * P * (7 + (1 if so is not None else 0)) / us / 1e3 /
+                                       HBM_PEAK_GBPS, 4))
+    return dict(kernel="k_agg_stream_reg (rule() + Adam from S_t after the all-reduce)",
+                bound="hbm", peak=HBM_PEAK_GBPS, **out) if out else None
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -215,23 +260,39 @@ def main():
         sim.epoch(sync_loss=False)
     torch.cuda.synchronize()
     probe = None if args.no_probe else KernelProbe(capacity=64 * 1024)
+    sim.time_collective = world > 1
+    sim.rank_worker_steps = []
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
+    # per-epoch device time from events on the compute stream (no host synchronisation in the
+    # window): which timed epochs hold a tick and what the steady-state epochs alone achieve
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
+    evs[0].record()
     ws = 0
-    for _ in range(args.steps):
+    for j in range(args.steps):
         sim.epoch(sync_loss=False)
         ws += int(sim.trace[-1].computes.sum())
+        evs[j + 1].record()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
+    epoch_ms = [evs[j].elapsed_time(evs[j + 1]) for j in range(args.steps)]
+    coll_ms = sim.collective_ms()
+    rank_ws = int(sum(sim.rank_worker_steps))
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     losses = sim.losses()
+    rank_ws_all = [rank_ws]
+    if world > 1:
+        t = torch.tensor([rank_ws], device=dev, dtype=torch.int64)
+        g = [torch.zeros_like(t) for _ in range(world)]
+        torch.distributed.all_gather(g, t)
+        rank_ws_all = [int(x.item()) for x in g]
 
     kern = probe.read() if probe else {}
     if probe:
@@ -290,6 +351,44 @@ def main():
             rus = traffic["trace_avg_ns"] / 1e3
             agg.update(rocprof_avg_launch_us=round(rus, 2))
 
+    # the timed epochs one by one: a tick epoch (t % d == 0: the slow worker computes and its
+    # stale entry joins rule()) and the epoch after it (every fast worker computes) are marked;
+    # steady_state = the other epochs alone
+    window = []
+    for j, plan in enumerate(sim.trace[-args.steps:]):
+        prev = sim.trace[-args.steps + j - 1] if len(sim.trace) > args.steps - j else None
+        window.append(dict(t=int(plan.t), worker_steps=int(plan.computes.sum()),
+                           ms=round(epoch_ms[j], 3), tick=bool(plan.stale),
+                           after_tick=bool(prev is not None and prev.stale)))
+    steady = [w for w in window if not w["tick"] and not w["after_tick"]]
+    steady_state = None
+    if steady:
+        sw, sms = sum(w["worker_steps"] for w in steady), sum(w["ms"] for w in steady)
+        steady_state = dict(epochs=len(steady), worker_steps=sw,
+                            worker_steps_per_s=round(sw / (sms / 1e3), 3),
+                            note="job worker-steps of the timed epochs that are neither a tick "
+                                 "nor the epoch after one / their device time on rank 0")
+    # SURVEY 8(d)'s aggregation bytes for the same launches: 4P (1 + distinct stale + 3 + 3), the
+    # rule() + Adam traffic without the slab reduction the fused step also streams
+    agg8d = None
+    if agg_rec and agg_name in ("slab_step", "slab_step_seq"):
+        P = sim.P
+        ticks = [w for w in window if w["tick"]]
+        cnt, ms, _ = agg_rec
+        b8 = 4.0 * P * (1 + 6) * cnt + 4.0 * P * sum(len({src for _, src in p.stale})
+                                                     for p in sim.trace[-args.steps:])
+        agg8d = dict(kernel=agg["kernel"], bytes_basis="SURVEY 8(d): 4P(1 + distinct stale + 6)",
+                     alg_bytes_per_launch=int(b8 / cnt), avg_launch_us=agg["avg_launch_us"],
+                     achieved=round(b8 / (ms / 1e3) / 1e9, 1), unit="GB/s",
+                     frac=round(b8 / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+                     ticks_in_window=len(ticks),
+                     note="the fused launch also streams the weight-gradient slabs "
+                          "(aggregation.alg_bytes_per_launch); this is the rule()+Adam share "
+                          "priced at the whole launch time")
+    agg_stream = None
+    if world == 1 and probe is not None and args.model == "PerformantNet1" and not args.no_stream:
+        agg_stream = stream_step_probe(sim)
+
     value = ws / elapsed
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -326,6 +425,16 @@ def main():
                                              (MFMA_F32_PEAK_TFLOPS * world), 4),
             "roofline": roofline,
             "aggregation": agg,
+            "aggregation_8d": agg8d,
+            "aggregation_stream": agg_stream,
+            "window": window,
+            "steady_state": steady_state,
+            "collective": (dict(backend=args.backend,
+                                per_epoch_ms=[round(x, 3) for x in coll_ms],
+                                mean_ms=round(float(np.mean(coll_ms)), 3),
+                                bytes_per_epoch=4 * int(sim.comm.numel()))
+                           if coll_ms else None),
+            "rank_worker_steps": rank_ws_all,
             "cpu_baseline": cpu,
             "gpu_vs_cpu": round(value / cpu["value"], 1) if cpu else None,
             "last_loss": losses[-1] if losses else None,

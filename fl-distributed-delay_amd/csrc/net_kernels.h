@@ -7,6 +7,7 @@
 // Wf[co][k(khkw, ci)] (forward) and Wd[ci][k(khkw', co)] = W[co][ci][2-kh'][2-kw'] (data
 // gradient), k in Im2colKC's channel-slice-major order (k_pack_fwd).
 #pragma once
+#include "gemm_direct.h"
 #include "loaders.h"
 #include "pn1.h"
 #include "probe.h"
@@ -26,13 +27,25 @@ k_fill_batch(const uint8_t* __restrict__ pool, const int32_t* __restrict__ label
     const int w = s / SAMPLES_PER_WORKER;
     const int j = s - w * SAMPLES_PER_WORKER;
     const WorkerRec wr = workers[w];
+    // --batch_size B (main.py:43-44): WorkerRec.pad = B (0 = 128); the B samples of worker i span
+    // ceil(B/128) records with i + g * 2^20 (group g); slot j of group g is sample g*128 + j of
+    // the worker's batch, drawn with the worker's own key; slots past B are padding (label -1:
+    // no loss, no gradient; zero image)
+    const uint32_t bsz = wr.pad ? wr.pad : (uint32_t)SAMPLES_PER_WORKER;
+    const uint32_t q = (wr.i >> 20) * SAMPLES_PER_WORKER + (uint32_t)j;
+    float* out = x0 + (long)s * 4096;
+    if (q >= bsz) {
+        if (threadIdx.x == 0) y[s] = -1;
+        for (int p = threadIdx.x; p < 1024; p += 256)
+            *reinterpret_cast<f32x4*>(out + 4 * p) = f32x4{0.f, 0.f, 0.f, 0.f};
+        return;
+    }
     const bool use_b = (int)wr.k == n_workers_total - 1;   // main.py:78-80: last dataset = {1,9}
     const int len = use_b ? len_b : len_a;
-    const uint32_t u = philox_word(seed, wr.t, wr.i, SITE_DATA, (uint32_t)j);
+    const uint32_t u = philox_word(seed, wr.t, wr.i & 0xfffffu, SITE_DATA, q);
     const int idx = use_b ? list_b[u % (uint32_t)len] : list_a[u % (uint32_t)len];
     if (threadIdx.x == 0) y[s] = labels[idx];
     const uint8_t* img = pool + (long)idx * 3072;
-    float* out = x0 + (long)s * 4096;
     for (int p = threadIdx.x; p < 1024; p += 256) {
         f32x4 v;
         v.x = lut[img[p]];
@@ -239,7 +252,7 @@ __global__ void __launch_bounds__(256)
 k_head(const float* __restrict__ e2, const float* __restrict__ W3, const float* __restrict__ b3,
        const int32_t* __restrict__ y, float* __restrict__ loss_s, float* __restrict__ dlog,
        float* __restrict__ dh2, int S, int backward, float sdrop, float gscale,
-       int32_t* __restrict__ pred, int n_pred) {
+       int32_t* __restrict__ pred, int n_pred, const WorkerRec* __restrict__ workers) {
     constexpr int NC = K / 256;
     static_assert(K % 256 == 0, "head width must be a multiple of 256");
     const int s = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -280,6 +293,11 @@ k_head(const float* __restrict__ e2, const float* __restrict__ W3, const float* 
         pred[s] = am;
     }
     if (!backward) return;
+    // CrossEntropyLoss's mean over the worker's B samples (WorkerRec.pad = B, 0: gscale)
+    if (workers) {
+        const uint32_t b = workers[s / SAMPLES_PER_WORKER].pad;
+        if (b) gscale = 1.f / (float)b;
+    }
     float g[10];
     const float inv = 1.f / se;
 #pragma unroll
@@ -328,9 +346,10 @@ k_worker_loss(const float* __restrict__ loss_s, float* __restrict__ out) {
 template <int K>
 static int head_and_loss(const float* e, const float* W, const float* b, const int32_t* y,
                          float* loss_s, float* dlog, float* dh, int S, int backward, float sdrop,
-                         float gscale, float* worker_loss, hipStream_t st) {
+                         float gscale, float* worker_loss, hipStream_t st,
+                         const WorkerRec* workers = nullptr) {
     hipLaunchKernelGGL(k_head<K>, dim3(ceil_div(S, 4)), dim3(256), 0, st, e, W, b, y, loss_s, dlog,
-                       dh, S, backward, sdrop, gscale, (int32_t*)nullptr, 0);
+                       dh, S, backward, sdrop, gscale, (int32_t*)nullptr, 0, workers);
     FLSIM_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_worker_loss, dim3(S / SAMPLES_PER_WORKER), dim3(128), 0, st, loss_s,
                        worker_loss);
@@ -343,7 +362,8 @@ template <int K>
 static int head_predict(const float* e, const float* W, const float* b, const int32_t* y,
                         float* loss_s, int S, int32_t* pred, int n_pred, hipStream_t st) {
     hipLaunchKernelGGL(k_head<K>, dim3(ceil_div(S, 4)), dim3(256), 0, st, e, W, b, y, loss_s,
-                       (float*)nullptr, (float*)nullptr, S, 0, 1.f, 1.f, pred, n_pred);
+                       (float*)nullptr, (float*)nullptr, S, 0, 1.f, 1.f, pred, n_pred,
+                       (const WorkerRec*)nullptr);
     FLSIM_LAUNCH_CHECK();
     return 0;
 }
@@ -601,6 +621,55 @@ static int launch_gemm(const AL& al, const BL& bl, const EPI& epi, int M, int N,
                           st, ps.start, ps.stop, 0, al, bl, epi, ksteps, per, tm, tn);
     FLSIM_LAUNCH_CHECK();
     return probe_end(ps, kid, alg_flops);
+}
+
+// direct-A GEMM (gemm_direct.h): rows = output pixels loaded per wave straight into MFMA
+// fragments, B (packed weights) staged through LDS KB k-steps at a time
+template <int FM, int FN, int WAVES, int KB, int DEPTH, class AD, class BL, class EPI>
+static int launch_direct(const AD& ad, const BL& bl, const EPI& epi, int M, int N, int ksteps,
+                         hipStream_t st, int kid, double alg_flops) {
+    constexpr int BM = 16 * FM * WAVES, BN = 16 * FN;
+    FLSIM_REQUIRE(ksteps % KB == 0, "direct GEMM: %d k-steps not a multiple of %d", ksteps, KB);
+    const int tm = ceil_div(M, BM), tn = ceil_div(N, BN);
+    const ProbeSlot ps = probe_begin();
+    hipExtLaunchKernelGGL((gemm_direct_kernel<FM, FN, WAVES, KB, DEPTH, AD, BL, EPI>),
+                          dim3(tm * tn), dim3(64 * WAVES), 0, st, ps.start, ps.stop, 0, ad, bl,
+                          epi, ksteps, tm, tn);
+    FLSIM_LAUNCH_CHECK();
+    return probe_end(ps, kid, alg_flops);
+}
+
+// forward conv (also the data-gradient conv) on the direct-A kernel: out[m][n], m < S*OH*OW
+// (WIN: pool-window row order, see Im2colKC; OHX: explicit output size)
+template <int IH, int IW, int CI, int PAD, int FM, int FN, int WAVES, int KB, int DEPTH,
+          bool WIN, int OHX, class EPI>
+static int conv_direct(const float* X, int S, const float* Wpk, int N, int KP, const EPI& epi,
+                       hipStream_t st, int kid, int kreal) {
+    using AD = Im2colDirect<IH, IW, CI, PAD, FM, WIN, OHX>;
+    using BL = RowsKCStage<16 * FN, 64 * WAVES>;
+    AD ad;
+    ad.X = X;
+    ad.M = S * AD::ROWS_PER_IMG;
+    BL bl;
+    bl.P = Wpk;
+    bl.ld = KP;
+    bl.NR = N;
+    return launch_direct<FM, FN, WAVES, KB, DEPTH>(ad, bl, epi, ad.M, N, KP / GK, st, kid,
+                                                   2.0 * ad.M * N * kreal);
+}
+
+// conv_pool_fwd on the direct-A kernel (rows in pool-window order, EpiPoolDrop)
+template <int IH, int IW, int CI, int CO, int PAD, int FM, int FN, int WAVES, int KB, int DEPTH,
+          bool NCHW_OUT>
+static int conv_pool_direct(const float* X, int S, const float* Wpk, int KP, float* d,
+                            uint8_t* idx, const float* bias, const WorkerRec* workers,
+                            uint64_t seed, uint32_t site, uint32_t thr, float scale, int dropout,
+                            hipStream_t st, int kid, int kreal) {
+    using AD = Im2colDirect<IH, IW, CI, PAD, FM, true>;
+    EpiPoolDrop<AD::PH, AD::PW, CO, NCHW_OUT> epi{d, idx, bias, workers, seed, site, thr,
+                                                  scale, dropout, S * AD::ROWS_PER_IMG};
+    return conv_direct<IH, IW, CI, PAD, FM, FN, WAVES, KB, DEPTH, true, 0>(
+        X, S, Wpk, CO, KP, epi, st, kid, kreal);
 }
 
 // Splits of a slab-accumulating GEMM (weight gradients: the reduction runs over the chunk's

@@ -34,7 +34,8 @@ namespace flsim {
 
 constexpr int NYR = 8;          // entry arrays staged per thread (LDS); the rest load on demand
 constexpr int MAX_TAILS = 8;    // tensor tails per streaming launch (host splits longer lists)
-constexpr int MAX_EDGE = 4 * (2 * MAX_TAILS + 2);   // 256-element edge pieces per launch
+constexpr int AGG_GMAX = 2;     // float4 groups per thread of the register-array stream
+constexpr int MAX_EDGE = 4 * AGG_GMAX * (2 * MAX_TAILS + 2);   // 256-element edge pieces per launch
 
 // ---- element arithmetic -----------------------------------------------------------------------
 // Correctly rounded fp32 sqrt.  v_sqrt_f32 is within 1 ulp; the exact residuals x - s'*s of the
@@ -118,6 +119,7 @@ static int stage_program(const RuleProg& R, hipStream_t stream) {
 // ================================================================================================
 struct AggArgs {
     const float* S;
+    float* S_out;                   // nullable: S_t also written here (the FIFO slot at a tick)
     float* p;
     float* m;
     float* v;
@@ -141,8 +143,8 @@ __device__ __forceinline__ bool in_tail(const AggArgs& A, long e) {
     return r;
 }
 
-__device__ __forceinline__ bool block_touch(const AggArgs& A, long blo) {
-    const long bhi = blo + 1024;
+__device__ __forceinline__ bool block_touch(const AggArgs& A, long blo, long span = 1024) {
+    const long bhi = blo + span;
     bool touch = blo < A.lo || bhi > A.hi;
 #pragma unroll
     for (int t = 0; t < MAX_TAILS; ++t)
@@ -175,6 +177,7 @@ __global__ void __launch_bounds__(256) k_agg_stream(AggArgs A) {
         A.p[e] = p;
         A.m[e] = m;
         A.v[e] = v;
+        if (A.S_out) A.S_out[e] = x;
         return;
     }
     const long e0 = 4 * (A.g0 + (long)(blockIdx.x - A.nedge) * 256) + 4 * tid;
@@ -212,6 +215,103 @@ __global__ void __launch_bounds__(256) k_agg_stream(AggArgs A) {
     st(A.p + e0, p);
     st(A.m + e0, m);
     st(A.v + e0, v);
+    if (A.S_out) st(A.S_out + e0, x);
+}
+
+// The reference-order stream with its few entry arrays (NY <= 2: the popped FIFO entries of the
+// reference's one slow worker) held in registers instead of LDS, and G float4 groups per thread
+// (block = 256 * G groups, group j of thread t at 256 j + t: each j is one coalesced sweep).  All
+// of a thread's loads are issued before any arithmetic; no LDS, so 8 blocks of 4 waves fit a CU
+// (the LDS-staged form above holds 32 KB per block: 5).  The interpreter runs once per thread on
+// G * 4 elements in lock step (T = a 4G-wide vector; the program is uniform).  Edge pieces as
+// k_agg_stream (a streaming block covers 1024 G elements).
+template <int G>
+struct AggVec;
+template <>
+struct AggVec<1> { typedef float T __attribute__((ext_vector_type(4))); };
+template <>
+struct AggVec<2> { typedef float T __attribute__((ext_vector_type(8))); };
+
+template <int G, int NY>
+__global__ void __launch_bounds__(256) k_agg_stream_reg(AggArgs A) {
+    typedef typename AggVec<G>::T T;
+    const ProgRef<true> prog{A.R};
+    const int tid = threadIdx.x;
+    if ((int)blockIdx.x < A.nedge) {
+        const long e = A.edge_lo[blockIdx.x] + tid;
+        if (e < A.lo || e >= A.hi) return;
+        const float x = A.S[e];
+        float p = A.p[e], m = A.m[e], v = A.v[e];
+        auto yf = [&](int q) -> float { return A.R.arr[q] ? A.R.arr[q][e] : 0.f; };
+        const CascVals<float> cv = casc_values(x, A.R.info.need, A.R.info.lp);
+        const bool tail = in_tail(A, e);
+        float s = 0.f;
+        if (!tail) s = casc_run_macro(prog, 0, cv, yf);
+        if (tail) s = casc_run_macro(prog, A.R.info.tail_off, cv, yf);
+        adam_elem(A.ac, s, p, m, v);
+        A.p[e] = p;
+        A.m[e] = m;
+        A.v[e] = v;
+        if (A.S_out) A.S_out[e] = x;
+        return;
+    }
+    const long b0 = 4 * (A.g0 + (long)(blockIdx.x - A.nedge) * 256 * G);   // block's first element
+    if (block_touch(A, b0, 1024L * G)) return;
+    auto ld = [](const float* ptr) -> f32x4 {
+        return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(ptr));
+    };
+    auto st = [](float* ptr, f32x4 val) {
+        __builtin_nontemporal_store(val, reinterpret_cast<f32x4*>(ptr));
+    };
+    long e[G];
+#pragma unroll
+    for (int j = 0; j < G; ++j) e[j] = b0 + 1024L * j + 4 * tid;
+    f32x4 xs[G], ps[G], ms[G], vs[G], ys[NY > 0 ? NY : 1][G];
+#pragma unroll
+    for (int q = 0; q < NY; ++q)
+#pragma unroll
+        for (int j = 0; j < G; ++j)
+            ys[q][j] = A.R.arr[q] ? ld(A.R.arr[q] + e[j]) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+        xs[j] = ld(A.S + e[j]);
+        ps[j] = ld(A.p + e[j]);
+        ms[j] = ld(A.m + e[j]);
+        vs[j] = ld(A.v + e[j]);
+    }
+    auto widen = [](const f32x4 (&a)[G]) -> T {
+        T t;
+#pragma unroll
+        for (int j = 0; j < G; ++j)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) t[4 * j + u] = a[j][u];
+        return t;
+    };
+    T yw[NY > 0 ? NY : 1];
+#pragma unroll
+    for (int q = 0; q < NY; ++q) yw[q] = widen(ys[q]);
+    auto yf = [&](int q) -> T {
+        if constexpr (NY == 0) return T(0.f);
+        else if constexpr (NY == 1) return yw[0];
+        else return q == 0 ? yw[0] : yw[1];
+    };
+    const T sum = casc_run_macro<true>(prog, 0, casc_values(widen(xs), A.R.info.need, A.R.info.lp),
+                                       yf);
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            float pp = ps[j][u], mm = ms[j][u], vv = vs[j][u];
+            adam_elem(A.ac, sum[4 * j + u], pp, mm, vv);
+            ps[j][u] = pp;
+            ms[j][u] = mm;
+            vs[j][u] = vv;
+        }
+        st(A.p + e[j], ps[j]);
+        st(A.m + e[j], ms[j]);
+        st(A.v + e[j], vs[j]);
+        if (A.S_out) st(A.S_out + e[j], xs[j]);
+    }
 }
 
 // ================================================================================================
@@ -832,16 +932,37 @@ extern "C" {
 int flsim_aggregate_adam_rule(const float* S, const flsim_rule* rule, float* p, float* m, float* v,
                               long P, const long* tensor_sizes, int n_tensors, long step, double lr,
                               double beta1, double beta2, double eps, hipStream_t stream) {
+    return flsim_aggregate_adam_rule_push(S, nullptr, rule, p, m, v, P, tensor_sizes, n_tensors,
+                                          step, lr, beta1, beta2, eps, stream);
+}
+
+// the same, also writing S_t to S_out (the slow worker's FIFO slot at a tick, main.py:156,161)
+// in the same pass: world > 1 after the all-reduce
+int flsim_aggregate_adam_rule_push(const float* S, float* S_out, const flsim_rule* rule, float* p,
+                                   float* m, float* v, long P, const long* tensor_sizes,
+                                   int n_tensors, long step, double lr, double beta1, double beta2,
+                                   double eps, hipStream_t stream) {
     FLSIM_REQUIRE(S && p && m && v && tensor_sizes && rule, "null pointer");
     FLSIM_REQUIRE(P > 0 && P < (1L << 31), "P = %ld out of range", P);
-    const uintptr_t al = (uintptr_t)S | (uintptr_t)p | (uintptr_t)m | (uintptr_t)v;
-    FLSIM_REQUIRE((al & 15) == 0, "S/p/m/v must be 16-byte aligned");
+    const uintptr_t al = (uintptr_t)S | (uintptr_t)p | (uintptr_t)m | (uintptr_t)v |
+                         (uintptr_t)S_out;
+    FLSIM_REQUIRE((al & 15) == 0, "S/S_out/p/m/v must be 16-byte aligned");
     AggArgs A{};
     RC(make_rule(rule, &A.R));
     for (int q = 0; q < A.R.narr; ++q)
         FLSIM_REQUIRE(((uintptr_t)A.R.arr[q] & 15) == 0, "entry arrays must be 16-byte aligned");
     RC(make_adam_const(rule->k, step, lr, beta1, beta2, eps, &A.ac));
+    // the register-array stream for the reference order with <= 2 entry arrays: 2 float4 groups
+    // per thread without a stale array, 1 with (tools/agg_bench.py, profiles/r03a/agg_bench.txt:
+    // 28.2 vs 28.4 us for k = 512; 32.0 vs 33.1 us for k = 513 with the stale S_{t-d});
+    // FLSIM_AGG_G = 1 / 2 forces a form, 0 the LDS-staged k_agg_stream (measurement only)
+    int agg_g = A.R.narr == 0 ? 2 : 1;
+    if (const char* e = getenv("FLSIM_AGG_G")) agg_g = atoi(e);
+    if (agg_g < 0 || agg_g > AGG_GMAX) agg_g = 1;
+    const bool reg = A.R.prog == nullptr && A.R.narr <= 2 && agg_g > 0;
+    const int G = reg ? agg_g : 1;
     A.S = S;
+    A.S_out = S_out;
     A.p = p;
     A.m = m;
     A.v = v;
@@ -875,34 +996,43 @@ int flsim_aggregate_adam_rule(const float* S, const flsim_rule* rule, float* p, 
         A.hi = hi;
         A.g0 = lo / 4;
         const long groups = (hi + 3) / 4 - A.g0;
-        const long nblk = (groups + 255) / 256;
+        const long gpb = 256L * G;                  // float4 groups per streaming block
+        const long nblk = (groups + gpb - 1) / gpb;
         // edge pieces: the first and last block when they cross the launch range, and every
         // block holding a tail range (host copy of block_touch)
         A.nedge = 0;
         auto add_block = [&](long b) {
-            const long blo = 4 * (A.g0 + b * 256);
-            for (int j = 0; j < A.nedge; j += 4)
+            const long blo = 4 * (A.g0 + b * gpb);
+            for (int j = 0; j < A.nedge; j += 4 * G)
                 if (A.edge_lo[j] == blo) return;
-            for (int j = 0; j < 4; ++j) A.edge_lo[A.nedge++] = blo + 256 * j;
+            for (int j = 0; j < 4 * G; ++j) A.edge_lo[A.nedge++] = blo + 256 * j;
         };
         for (long b : {0L, nblk - 1}) {
-            const long blo = 4 * (A.g0 + b * 256);
-            if (blo < A.lo || blo + 1024 > A.hi) add_block(b);
+            const long blo = 4 * (A.g0 + b * gpb);
+            if (blo < A.lo || blo + 4 * gpb > A.hi) add_block(b);
         }
         for (int j = 0; j < A.ntail; ++j) {
-            const long b0 = (A.tail_lo[j] / 4 - A.g0) / 256;
-            const long b1 = ((A.tail_hi[j] - 1) / 4 - A.g0) / 256;
+            const long b0 = (A.tail_lo[j] / 4 - A.g0) / gpb;
+            const long b1 = ((A.tail_hi[j] - 1) / 4 - A.g0) / gpb;
             for (long b = b0; b <= b1; ++b) add_block(b);
         }
         // algorithmic HBM bytes: read S_t + the distinct entry arrays + p, m, v; write p, m, v
-        const double bytes = 4.0 * (double)(hi - lo) * (7 + A.R.distinct);
+        // [+ S_out]
+        const double bytes = 4.0 * (double)(hi - lo) * (7 + A.R.distinct + (S_out ? 1 : 0));
         const ProbeSlot ps = probe_begin();
-        if (A.R.prog == nullptr)
-            hipExtLaunchKernelGGL(k_agg_stream<true>, dim3((unsigned)(nblk + A.nedge)), dim3(256),
+        const dim3 grid((unsigned)(nblk + A.nedge));
+        if (reg) {
+            auto k = G == 2 ? (A.R.narr == 0 ? k_agg_stream_reg<2, 0>
+                               : A.R.narr == 1 ? k_agg_stream_reg<2, 1> : k_agg_stream_reg<2, 2>)
+                            : (A.R.narr == 0 ? k_agg_stream_reg<1, 0>
+                               : A.R.narr == 1 ? k_agg_stream_reg<1, 1> : k_agg_stream_reg<1, 2>);
+            hipExtLaunchKernelGGL(k, grid, dim3(256), 0, stream, ps.start, ps.stop, 0, A);
+        } else if (A.R.prog == nullptr)
+            hipExtLaunchKernelGGL(k_agg_stream<true>, grid, dim3(256),
                                   0, stream, ps.start, ps.stop, 0, A);
         else {
             RC(stage_program(A.R, stream));
-            hipExtLaunchKernelGGL(k_agg_stream<false>, dim3((unsigned)(nblk + A.nedge)), dim3(256),
+            hipExtLaunchKernelGGL(k_agg_stream<false>, grid, dim3(256),
                                   0, stream, ps.start, ps.stop, 0, A);
         }
         FLSIM_LAUNCH_CHECK();

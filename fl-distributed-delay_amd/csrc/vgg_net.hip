@@ -425,7 +425,7 @@ static int vrun_chunk(void* gradstate, const VWS& w, const float* theta, const W
     RC(vforward<BN>(g, w, theta, o, S, workers, seed, dropout, &bn, stream));
     // Linear(512,10) + CrossEntropyLoss (models.py:64, main.py:107); no dropout after the ReLU
     RC(head_and_loss<VFEAT>(w.e2, theta + o.l3w, theta + o.l3b, w.y, w.loss_s, w.dlog, w.dh2, S,
-                            backward_pass, 1.f, gscale, worker_loss, stream));
+                            backward_pass, 1.f, gscale, worker_loss, stream, workers));
     if (backward_pass) RC(vbackward<BN>(g, w, theta, o, S, dropout, stream));
     return 0;
 }

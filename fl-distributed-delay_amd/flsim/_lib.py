@@ -33,6 +33,7 @@ EXPORTS = [
     "flsim_cascade_program", "flsim_cascade_eval_host",
     "flsim_probe_enable", "flsim_probe_read", "flsim_probe_disable",
     "flsim_probe_kernel_count", "flsim_probe_kernel_name", "flsim_pn1_release",
+    "flsim_aggregate_adam_rule_push",
 ]
 
 
@@ -107,6 +108,9 @@ def lib():
         ctypes.c_long, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp]
     L.flsim_aggregate_adam_rule.argtypes = [
         vp, vp, vp, vp, vp, ctypes.c_long, vp, ctypes.c_int,
+        ctypes.c_long, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp]
+    L.flsim_aggregate_adam_rule_push.argtypes = [
+        vp, vp, vp, vp, vp, vp, ctypes.c_long, vp, ctypes.c_int,
         ctypes.c_long, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp]
     L.flsim_cascade_program.argtypes = [ctypes.c_int, vp, vp, ctypes.c_int, vp, ctypes.c_int, vp]
     L.flsim_cascade_eval_host.argtypes = [vp, vp, vp, vp, ctypes.c_int, vp, ctypes.c_long, vp]

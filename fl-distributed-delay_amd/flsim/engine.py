@@ -201,8 +201,11 @@ class NetEngine:
     def aggregate_adam_sum(self, S, k, theta, m, v, step, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
         aggregate_adam_sum(S, k, theta, m, v, step, self.SIZES, lr, betas, eps)
 
-    def aggregate_rule(self, S, rule, theta, m, v, step, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
-        aggregate_rule(S, rule, theta, m, v, step, self.SIZES, lr, betas, eps)
+    def aggregate_rule(self, S, rule, theta, m, v, step, lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
+                       S_out=None):
+        """rule() + Adam from S_t in a buffer; S_out (optional): S_t is also written there in
+        the same pass (the FIFO slot of a tick epoch at world > 1)."""
+        aggregate_rule(S, rule, theta, m, v, step, self.SIZES, lr, betas, eps, S_out=S_out)
 
 
 class PN1Engine(NetEngine):
@@ -395,13 +398,14 @@ class ProgramStager:
         return self.dev[j]
 
 
-def aggregate_rule(S, rule, theta, m, v, step, sizes, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
-    """rule() + Adam from S_t in a buffer (flsim_aggregate_adam_rule)."""
+def aggregate_rule(S, rule, theta, m, v, step, sizes, lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
+                   S_out=None):
+    """rule() + Adam from S_t in a buffer (flsim_aggregate_adam_rule_push; S_out may be None)."""
     csz = (ctypes.c_long * len(sizes))(*[int(n) for n in sizes])
-    check(lib().flsim_aggregate_adam_rule(
-        ptr(S), ctypes.byref(rule.c_rule), ptr(theta), ptr(m), ptr(v), sum(int(n) for n in sizes),
-        csz, len(sizes), int(step), float(lr), float(betas[0]), float(betas[1]), float(eps),
-        stream_ptr()))
+    check(lib().flsim_aggregate_adam_rule_push(
+        ptr(S), ptr(S_out), ctypes.byref(rule.c_rule), ptr(theta), ptr(m), ptr(v),
+        sum(int(n) for n in sizes), csz, len(sizes), int(step), float(lr), float(betas[0]),
+        float(betas[1]), float(eps), stream_ptr()))
 
 
 def worker_table(recs, device):

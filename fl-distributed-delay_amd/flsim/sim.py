@@ -58,7 +58,7 @@ class FLSimulation:
                  semantics="reference", dropout=True, chunk_workers=128, device=None, theta0=None,
                  group=None, max_throttle=32, pool=None, betas=(0.9, 0.999), eps=1e-8,
                  engine=None, device_pool=None, test_pool=None, model="PerformantNet1",
-                 fused=True, keep_S=False):
+                 fused=True, keep_S=False, batch_size=128):
         if semantics not in SEMANTICS:
             raise NotImplementedError(f"semantics {semantics!r} (supported: {SEMANTICS})")
         self.n = int(n_workers)
@@ -78,6 +78,14 @@ class FLSimulation:
         self.keep_S = bool(keep_S)
         self.group = group
         self.model = model
+        # --batch_size B (main.py:43-44): every worker-step is G = ceil(B/128) 128-sample groups
+        # (the engine's unit; WorkerRec.pad = B, include/flsim.h), the last one padded
+        self.batch_size = int(batch_size)
+        if self.batch_size < 1:
+            raise ValueError("batch_size must be >= 1")
+        self.G = -(-self.batch_size // 128)
+        if self.batch_size != 128 and semantics == "independent":
+            raise NotImplementedError("independent entries with --batch_size != 128")
         dist = torch.distributed
         if dist.is_available() and dist.is_initialized():
             self.rank = dist.get_rank(group)
@@ -90,7 +98,10 @@ class FLSimulation:
         # collective logic with a CPU stand-in (gloo); the product path always builds PN1Engine
         # a chunk never needs more workers than the run has (the workspace scales with it)
         self.engine = engine if engine is not None else \
-            engine_class(model)(self.device, min(int(chunk_workers), self.n))
+            engine_class(model)(self.device, min(int(chunk_workers), self.n * self.G))
+        if self.batch_size != 128 and getattr(self.engine, "STATS_PER_WORKER", 0):
+            raise NotImplementedError("BatchNorm models: one BatchNorm batch is one 128-sample "
+                                      "fwd_bkwd call (--batch_size 128)")
         self.pool = device_pool if device_pool is not None else \
             DevicePool(self.device, self.seed, pool)
         self.max_throttle = int(max_throttle)
@@ -109,7 +120,7 @@ class FLSimulation:
         self.nstat = int(getattr(self.engine, "STATS_PER_WORKER", 0))
         if self.nstat and semantics == "independent":
             raise NotImplementedError("independent entries with BatchNorm models")
-        self.stats_off = self.Ppad + padded(self.n)
+        self.stats_off = self.Ppad + padded(self.n * self.G)
         self.comm = torch.zeros(self.stats_off + self.n * self.nstat, device=self.device)
         self._stager = ProgramStager(self.device)
         self.stale_store = {}     # epoch -> [slot tensor, refcount]
@@ -118,6 +129,13 @@ class FLSimulation:
         self.loss_log = []        # per epoch: float (synced) or (device tensor, fast mask)
         self._test_src = test_pool  # (imgs, labels) of the test split, or None = synthetic
         self._test = None
+        # measurement (bench.py): worker-steps this rank executed per epoch, and when enabled the
+        # per-epoch collective bracketed by events on the compute stream (RCCL's own stream is
+        # joined back into it by the blocking all_reduce, so the pair spans the collective and the
+        # wait for the slowest rank)
+        self.rank_worker_steps = []
+        self.time_collective = False
+        self.coll_events = []
 
     # ---------------------------------------------------------------------------------------------
     def _slot(self):
@@ -126,7 +144,12 @@ class FLSimulation:
 
     def _worker_table(self, t, workers, ks):
         """WorkerRec (t, i, k, 0) of this rank's computing workers, copied host->device from a
-        pinned staging buffer (asynchronous: the host never waits for the GPU here)."""
+        pinned staging buffer (asynchronous: the host never waits for the GPU here).  With
+        --batch_size B != 128 each worker is G records (t, i + g * 2^20, k, B), g < G."""
+        G = self.G
+        if G > 1 or self.batch_size != 128:
+            workers = np.repeat(np.asarray(workers, np.int64), G)
+            grp = np.tile(np.arange(G, dtype=np.int64), len(workers) // G)
         n = len(workers)
         if getattr(self, "_wt_cap", 0) < max(1, n):
             cap = max(1, n)
@@ -142,9 +165,13 @@ class FLSimulation:
             self._wt_ev[j].synchronize()          # staging buffer j free again (2 epochs ago)
         h = self._wt_host[j][:n].numpy()
         h[:, 0] = t
-        h[:, 1] = workers
         h[:, 2] = ks[workers]
-        h[:, 3] = 0
+        if G > 1 or self.batch_size != 128:
+            h[:, 1] = workers + (grp << 20)
+            h[:, 3] = self.batch_size
+        else:
+            h[:, 1] = workers
+            h[:, 3] = 0
         dev = self._wt_dev[:n]
         if n:
             dev.copy_(self._wt_host[j][:n], non_blocking=True)
@@ -153,6 +180,26 @@ class FLSimulation:
             ev.record()
             self._wt_ev[j] = ev
         return dev
+
+    def _all_reduce(self, buf):
+        """The epoch's one collective (RCCL over xGMI with the nccl backend)."""
+        if self.time_collective and self.device.type == "cuda":
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            torch.distributed.all_reduce(buf, group=self.group)
+            e1.record()
+            self.coll_events.append((e0, e1))
+        else:
+            torch.distributed.all_reduce(buf, group=self.group)
+
+    def collective_ms(self):
+        """Per-epoch collective times (ms) recorded since the last call (synchronises)."""
+        if not self.coll_events:
+            return []
+        self.coll_events[-1][1].synchronize()
+        out = [a.elapsed_time(b) for a, b in self.coll_events]
+        self.coll_events = []
+        return out
 
     def _rule(self, plan, stale):
         """weight_ups of this epoch as a Rule: k = c_t + s_t entries, the stale ones in append
@@ -211,8 +258,9 @@ class FLSimulation:
         active = np.nonzero(plan.computes)[0]
         lo, hi = self.shard(active)
         eng = self.engine
+        G = self.G                               # 128-sample groups (units) per worker-step
         S = self.comm[:self.P]
-        losses = self.comm[self.Ppad:self.Ppad + len(active)]
+        losses = self.comm[self.Ppad:self.Ppad + len(active) * G]
         stats = self.comm[self.stats_off:self.stats_off + len(active) * self.nstat].view(
             len(active), self.nstat)
         if self.world > 1:
@@ -220,25 +268,28 @@ class FLSimulation:
             stats.zero_()
         eng.begin_epoch(self.theta)
         wt = self._worker_table(t, active[lo:hi], ks)      # one async upload per epoch
-        for c0, c1 in self.chunks(lo, hi):
+        for c0, c1 in self.chunks(lo * G, hi * G):
             kw = {"stats_out": stats[c0:c1]} if self.nstat else {}
-            eng.run_chunk(self.theta, self.pool, wt[c0 - lo:c1 - lo], c1 - c0, self.n, self.seed,
-                          self.dropout, losses[c0:c1], **kw)
+            eng.run_chunk(self.theta, self.pool, wt[c0 - lo * G:c1 - lo * G], c1 - c0, self.n,
+                          self.seed, self.dropout, losses[c0:c1], **kw)
         fused = self.fused and self.world == 1 and hasattr(eng, "server_step")
         if not fused or self.keep_S:
             eng.end_epoch(S)
+        self.rank_worker_steps.append(hi - lo)
         if self.world > 1:
             end = self.stats_off + len(active) * self.nstat if self.nstat else \
-                self.Ppad + len(active)
-            torch.distributed.all_reduce(self.comm[:end], group=self.group)
+                self.Ppad + len(active) * G
+            self._all_reduce(self.comm[:end])
         if self.nstat:   # BatchNorm running buffers: every computing worker's call, in order
             eng.update_running(stats, len(active))
         push = None
         if plan.pushed and self.semantics == "reference":
             n_push = int(sum(1 for i in range(self.n) if self.delays[i] != 0 and plan.computes[i]))
             push = self._slot()
-            if not fused or self.keep_S:
+            if fused and self.keep_S:
                 push[:self.P].copy_(S)
+            # otherwise the server step writes S_t into the slot in its own pass: the fused
+            # slab step (world = 1) or the stream after the all-reduce (world > 1)
             self.stale_store[t] = [push, n_push]
         stale = []
         for (_, src) in plan.stale:
@@ -252,8 +303,10 @@ class FLSimulation:
         hp = dict(lr=self.lr, betas=self.betas, eps=self.eps)
         if fused and not self.keep_S:
             eng.server_step(push, rule, self.theta, self.m, self.v, self.step, **hp)
-        else:
+        elif fused:
             eng.aggregate_rule(S, rule, self.theta, self.m, self.v, self.step, **hp)
+        else:
+            eng.aggregate_rule(S, rule, self.theta, self.m, self.v, self.step, S_out=push, **hp)
         for (_, src) in plan.stale:
             if self.semantics == "reference":
                 entry = self.stale_store[src]
@@ -264,12 +317,20 @@ class FLSimulation:
         fast_pos = np.nonzero(plan.fast[active])[0]
         self.trace.append(plan)
         if sync_loss:
-            lv = losses.detach().cpu().numpy()[fast_pos]
+            lv = self._worker_losses(losses.detach().cpu().numpy())[fast_pos]
             val = float(np.mean(lv.astype(np.float32))) if len(lv) else float("nan")
             self.loss_log.append(val)
             return val
         self.loss_log.append((losses.detach().clone(), fast_pos))
         return None
+
+    def _worker_losses(self, lv):
+        """Per-worker CrossEntropyLoss(mean) from the per-group values (group sum / 128):
+        sum over the worker's groups * 128 / B (agents.py:40's lossval per call)."""
+        if self.G == 1 and self.batch_size == 128:
+            return lv
+        tot = lv.reshape(-1, self.G).astype(np.float64).sum(1)
+        return (tot * 128.0 / self.batch_size).astype(np.float32)
 
     def _epoch_independent(self, plan, ks, sync_loss):
         """Independent-entry semantics: every weight_ups entry is a distinct
@@ -329,8 +390,9 @@ class FLSimulation:
                 slot = self.stale_store.pop(key)
                 S.add_(slot[:self.P])
                 self.free_slots.append(slot)
+        self.rank_worker_steps.append(hi - lo + len(own_workers))
         if self.world > 1:
-            torch.distributed.all_reduce(self.comm[:self.Ppad + len(fast)], group=self.group)
+            self._all_reduce(self.comm[:self.Ppad + len(fast)])
         self.step += 1
         eng.aggregate_adam_sum(S, len(fast) + len(plan.stale), self.theta, self.m, self.v,
                                self.step, self.lr, self.betas, self.eps)
@@ -347,7 +409,7 @@ class FLSimulation:
         out = []
         for e in self.loss_log:
             if isinstance(e, tuple):
-                lv = e[0].cpu().numpy()[e[1]]
+                lv = self._worker_losses(e[0].cpu().numpy())[e[1]]
                 out.append(float(np.mean(lv.astype(np.float32))) if len(lv) else float("nan"))
             else:
                 out.append(e)
@@ -405,7 +467,8 @@ class FLSimulation:
                        "model": self.model,
                        "throttle": self.throttle, "seed": self.seed, "semantics": self.semantics,
                        "dropout": self.dropout, "lr": self.lr, "betas": list(self.betas),
-                       "eps": self.eps, "max_throttle": self.max_throttle},
+                       "eps": self.eps, "max_throttle": self.max_throttle,
+                       "batch_size": self.batch_size},
             "epoch": len(self.trace), "step": self.step,
             "theta": self.theta.detach().cpu(), "m": self.m.detach().cpu(),
             "v": self.v.detach().cpu(),
@@ -430,7 +493,7 @@ class FLSimulation:
         mine = {"n": self.n, "throttle": self.throttle, "seed": self.seed,
                 "semantics": self.semantics, "dropout": self.dropout, "model": self.model,
                 "lr": self.lr, "betas": list(self.betas), "eps": self.eps,
-                "max_throttle": self.max_throttle}
+                "max_throttle": self.max_throttle, "batch_size": self.batch_size}
         delays = cfg["delays"].numpy().astype(np.int32)
         if fmt == "flsim-checkpoint-1":
             # format 1 (round 1) had no model / optimizer / throttle-cap keys (they were the
@@ -438,7 +501,7 @@ class FLSimulation:
             import warnings
             from .schedule import DELAY_ZERO
             for k, v in (("model", "PerformantNet1"), ("lr", 1e-3), ("betas", [0.9, 0.999]),
-                         ("eps", 1e-8), ("max_throttle", 32)):
+                         ("eps", 1e-8), ("max_throttle", 32), ("batch_size", 128)):
                 if k not in cfg:
                     cfg[k] = v
                     warnings.warn(f"format-1 checkpoint: {k} not recorded, taken as {v!r}")

@@ -64,8 +64,6 @@ def parse(argv=None):
 
 def main(argv=None):
     args = parse(argv)
-    if args.batch_size != 128:
-        raise SystemExit("the HIP engine is built for --batch_size 128 (the reference default)")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if not torch.cuda.is_available():
@@ -89,7 +87,8 @@ def main(argv=None):
     sim = FLSimulation(args.n_workers, delay=args.delay, throttle=args.throttle,
                        lr=args.learning_rate, seed=args.seed, semantics=args.semantics,
                        dropout=not args.no_dropout, chunk_workers=args.chunk, device=dev,
-                       theta0=theta0, pool=pool, test_pool=test_pool, model=args.model)
+                       theta0=theta0, pool=pool, test_pool=test_pool, model=args.model,
+                       batch_size=args.batch_size)
     if buffers:
         sim.engine.load_buffers(buffers)
     if args.resume:

@@ -21,7 +21,13 @@ extern "C" {
 
 typedef struct ihipStream_t* flsim_stream_t; /* == hipStream_t */
 
-/* one simulated worker-step of a chunk: epoch t, worker i, dataset index k (main.py:138) */
+/* one simulated worker-step of a chunk: epoch t, worker i, dataset index k (main.py:138).
+ * pad = the worker's batch size B (main.py:43-44 --batch_size; 0 = the default 128): a batch of
+ * B samples spans ceil(B/128) consecutive records (128-sample groups) whose i is worker +
+ * g * 2^20 for group g (the group's dropout key); sample slot j of group g is sample g*128 + j
+ * of the worker's batch, drawn with the worker's key; slots past B are padding that adds no loss
+ * and no gradient; the CrossEntropyLoss gradient is the mean over the B samples.  worker_loss of
+ * a group = its summed loss / 128, so the worker's loss = sum over its groups * 128 / B. */
 typedef struct WorkerRec {
     uint32_t t;
     uint32_t i;
@@ -219,6 +225,13 @@ int flsim_cascade_eval_host(const int32_t* prog, const int32_t* info, const floa
 int flsim_aggregate_adam_rule(const float* S, const flsim_rule* rule, float* p, float* m, float* v,
                               long P, const long* tensor_sizes, int n_tensors, long step, double lr,
                               double beta1, double beta2, double eps, flsim_stream_t stream);
+/* the same, also writing S_t into S_out (nullable; 16-byte aligned) in the same pass: the slow
+ * worker's FIFO entry at a tick (main.py:156,161) when S_t arrives in a buffer (world > 1, after
+ * the all-reduce) */
+int flsim_aggregate_adam_rule_push(const float* S, float* S_out, const flsim_rule* rule, float* p,
+                                   float* m, float* v, long P, const long* tensor_sizes,
+                                   int n_tensors, long step, double lr, double beta1, double beta2,
+                                   double eps, flsim_stream_t stream);
 /* convenience forms of the above: reference order with n_stale <= 8 stale entries; and the
  * independent-entry semantics (S = sum of k distinct entries, mean = S / k) */
 int flsim_aggregate_adam(const float* S, int c, const float* const* stale, int n_stale,

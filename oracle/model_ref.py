@@ -267,6 +267,21 @@ def dropout_noise(seed, t, worker, nsamples, dtype=torch.float32, model="Perform
     return res
 
 
+GROUP_KEY_STRIDE = 1 << 20
+
+
+def batch_noise(seed, t, worker, nsamples, dtype=torch.float32, model="PerformantNet1"):
+    """Dropout noise of a worker's batch of any size: 128-sample group g keyed (t, worker +
+    g * 2^20) (the build's spec for --batch_size != 128), the groups'
+    samples concatenated and cut to nsamples.  nsamples = 128: dropout_noise itself."""
+    if nsamples == 128:
+        return dropout_noise(seed, t, worker, 128, dtype, model)
+    groups = -(-nsamples // 128)
+    per = [dropout_noise(seed, t, worker + g * GROUP_KEY_STRIDE, 128, dtype, model)
+           for g in range(groups)]
+    return [torch.cat([p[s] for p in per])[:nsamples] for s in range(len(per[0]))]
+
+
 def fwd_bkwd(params, x, y, noise, fwd=forward):
     """agents.py:32-40: loss = CE(mean) ; backward() accumulates into p.grad ; returns loss."""
     pred = fwd(params, x, noise)
@@ -282,8 +297,9 @@ class OracleSim:
 
     def __init__(self, n, delay=None, delays=None, throttle=False, seed=0, dtype=torch.float32,
                  semantics="reference", dropout=True, pool=None, lr=1e-3, theta0=None,
-                 max_throttle=32, model="PerformantNet1"):
+                 max_throttle=32, model="PerformantNet1", batch_size=128):
         self.n = n
+        self.batch_size = int(batch_size)      # main.py:43-44 --batch_size
         self.delays = np.asarray(delays if delays is not None else O.reference_delays(n, delay),
                                  np.int32)
         self.throttle = bool(throttle)
@@ -315,8 +331,8 @@ class OracleSim:
 
     # ---- data (main.py:138-142) ----
     def batch(self, t, i, k, dtype=None):
-        idx = O.batch_indices(self.seed, t, i, k, self.n, self.lists)
-        x = self.lut[self.imgs[idx]]                      # [128,3,32,32] fp32
+        idx = O.batch_indices(self.seed, t, i, k, self.n, self.lists, self.batch_size)
+        x = self.lut[self.imgs[idx]]                      # [B,3,32,32] fp32
         y = self.labels[idx]
         dt = dtype or self.dtype
         return torch.from_numpy(x).to(dt), torch.from_numpy(y)
@@ -339,7 +355,7 @@ class OracleSim:
         losses = []
         for (t, i, k) in items:
             x, y = self.batch(t, i, k, dt)
-            noise = dropout_noise(self.seed, t, i, x.shape[0], dt, self.model) \
+            noise = batch_noise(self.seed, t, i, x.shape[0], dt, self.model) \
                 if self.dropout else None
             losses.append(float(fwd_bkwd(params, x, y, noise, fwd)))
         g = torch.cat([p.grad.reshape(-1) for p in params]).numpy()

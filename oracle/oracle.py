@@ -136,9 +136,12 @@ def worker_k_sequence(seed, n, n_epochs):
         np.zeros((0, n), np.int64)
 
 
-def batch_indices(seed, t, worker, k, n, lists):
+def batch_indices(seed, t, worker, k, n, lists, batch=BATCH):
+    """main.py:138-142 draw of worker-step (t, worker): `batch` samples with replacement from
+    dataset k's class list; slot e from philox(seed, t, worker, SITE_DATA, e) (e < batch: any
+    --batch_size, main.py:43-44)."""
     lst = lists[1] if k == n - 1 else lists[0]
-    return lst[sample_slots(seed, t, worker, len(lst))]
+    return lst[sample_slots(seed, t, worker, len(lst), batch)]
 
 
 # ---------------------------------------------------------------------------------------------

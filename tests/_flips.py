@@ -91,11 +91,13 @@ def grad(theta, dtype, x, y, noise, scale, forced=None):
     return torch.cat([p.grad.reshape(-1) for p in P]).double().numpy(), dec
 
 
-def gpu_decisions(eng, n):
-    """The GPU's forward decisions for the first n samples of the engine's last chunk, from its
-    workspace (NHWC -> NCHW)."""
+def gpu_decisions(eng, n, rows=None):
+    """The GPU's forward decisions for the first n samples of the engine's last chunk (or for the
+    workspace sample rows `rows`: padded groups of a --batch_size != 128 run), from its workspace
+    (NHWC -> NCHW)."""
     NS = eng.max_samples
-    W = lambda i, shp, dt=torch.float32: eng.workspace_view(i, shp, dt).cpu()[:n]  # noqa: E731
+    sel = slice(0, n) if rows is None else torch.as_tensor(rows, dtype=torch.long)
+    W = lambda i, shp, dt=torch.float32: eng.workspace_view(i, shp, dt).cpu()[sel]  # noqa: E731
     nchw = lambda a: a.permute(0, 3, 1, 2).contiguous()                            # noqa: E731
     d = dict(a1=nchw(W(1, (NS, 34, 34, 48))) > 0, a3=nchw(W(4, (NS, 20, 20, 96))) > 0,
              a5=nchw(W(7, (NS, 13, 13, 192))) > 0, e1=W(10, (NS, 512)) > 0,
@@ -127,10 +129,11 @@ def noise_groups(keys, n, dropout=True):
     return [torch.cat([p[s] for p in per])[:n] for s in range(len(per[0]))]
 
 
-def check_worker_step(g_gpu, eng, theta, x, y, noise, scale):
-    """Both checks above for a GPU gradient g_gpu of the batch (x, y) the engine ran last."""
+def check_worker_step(g_gpu, eng, theta, x, y, noise, scale, rows=None):
+    """Both checks above for a GPU gradient g_gpu of the batch (x, y) the engine ran last (rows:
+    the workspace rows of its samples when they are not the first n)."""
     n = x.shape[0]
-    forced = gpu_decisions(eng, n)
+    forced = gpu_decisions(eng, n, rows)
     g_tf, _ = grad(theta, torch.float64, x, y, noise, scale, forced)
     g_64, d64 = grad(theta, torch.float64, x, y, noise, scale)
     _, d32 = grad(theta, torch.float32, x, y, noise, scale)

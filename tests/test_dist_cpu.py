@@ -41,9 +41,13 @@ class StandInEngine:
     def aggregate_adam_sum(self, S, k, theta, m, v, step, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
         theta -= lr * S / k
 
-    def aggregate_rule(self, S, rule, theta, m, v, step, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
+    def aggregate_rule(self, S, rule, theta, m, v, step, lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
+                       S_out=None):
         """rule.arrays in order after c copies of S (reference order) or at the event
-        positions (general order); a plain weighted mean, enough to check the sharding."""
+        positions (general order); a plain weighted mean, enough to check the sharding.  S_out:
+        the FIFO slot of a tick, written with S_t (the product stream does it in its pass)."""
+        if S_out is not None:
+            S_out[:P].copy_(S)
         if rule.events is None:
             n_s, extra = rule.c, rule.arrays
         else:

@@ -132,3 +132,139 @@ def test_vgg11_max_chunk_matches_small_chunks(pool):
         r = _rel_l2(sb[off:off + size], sa[off:off + size])
         assert r <= 1e-5, (name, r)
         off += size
+
+
+def test_n1024_d500_crosses_first_tick(pool, golden):
+    """configs[2] (n = 1024, delay 500, --throttle): the first tick at t = 500.  A synthetic
+    checkpoint at t = 499 (main.py:119's FIFO holding S_0, refcount 1) is restored and epochs
+    499-501 run: the staleness trace is bit-exact with the reference's own loop
+    (tests/golden/schedule.npz), the tick's rule() + Adam over [S_500] * 512 + [S_0] is bit-exact
+    with the oracle's cascade + Adam (main.py:23-25, agents.py:9-21), the FIFO slot of t = 0 is
+    released and the one of t = 500 holds S_500, and the 1023-worker epoch after it runs."""
+    from flsim.engine import PN1_SIZES
+    from flsim.sim import CKPT_FORMAT, FLSimulation, default_theta
+    from oracle import oracle as O
+    key = "n1024_d500_thr1_e600"
+    gs = golden.schedule
+    ref_comp = np.unpackbits(gs[key + "_computes"], axis=1)[:, :1024]
+    ref_c, ref_stale = gs[key + "_c_t"], gs[key + "_stale"]
+    kw = dict(delay=500, throttle=True, device=DEV, pool=pool, keep_S=True)
+    sim = FLSimulation(1024, **kw)
+    P = sim.P
+    g = torch.Generator().manual_seed(7)
+    S0 = torch.randn(P, generator=g) * 1e-3
+    ck = dict(sim.checkpoint(), epoch=499, step=499, theta=default_theta(0),
+              m=torch.randn(P, generator=g) * 1e-4, v=torch.rand(P, generator=g) * 1e-6,
+              stale={0: (S0, 1)}, loss_log=[float("nan")] * 499, buffers={})
+    assert ck["format"] == CKPT_FORMAT
+    sim = FLSimulation(1024, **kw)
+    sim.restore(ck)
+    sim.epoch()                                            # t = 499
+    p = sim.theta[:P].cpu().numpy().copy()
+    m = sim.m[:P].cpu().numpy().copy()
+    v = sim.v[:P].cpu().numpy().copy()
+    l500 = sim.epoch()                                     # t = 500: the tick
+    S = sim.comm[:P].cpu().numpy()
+    plan = sim.trace[500]
+    assert plan.stale == [(1023, 0)] and plan.pushed and plan.c_t == int(ref_c[500])
+    assert sorted(sim.stale_store) == [500] and sim.stale_store[500][1] == 1
+    assert torch.equal(sim.stale_store[500][0][:P].cpu(), torch.from_numpy(S))
+    gm = np.empty_like(S)
+    off = 0
+    for n in PN1_SIZES:
+        gm[off:off + n] = O.cascade_mean([S[off:off + n]] * plan.c_t +
+                                         [S0.numpy()[off:off + n]])
+        off += n
+    O.adam_step(p, m, v, gm, 500)
+    for name, x, y in (("p", sim.theta, p), ("m", sim.m, m), ("v", sim.v, v)):
+        assert np.array_equal(x[:P].cpu().numpy().view(np.uint32), y.view(np.uint32)), name
+    l501 = sim.epoch()                                     # t = 501: every fast worker
+    assert int(sim.trace[501].computes.sum()) == 1023
+    for t in (499, 500, 501):
+        pl = sim.trace[t]
+        assert np.array_equal(pl.computes, ref_comp[t]), t
+        assert pl.c_t == ref_c[t], t
+        assert [s for (_, s) in pl.stale] == ([int(ref_stale[t])] if ref_stale[t] >= 0 else []), t
+    assert np.isfinite(l500) and np.isfinite(l501)
+
+
+def test_configs3_heterogeneous_full_size(pool):
+    """configs[3] at its own size: n = 16,384 workers with the heterogeneous delay spec
+    (flsim.schedule.heterogeneous_delays: 10 % slow workers, 1 + Geometric(1/100) up to 1000), three
+    epochs (delay-1 workers tick from t = 1, so epochs 1 and 2 pop FIFO entries among the fresh
+    ones): the trace is bit-exact with the oracle's loop on the same delays, every loss is finite,
+    the slot lifetimes follow the FIFOs, and epoch 2's per-worker losses are identical under 128-
+    and 32-worker chunking (S_t within split-K reordering)."""
+    from flsim.engine import PN1_SHAPES, PN1_SIZES
+    from flsim.schedule import heterogeneous_delays
+    from flsim.sim import FLSimulation
+    from oracle import oracle as O
+    n = 16384
+    delays = heterogeneous_delays(n)
+    kw = dict(delays=delays, throttle=True, device=DEV, pool=pool)
+    a = FLSimulation(n, **kw)
+    for _ in range(2):
+        a.epoch(sync_loss=False)
+    live = {src: rc for src, (_, rc) in a.stale_store.items()}
+    ck = a.checkpoint()
+    b = FLSimulation(n, chunk_workers=32, keep_S=True, **kw)
+    b.restore(ck)
+    a.keep_S = True
+    a.epoch(sync_loss=False)
+    b.epoch(sync_loss=False)
+    ref = O.schedule(n, delays, True, 3)
+    for t, plan in enumerate(a.trace):
+        assert np.array_equal(plan.computes, ref.computes[t]), t
+        assert plan.c_t == ref.c_t[t] and plan.s_t == ref.s_t[t], t
+        assert [s for (_, s) in plan.stale] == \
+            [int(x) for x in ref.stale_src[t][ref.stale_src[t] >= 0]], t
+    assert sum(len(p.stale) for p in a.trace) > 0
+    # FIFO slots after epochs 0 and 1: every slow worker pushed S_0; the delay-1 ones popped it
+    # at t = 1 and pushed S_1 (main.py:156-162 per slow worker)
+    n_slow, n_d1 = int((delays != 0).sum()), int((delays == 1).sum())
+    assert n_d1 > 0 and live == {0: n_slow - n_d1, 1: n_d1}, live
+    assert all(np.isfinite(a.losses())) and all(np.isfinite(b.losses()[-1:]))
+    na = int(a.trace[-1].computes.sum())
+    wa = a.comm[a.Ppad:a.Ppad + na].cpu().numpy()
+    wb = b.comm[b.Ppad:b.Ppad + na].cpu().numpy()
+    assert np.array_equal(wa.view(np.uint32), wb.view(np.uint32))
+    sa = a.comm[:a.P].cpu().numpy().astype(np.float64)
+    sb = b.comm[:b.P].cpu().numpy().astype(np.float64)
+    off = 0
+    for (name, _), size in zip(PN1_SHAPES, PN1_SIZES):
+        r = _rel_l2(sb[off:off + size], sa[off:off + size])
+        assert r <= 1e-5, (name, r)
+        off += size
+
+
+@pytest.mark.parametrize("B", [100, 200])
+def test_batch_size_epoch_teacher_forced(pool, B):
+    """--batch_size B != 128 (main.py:43-44) through FLSimulation's worker-batched path: each
+    worker-step is ceil(B/128) 128-sample groups, the last padded.  Epoch 0 of n = 2, delay 5 (the
+    fast worker and the slow one compute): S_0 against the fp64 oracle forced to the GPU's own
+    decisions (tests/_flips.py, scale 1/B), the decision census, and the fast worker's
+    CrossEntropyLoss(mean over B) against the oracle's."""
+    import _flips
+    from flsim.sim import FLSimulation
+    from oracle import model_ref as MR
+    sim = FLSimulation(2, delay=5, device=DEV, pool=pool, batch_size=B, keep_S=True,
+                       chunk_workers=8)
+    loss = sim.epoch()
+    S = sim.comm[:sim.P].cpu().numpy().astype(np.float64)
+    osim = MR.OracleSim(2, delay=5, pool=pool, batch_size=B, dtype=torch.float64)
+    ks = np.random.RandomState(0).randint(0, 2, size=2)
+    xs, ys, noise = [], [], []
+    for i in range(2):
+        x, y = osim.batch(0, i, int(ks[i]), torch.float64)
+        xs.append(x)
+        ys.append(y)
+        noise.append(MR.batch_noise(0, 0, i, B, torch.float64))
+    x, y = torch.cat(xs), torch.cat(ys)
+    nz = [torch.cat([noise[0][s], noise[1][s]]) for s in range(len(noise[0]))]
+    G = -(-B // 128)
+    rows = np.concatenate([w * G * 128 + np.arange(B) for w in range(2)])
+    theta0 = MR.init_params(0)
+    stats = _flips.check_worker_step(S, sim.engine, theta0, x, y, nz, 1.0 / B, rows=rows)
+    print("batch", B, stats)
+    _, l64 = osim.grad_of(theta0, [(0, 0, int(ks[0]))])
+    assert abs(loss - l64[0]) <= 1e-4, (loss, l64[0])

@@ -123,3 +123,31 @@ def test_stream_rule_reference_tick_bit_exact_vs_oracle():
     O.adam_step(p, m, v, g, 51)
     for name, x, y in (("p", dp, p), ("m", dm, m), ("v", dv, v)):
         assert np.array_equal(x.cpu().numpy().view(np.uint32), y.view(np.uint32)), name
+
+
+@pytest.mark.parametrize("narr", [0, 1, 2])
+def test_stream_variants_and_fifo_write_agree(narr, monkeypatch):
+    """The register-array stream (k_agg_stream_reg, 1 and 2 float4 groups per thread) and the
+    LDS-staged k_agg_stream (FLSIM_AGG_G=0) give the same bits for the reference order with 0, 1
+    and 2 stale arrays, on every tensor edge and tail; S_out (the FIFO slot written in the same
+    pass, world > 1 at a tick) equals S_t."""
+    from flsim.engine import PN1_SIZES, Rule, aggregate_rule
+    P = sum(PN1_SIZES)
+    g = torch.Generator(device="cpu").manual_seed(5 + narr)
+    S = (torch.randn(P + 64, generator=g) * 1e-2).to(DEV)
+    arrs = [(torch.randn(P + 64, generator=g) * 1e-2).to(DEV) for _ in range(narr)]
+    base = [torch.randn(P + 64, generator=g).to(DEV), (torch.randn(P + 64, generator=g) * 1e-3).to(DEV),
+            (torch.rand(P + 64, generator=g) * 1e-5).to(DEV)]
+    outs = {}
+    for G in ("0", "1", "2"):
+        monkeypatch.setenv("FLSIM_AGG_G", G)
+        a = [t.clone() for t in base]
+        slot = torch.full_like(S, float("nan"))
+        aggregate_rule(S, Rule(512 + narr, arrs, c=512), *a, 7, PN1_SIZES, S_out=slot)
+        torch.cuda.synchronize()
+        assert torch.equal(slot[:P], S[:P]), G
+        outs[G] = a
+    for G in ("1", "2"):
+        for x, y, what in zip(outs[G], outs["0"], "pmv"):
+            bad = int((x[:P].view(torch.int32) != y[:P].view(torch.int32)).sum())
+            assert bad == 0, (G, what, bad)

@@ -119,56 +119,36 @@ int main(int argc, char** argv) {
     const size_t o2 = (size_t)S * 36 * 36 * 48;
     const size_t o3d = (size_t)S * 18 * 18 * 48;
     const size_t o5 = (size_t)S * 13 * 13 * 192;
-    // conv6 forward (13x13x192 -> 15x15x192)
+    const size_t o5d = (size_t)S * 11 * 11 * 96, o3 = (size_t)S * 20 * 20 * 96;
+    const size_t o2d = (size_t)S * 34 * 34 * 48;
+    // round-3 sweep: per layer the product tile, then direct-A variants (FM, FN, waves, KB, DEPTH)
+#define SWEEP(tag, IH, CI, PAD, CO, OHX, OUT, FNF)                                      \
+    D(tag, IH, CI, PAD, CO, 2, FNF, 8, 3, 2, OHX, OUT)                                   \
+    D(tag, IH, CI, PAD, CO, 2, FNF, 8, 6, 2, OHX, OUT)                                   \
+    D(tag, IH, CI, PAD, CO, 2, FNF, 8, 9, 2, OHX, OUT)                                   \
+    D(tag, IH, CI, PAD, CO, 2, FNF, 8, 6, 5, OHX, OUT)                                   \
+    D(tag, IH, CI, PAD, CO, 4, FNF, 8, 3, 2, OHX, OUT)                                   \
+    D(tag, IH, CI, PAD, CO, 1, FNF, 8, 3, 2, OHX, OUT)                                   \
+    D(tag, IH, CI, PAD, CO, 2, FNF, 6, 3, 2, OHX, OUT)
     P("fwd6", 13, 192, 2, 192, 2, 3, 4, 2, 0)
-    D("fwd6", 13, 192, 2, 192, 2, 6, 8, 9, 2, 0, o6)
-    D("fwd6", 13, 192, 2, 192, 2, 6, 4, 9, 2, 0, o6)
-    D("fwd6", 13, 192, 2, 192, 4, 6, 4, 9, 2, 0, o6)
-    D("fwd6", 13, 192, 2, 192, 2, 12, 8, 3, 2, 0, o6)
-    D("fwd6", 13, 192, 2, 192, 4, 3, 8, 9, 2, 0, o6)
-    D("fwd6", 13, 192, 2, 192, 2, 6, 8, 3, 2, 0, o6)
-    D("fwd6", 13, 192, 2, 192, 2, 6, 4, 3, 2, 0, o6)
-    D("fwd6", 13, 192, 2, 192, 4, 6, 4, 3, 2, 0, o6)
-    D("fwd6", 13, 192, 2, 192, 4, 3, 4, 3, 2, 0, o6)
-    // conv6 data gradient (14x14 dZ, pad 0 -> 13x13)
+    SWEEP("fwd6", 13, 192, 2, 192, 0, o6, 6)
     P("dg6", 14, 192, 0, 192, 4, 3, 4, 2, 13)
-    D("dg6", 14, 192, 0, 192, 2, 6, 8, 9, 2, 13, o6d)
-    D("dg6", 14, 192, 0, 192, 4, 3, 8, 9, 2, 13, o6d)
-    D("dg6", 14, 192, 0, 192, 2, 6, 8, 3, 2, 13, o6d)
-    D("dg6", 14, 192, 0, 192, 4, 6, 4, 3, 2, 13, o6d)
-    // conv4 data gradient (22x22x96 -> 20x20x96)
-    P("dg4", 22, 96, 0, 96, 4, 3, 2, 2, 0)
-    D("dg4", 22, 96, 0, 96, 2, 6, 8, 9, 2, 0, o4d)
-    D("dg4", 22, 96, 0, 96, 4, 6, 4, 9, 2, 0, o4d)
-    D("dg4", 22, 96, 0, 96, 2, 6, 4, 9, 2, 0, o4d)
-    D("dg4", 22, 96, 0, 96, 2, 6, 8, 3, 2, 0, o4d)
-    D("dg4", 22, 96, 0, 96, 4, 6, 4, 3, 2, 0, o4d)
-    D("dg4", 22, 96, 0, 96, 2, 6, 4, 3, 2, 0, o4d)
-    // conv4 forward (20x20x96 -> 22x22x96)
-    P("fwd4", 20, 96, 2, 96, 4, 3, 2, 2, 0)
-    D("fwd4", 20, 96, 2, 96, 2, 6, 8, 9, 2, 0, o4)
-    D("fwd4", 20, 96, 2, 96, 4, 6, 4, 9, 2, 0, o4)
-    D("fwd4", 20, 96, 2, 96, 2, 6, 8, 3, 2, 0, o4)
-    D("fwd4", 20, 96, 2, 96, 2, 6, 4, 3, 2, 0, o4)
-    // conv5 forward (11x11x96 -> 13x13x192)
+    SWEEP("dg6", 14, 192, 0, 192, 13, o6d, 6)
     P("fwd5", 11, 96, 2, 192, 2, 3, 4, 2, 0)
-    D("fwd5", 11, 96, 2, 192, 2, 6, 8, 9, 2, 0, o5)
-    D("fwd5", 11, 96, 2, 192, 4, 6, 4, 9, 2, 0, o5)
-    // conv2 forward (34x34x48 -> 36x36x48)
-    P("fwd2", 34, 48, 2, 48, 2, 3, 4, 1, 0)
-    D("fwd2", 34, 48, 2, 48, 2, 3, 8, 9, 2, 0, o2)
-    D("fwd2", 34, 48, 2, 48, 4, 3, 4, 9, 2, 0, o2)
-    D("fwd2", 34, 48, 2, 48, 2, 3, 4, 9, 2, 0, o2)
-    D("fwd2", 34, 48, 2, 48, 4, 3, 8, 9, 2, 0, o2)
-    D("fwd2", 34, 48, 2, 48, 2, 3, 8, 3, 2, 0, o2)
-    D("fwd2", 34, 48, 2, 48, 4, 3, 4, 3, 2, 0, o2)
-    D("fwd2", 34, 48, 2, 48, 2, 3, 4, 3, 2, 0, o2)
-    // conv3 data gradient (20x20x96 dZ -> 18x18x48)
+    SWEEP("fwd5", 11, 96, 2, 192, 0, o5, 6)
+    P("dg5", 13, 192, 0, 96, 4, 3, 2, 2, 0)
+    SWEEP("dg5", 13, 192, 0, 96, 0, o5d, 6)
+    P("fwd4", 20, 96, 2, 96, 4, 3, 2, 2, 0)
+    SWEEP("fwd4", 20, 96, 2, 96, 0, o4, 6)
+    P("dg4", 22, 96, 0, 96, 4, 3, 2, 2, 0)
+    SWEEP("dg4", 22, 96, 0, 96, 0, o4d, 6)
+    P("fwd3", 18, 48, 2, 96, 2, 3, 4, 2, 0)
+    SWEEP("fwd3", 18, 48, 2, 96, 0, o3, 6)
     P("dg3", 20, 96, 0, 48, 4, 3, 4, 1, 0)
-    D("dg3", 20, 96, 0, 48, 2, 3, 8, 9, 2, 0, o3d)
-    D("dg3", 20, 96, 0, 48, 4, 3, 4, 9, 2, 0, o3d)
-    D("dg3", 20, 96, 0, 48, 4, 3, 8, 9, 2, 0, o3d)
-    D("dg3", 20, 96, 0, 48, 2, 3, 8, 3, 2, 0, o3d)
-    D("dg3", 20, 96, 0, 48, 4, 3, 4, 3, 2, 0, o3d)
+    SWEEP("dg3", 20, 96, 0, 48, 0, o3d, 3)
+    P("fwd2", 34, 48, 2, 48, 2, 3, 4, 1, 0)
+    SWEEP("fwd2", 34, 48, 2, 48, 0, o2, 3)
+    P("dg2", 36, 48, 0, 48, 2, 3, 4, 1, 0)
+    SWEEP("dg2", 36, 48, 0, 48, 0, o2d, 3)
     return 0;
 }

@@ -40,7 +40,7 @@ def probe_name(kname):
     m = re.search(r"Im2colKM<(\d+), (\d+), (\d+),", kname)
     if m:
         return f"conv{FWD[tuple(map(int, m.groups()))]}_wgrad"
-    m = re.search(r"Im2colKC<(\d+), (\d+), (\d+), (\d+),", kname)
+    m = re.search(r"Im2col(?:KC|Direct)<(\d+), (\d+), (\d+), (\d+),", kname)
     if m:
         ih, iw, ci, pad = map(int, m.groups())
         if pad == 2:
