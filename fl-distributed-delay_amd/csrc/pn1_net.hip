@@ -284,9 +284,10 @@ static int forward(const GradState& g, const WS& w, const float* theta, int S,
     // conv1, conv2 (+ReLU)  models.py:29-30
     RC(conv1_fwd(w.x0, theta + P_OFF[0], theta + P_OFF[1], w.a1, S, st));
     // conv2 + ReLU + pool1 + dropout1 (models.py:30-32), one fused launch
-    RC((conv_pool_direct<34, 34, 48, 48, 2, 2, 3, 8, 3, 2, false>(w.a1, S, g.wf[1], 432, w.d1,
-        w.i1, theta + P_OFF[3], workers, seed, SITE_DROP1, THR_P25, SCALE_P25, dropout, st,
-        K_FWD2, 432)));
+    // (gemm_kernel: the direct-A form measured 7.51 vs 7.30 ms with this epilogue, r03b)
+    RC((conv_pool_fwd<34, 34, 48, 48, 2, 2, 3, 4, 1, false>(w.a1, S, g.wf[1], 432, w.d1, w.i1,
+        theta + P_OFF[3], workers, seed, SITE_DROP1, THR_P25, SCALE_P25, dropout, st, K_FWD2,
+        432)));
     RC((conv_like<18, 18, 48, 2, 2, 3, 4, 2>(w.d1, S, g.wf[2], 96, 432,
         EpiBiasRelu{w.a3, theta + P_OFF[5], S * 20 * 20, 96}, st, K_FWD3, 432)));
     // conv4 + ReLU + pool2 + dropout1 (models.py:34-36)
@@ -397,7 +398,8 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC((conv_wgrad<18, 18, 48, 2, 3, 3, 2, 1>(dz3, w.d1, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW,
                                              st, K_WG3, 432, zi(2),
                                              &zu[2])));
-    RC((conv_direct<20, 20, 96, 0, 2, 3, 8, 3, 2, false, 0>(dz3, S, g.wd[2], 48, 864,
+    // (gemm_kernel: the direct-A form measured 3.87 vs 3.78 ms with this staged epilogue, r03b)
+    RC((conv_like<20, 20, 96, 0, 4, 3, 4, 1>(dz3, S, g.wd[2], 48, 864,
         EpiDropScatterRows<18, 18, 48>{w.a2, w.d1, w.i1, s25, S * 18 * 18}, st, K_DG3, 864)));
     float* dz2 = w.a2;
     // ---- conv2: wgrad (input a1), bias, dgrad -> dz1 = . * (a1 > 0) into gx ----

@@ -73,18 +73,46 @@ def test_n1024_d50_through_first_tick(pool, golden):
     assert b.losses()[-1] == losses[-1]
 
 
-# Stated bound of the configs[1] trajectory test: the GPU's distance from the fp64 oracle is at
-# most DRIFT_C times the CPU fp32 port's own distance from it (+ a floor for the first epochs,
-# where both are at the fp32 noise level), in the running-max loss gap and in parameters.
-DRIFT_C = 4.0
+# Stated bounds of the configs[1] trajectory test: the GPU's distance from the fp64 oracle is at
+# most GAP_C times the CPU fp32 port's own distance from it (+ a 2e-4 floor for the first epochs,
+# where both are at the fp32 noise level) in the running-max loss gap, and at most DRIFT_C times
+# it in parameters (JL sketch).  Both are 1.5 x the ratios measured on MI355X from the warm start
+# (profiles/r03a/trajectory_bounds.json: loss gap 1.61, parameter drift 1.27).
+GAP_C = 2.4
+DRIFT_C = 1.9
 
 
-def test_n10_d50_trajectory_drift_vs_oracle(pool, golden):
-    from flsim.sim import FLSimulation
+def test_n10_d50_trajectory_drift_vs_oracle(pool, golden, tmp_path):
+    """configs[1]: n = 10, delay 50, --throttle, --model_file warm_start.pt.  The warm start is
+    tests/golden/warm_n10.npz (a short fp64 oracle pre-training, sha-pinned), written as a
+    models.py state_dict and read back through load_model_file (main.py:98-100); the oracle's
+    fp32 / fp64 trajectories from the same theta are tests/golden/traj_n10.npz."""
+    import hashlib
+    import json
+    import os
+    import sys
+    from FL.models import PerformantNet1
+    from flsim.engine import split_views
+    from flsim.sim import FLSimulation, load_model_file
     from oracle import oracle as O
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    sys.path.insert(0, here)
+    from make_warm_start_n10 import dequantise
+    w = np.load(os.path.join(here, "warm_n10.npz"))
+    warm = dequantise(w["codes"], w["scales"])
+    pin = json.load(open(os.path.join(here, "meta.json")))["warm_n10"]["sha256"]
+    assert hashlib.sha256(warm.tobytes()).hexdigest() == pin
+    m = PerformantNet1()
+    with torch.no_grad():
+        for p_, v_ in zip(m.parameters(), split_views(torch.from_numpy(warm))):
+            p_.copy_(v_)
+    path = str(tmp_path / "warm_start.pt")
+    torch.save(m.state_dict(), path)
+    theta0, _ = load_model_file(path)
+    assert np.array_equal(theta0.numpy(), warm)
     f = golden.traj_n10
     n, d, seed, E = (int(x) for x in f["config"])
-    sim = FLSimulation(n, delay=d, throttle=True, seed=seed, device=DEV, pool=pool)
+    sim = FLSimulation(n, delay=d, throttle=True, seed=seed, device=DEV, pool=pool, theta0=theta0)
     l64, l32 = f["loss64"], f["loss32"]
     at = [int(x) for x in f["sketch_at"]]
     lg, sk = [], []
@@ -101,9 +129,15 @@ def test_n10_d50_trajectory_drift_vs_oracle(pool, golden):
     print("loss gap gpu/cpu:", [(int(t), float(a), float(b)) for t, a, b in
                                 zip(range(0, E, 5), gap_gpu[::5], gap_cpu[::5])])
     print("param drift gpu/cpu:", list(zip(at, d_gpu, d_cpu)))
-    assert np.all(gap_gpu <= DRIFT_C * gap_cpu + 2e-4), (gap_gpu, gap_cpu)
+    print("MEASURED", json.dumps(dict(
+        test="n10_d50_warm_trajectory",
+        loss_gap_ratio_max=float(np.max((gap_gpu - 2e-4) / np.maximum(gap_cpu, 1e-12))),
+        loss_gap_gpu_final=float(gap_gpu[-1]), loss_gap_cpu_final=float(gap_cpu[-1]),
+        drift_ratio=[float(a / b) for a, b in zip(d_gpu, d_cpu)],
+        drift_gpu=[float(x) for x in d_gpu], drift_cpu=[float(x) for x in d_cpu])))
+    assert np.all(gap_gpu <= GAP_C * gap_cpu + 2e-4), (gap_gpu, gap_cpu)
     for t, dg, dc in zip(at, d_gpu, d_cpu):
-        assert dg <= DRIFT_C * dc + 1e-6, (t, dg, dc)
+        assert dg <= DRIFT_C * dc, (t, dg, dc)
 
 
 def test_vgg11_max_chunk_matches_small_chunks(pool):
@@ -175,7 +209,8 @@ def test_n1024_d500_crosses_first_tick(pool, golden):
         gm[off:off + n] = O.cascade_mean([S[off:off + n]] * plan.c_t +
                                          [S0.numpy()[off:off + n]])
         off += n
-    O.adam_step(p, m, v, gm, 500)
+    assert sim.step == 501                                 # Adam steps: 499 restored + 2
+    O.adam_step(p, m, v, gm, sim.step)
     for name, x, y in (("p", sim.theta, p), ("m", sim.m, m), ("v", sim.v, v)):
         assert np.array_equal(x[:P].cpu().numpy().view(np.uint32), y.view(np.uint32)), name
     l501 = sim.epoch()                                     # t = 501: every fast worker

@@ -10,6 +10,8 @@ Tolerances:
   * losses: |dloss| <= 1e-4 on the first step, <= 1e-3 over the first epochs;
   * staleness trace: bit-exact.
 """
+import json
+
 import numpy as np
 import pytest
 import torch
@@ -220,7 +222,12 @@ def test_simulation_matches_oracle_trajectory(pool, thr):
     th = gsim.theta.cpu().numpy().astype(np.float64)
     drift_gpu = _rel_l2(th, o64.theta.astype(np.float64))
     drift_cpu = _rel_l2(osim.theta.astype(np.float64), o64.theta.astype(np.float64))
-    assert drift_gpu <= 6 * drift_cpu + 1e-3, (drift_gpu, drift_cpu)
+    print("MEASURED", json.dumps(dict(test=f"n4_d2_trajectory_thr{int(thr)}",
+                                      drift_gpu=drift_gpu, drift_cpu=drift_cpu,
+                                      ratio=drift_gpu / drift_cpu)))
+    # bound = 1.5 x the ratio measured on MI355X (profiles/r03a/trajectory_bounds.json: 1.97
+    # without throttle, 0.95 with)
+    assert drift_gpu <= (3.0 if not thr else 1.45) * drift_cpu, (drift_gpu, drift_cpu)
 
 
 def test_warm_start_model_file_trajectory(pool, tmp_path):
@@ -583,4 +590,10 @@ def test_independent_entries_trajectory(pool, thr):
     th = gsim.theta.cpu().numpy().astype(np.float64)
     drift_gpu = _rel_l2(th, o64.theta.astype(np.float64))
     drift_cpu = _rel_l2(osim.theta.astype(np.float64), o64.theta.astype(np.float64))
-    assert drift_gpu <= 6 * drift_cpu + 1e-3, (drift_gpu, drift_cpu)
+    print("MEASURED", json.dumps(dict(test=f"n4_d2_independent_thr{int(thr)}",
+                                      drift_gpu=drift_gpu, drift_cpu=drift_cpu,
+                                      ratio=drift_gpu / drift_cpu)))
+    # bound = 1.5 x the ratio measured on MI355X (profiles/r03a/trajectory_bounds.json: 2.98
+    # without throttle, 3.60 with; the GPU sums the fast workers' gradients in GEMM order, the
+    # oracle per worker)
+    assert drift_gpu <= (4.5 if not thr else 5.4) * drift_cpu, (drift_gpu, drift_cpu)

@@ -265,3 +265,23 @@ def test_vgg11_bn_oracle_trajectory_and_eval(golden):
         logits = MR.vgg_bn_forward(params, torch.from_numpy(O.normalize_lut()[timgs[:64]]), None,
                                    sim.bn)
     np.testing.assert_allclose(logits.double().numpy(), g["eval_logits"], rtol=1e-3, atol=1e-4)
+
+
+def test_warm_start_fixture_is_pinned():
+    """configs[1]'s warm start (tests/golden/make_warm_start_n10.py: a short fp64 oracle
+    pre-training, int8 per tensor): its dequantised fp32 vector has the pinned sha256 and the
+    models.py parameter count; it is not the default init."""
+    import hashlib
+    import json
+    import os
+    import sys
+    from oracle import model_ref as MR
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    sys.path.insert(0, here)
+    from make_warm_start_n10 import dequantise
+    w = np.load(os.path.join(here, "warm_n10.npz"))
+    theta = dequantise(w["codes"], w["scales"])
+    meta = json.load(open(os.path.join(here, "meta.json")))
+    assert hashlib.sha256(theta.tobytes()).hexdigest() == meta["warm_n10"]["sha256"]
+    assert theta.size == 5596090
+    assert np.abs(theta - MR.init_params(2)).max() > 1e-3

@@ -301,6 +301,20 @@ int main(int argc, char** argv) {
     F("dg2c 192x48 4w", 36, 48, 0, 48, 3, 3, 4, 1, 1, 0)
     F("dg2c 128x48 4w", 36, 48, 0, 48, 2, 3, 4, 1, 1, 0)
     F("dg2c 192x48 6w", 36, 48, 0, 48, 2, 3, 6, 1, 1, 0)
+    // round 3: weight-gradient blocks covering several / all taps (the 9 tap n-tiles of a split
+    // re-read the split's input window from other blocks today: L2 hit 36 % on conv2's)
+    G("wgx2 48x48 1w", 34, 48, 48, 4096, 3, 3, 1, 1, 1, 0, 0)
+    G("wgx2 48x432 9w", 34, 48, 48, 4096, 3, 3, 1, 9, 1, 0, 0)
+    G("wgx2 48x432 3w", 34, 48, 48, 4096, 3, 9, 1, 3, 1, 0, 0)
+    G("wgx2 48x144 3w", 34, 48, 48, 4096, 3, 3, 1, 3, 1, 0, 0)
+    G("wgx2 48x432 9w z2k", 34, 48, 48, 2048, 3, 3, 1, 9, 1, 0, 0)
+    G("wgx2 48x432 9w z8k", 34, 48, 48, 8192, 3, 3, 1, 9, 1, 0, 0)
+    G("wgx3 96x48 2w", 18, 48, 96, 2048, 3, 3, 2, 1, 1, 0, 0)
+    G("wgx3 96x432 9w", 18, 48, 96, 2048, 6, 3, 1, 9, 1, 0, 0)
+    G("wgx3 48x432 9w", 18, 48, 96, 2048, 3, 3, 1, 9, 1, 0, 0)
+    G("wgx4 96x96 4w", 20, 96, 96, 1024, 3, 3, 2, 2, 1, 0, 0)
+    G("wgx4 96x288 6w", 20, 96, 96, 1024, 3, 3, 2, 6, 1, 0, 0)
+    G("wgx4 48x288 6w", 20, 96, 96, 1024, 3, 3, 1, 6, 1, 0, 0)
     // vgg11 (padding 1), the product's 128x128 4-wave tile against others
     F("vfwd2 128x128 4w", 16, 64, 1, 128, 4, 4, 2, 2, 1, 0)
     F("vfwd2 128x128 8w", 16, 64, 1, 128, 2, 4, 4, 2, 1, 0)
