@@ -229,6 +229,24 @@ struct RowsKC {
 };
 
 // ---------------------------------------------------------------------------------------------
+// k-major tile row of thread tid when TPR threads share a row.  ds_write_b128 is serviced in
+// groups of 8 lanes on 32 banks (MI355X_MICROARCH.md, LDS table); with TPR = 4 (one-wave blocks)
+// a group holds two rows, and rows a, a + 1 (stride STRIDE = 4 mod 8) overlap on 4 banks: a
+// 2-way conflict on every store (conv2 weight gradient: SQ_LDS_BANK_CONFLICT 569 M cycles per
+// launch, profiles/r03a/pmc).  Rows a and a + 4 sit 4 * STRIDE = 16 (mod 32) banks apart, so the
+// two halves of each group take rows 4 apart.  The tile contents are unchanged.
+// ---------------------------------------------------------------------------------------------
+template <int TPR>
+__device__ __forceinline__ int km_row(int tid) {
+    if constexpr (TPR == 4) {
+        const int g = tid >> 3;
+        return (g & 3) + 4 * ((tid >> 2) & 1) + 8 * (g >> 2);
+    } else {
+        return tid / TPR;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Row-major matrix whose ROWS are the reduction index (KM): element (k, col) at P[k * ld + col];
 // the tile spans columns [c0, c0 + ROWS).  k >= NK or col >= NC read as zero (NC % 4 == 0).
 // PO > 0: the rows are the pixels of PO x PO images and k walks only the top-left PV x PV
@@ -254,7 +272,7 @@ struct RowsKM {
     short c4[UNITS];
     BufSrc buf;
     __device__ void setup(int c0, int tid) {
-        krow = tid / TPR;
+        krow = km_row<TPR>(tid);
         if constexpr (FLSIM_BUFLOAD) {
             const long rows = PO > 0 ? (long)((NK + PV * PV - 1) / (PV * PV)) * PO * PO : NK;
             buf.init(P, (unsigned long)rows * ld * 4);
@@ -325,7 +343,7 @@ struct Im2colKM {
     short c4[UNITS];
     BufSrc buf;
     __device__ void setup(int c0, int tid) {
-        krow = tid / TPR;
+        krow = km_row<TPR>(tid);
         if constexpr (FLSIM_BUFLOAD)
             buf.init(X, (unsigned long)((M + OH * OW - 1) / (OH * OW)) * IH * IW * CI * 4);
 #pragma unroll

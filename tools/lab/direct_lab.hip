@@ -5,6 +5,7 @@
 //         -I fl-distributed-delay_amd/csrc tools/lab/direct_lab.hip -o tools/lab/direct_lab
 #include "lab_common.h"
 #include "gemm_direct.h"
+#include "gemm_resident.h"
 
 static int g_iters = 5;
 
@@ -94,6 +95,28 @@ static void direct(const char* tag, const float* X, const float* W, const float*
     fflush(stdout);
 }
 
+// resident-B persistent kernel (gemm_resident.h): grid = NB blocks (one per CU by default)
+template <int IH, int CI, int PAD, int CO, int FM, int FN, int WAVES, int DEPTH, int OHX = 0>
+static void resident(const char* tag, const float* X, const float* W, const float* b, float* Y,
+                     int S, int NB) {
+    constexpr int BM = 16 * FM * WAVES;
+    constexpr int KS = 9 * CI / GK;
+    using AD = Im2colDirect<IH, IH, CI, PAD, FM, false, OHX>;
+    AD ad;
+    ad.X = X;
+    ad.M = S * AD::OH * AD::OW;
+    EpiBiasRelu epi{Y, b, ad.M, CO};
+    const int tm = ceil_div(ad.M, BM);
+    auto k = gemm_resident_kernel<FM, FN, WAVES, KS, DEPTH, 1, AD, EpiBiasRelu>;
+    const float ms = time_it([&] {
+        hipLaunchKernelGGL(k, dim3(NB), dim3(64 * WAVES), 0, 0, ad, W, 9 * CI, CO, epi, tm);
+    });
+    const double fl = 2.0 * ad.M * CO * 9 * CI;
+    printf("%-30s resid  tile %3dx%3d %dw D%d nb%d %8.3f ms  %6.1f TF/s\n", tag, BM, 16 * FN, WAVES,
+           DEPTH, NB, ms, fl / (ms * 1e-3) / 1e12);
+    fflush(stdout);
+}
+
 int main(int argc, char** argv) {
     const int S = getenv("FLSIM_LAB_S") ? atoi(getenv("FLSIM_LAB_S")) : 16384;
     if (getenv("LAB_ITERS")) g_iters = atoi(getenv("LAB_ITERS"));
@@ -146,6 +169,28 @@ int main(int argc, char** argv) {
     SWEEP("fwd3", 18, 48, 2, 96, 0, o3, 6)
     P("dg3", 20, 96, 0, 48, 4, 3, 4, 1, 0)
     SWEEP("dg3", 20, 96, 0, 48, 0, o3d, 3)
+#define RS(tag, IH, CI, PAD, CO, FM, FN, WV, DP, OHX, OUT, NB)                          \
+    if (want(tag)) {                                                                     \
+        CK(hipMemset(Y1, 0, (size_t)(OUT) * 4));                                         \
+        resident<IH, CI, PAD, CO, FM, FN, WV, DP, OHX>(tag, X, W, b, Y1, S, NB);          \
+        compare(tag, Y0, Y1, (size_t)(OUT));                                             \
+    }
+    // round 3: resident-B persistent kernel on conv2's forward and data gradient (B = 83 KB)
+    P("rfwd2", 34, 48, 2, 48, 2, 3, 4, 1, 0)
+    D("rfwd2", 34, 48, 2, 48, 2, 3, 8, 3, 2, 0, o2)
+    RS("rfwd2", 34, 48, 2, 48, 2, 3, 8, 2, 0, o2, 256)
+    RS("rfwd2", 34, 48, 2, 48, 2, 3, 8, 8, 0, o2, 256)
+    RS("rfwd2", 34, 48, 2, 48, 2, 3, 4, 2, 0, o2, 256)
+    RS("rfwd2", 34, 48, 2, 48, 4, 3, 4, 2, 0, o2, 256)
+    RS("rfwd2", 34, 48, 2, 48, 4, 3, 8, 2, 0, o2, 256)
+    RS("rfwd2", 34, 48, 2, 48, 1, 3, 8, 2, 0, o2, 256)
+    RS("rfwd2", 34, 48, 2, 48, 2, 3, 8, 2, 0, o2, 512)
+    P("rdg2", 36, 48, 0, 48, 2, 3, 4, 1, 0)
+    D("rdg2", 36, 48, 0, 48, 2, 3, 8, 3, 2, 0, o2d)
+    RS("rdg2", 36, 48, 0, 48, 2, 3, 8, 2, 0, o2d, 256)
+    RS("rdg2", 36, 48, 0, 48, 2, 3, 8, 8, 0, o2d, 256)
+    RS("rdg2", 36, 48, 0, 48, 4, 3, 4, 2, 0, o2d, 256)
+    RS("rdg2", 36, 48, 0, 48, 4, 3, 8, 2, 0, o2d, 256)
     P("fwd2", 34, 48, 2, 48, 2, 3, 4, 1, 0)
     SWEEP("fwd2", 34, 48, 2, 48, 0, o2, 3)
     P("dg2", 36, 48, 0, 48, 2, 3, 4, 1, 0)
