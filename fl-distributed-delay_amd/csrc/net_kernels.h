@@ -672,6 +672,44 @@ static int conv_pool_direct(const float* X, int S, const float* Wpk, int KP, flo
         X, S, Wpk, CO, KP, epi, st, kid, kreal);
 }
 
+// Small chunks (configs[1]: 5 workers = 640 samples per epoch) leave the 256-row direct tiles with
+// a few rounds of blocks on 256 CUs, so the last, partial round costs up to 15-25 % on the
+// conv5/conv6 passes; chunks of at most small_chunk_samples() samples run the same GEMMs with
+// 128-row tiles (FM halved).  The k order per output is unchanged, so the results are
+// bit-identical.  FLSIM_SMALL_S overrides the threshold (0: never).
+static int small_chunk_samples() {
+    static int s = -1;
+    if (s < 0) {
+        const char* e = getenv("FLSIM_SMALL_S");
+        s = e ? atoi(e) : 2048;
+    }
+    return s;
+}
+
+template <int IH, int IW, int CI, int PAD, int FM, int FMS, int FN, int WAVES, int KB, int DEPTH,
+          bool WIN, int OHX, class EPI>
+static int conv_direct_sz(const float* X, int S, const float* Wpk, int N, int KP, const EPI& epi,
+                          hipStream_t st, int kid, int kreal) {
+    if (S <= small_chunk_samples())
+        return conv_direct<IH, IW, CI, PAD, FMS, FN, WAVES, KB, DEPTH, WIN, OHX>(X, S, Wpk, N, KP,
+                                                                              epi, st, kid, kreal);
+    return conv_direct<IH, IW, CI, PAD, FM, FN, WAVES, KB, DEPTH, WIN, OHX>(X, S, Wpk, N, KP, epi,
+                                                                          st, kid, kreal);
+}
+
+template <int IH, int IW, int CI, int CO, int PAD, int FM, int FMS, int FN, int WAVES, int KB,
+          int DEPTH, bool NCHW_OUT>
+static int conv_pool_direct_sz(const float* X, int S, const float* Wpk, int KP, float* d,
+                               uint8_t* idx, const float* bias, const WorkerRec* workers,
+                               uint64_t seed, uint32_t site, uint32_t thr, float scale,
+                               int dropout, hipStream_t st, int kid, int kreal) {
+    if (S <= small_chunk_samples())
+        return conv_pool_direct<IH, IW, CI, CO, PAD, FMS, FN, WAVES, KB, DEPTH, NCHW_OUT>(
+            X, S, Wpk, KP, d, idx, bias, workers, seed, site, thr, scale, dropout, st, kid, kreal);
+    return conv_pool_direct<IH, IW, CI, CO, PAD, FM, FN, WAVES, KB, DEPTH, NCHW_OUT>(
+        X, S, Wpk, KP, d, idx, bias, workers, seed, site, thr, scale, dropout, st, kid, kreal);
+}
+
 // Splits of a slab-accumulating GEMM (weight gradients: the reduction runs over the chunk's
 // pixels or samples).  The slab has Z rows; a small chunk (configs[1]: 5 workers = 640 samples)
 // would leave each split a handful of k-steps, so the per-block prologue and the slab
@@ -679,7 +717,12 @@ static int conv_pool_direct(const float* X, int S, const float* Wpk, int KP, flo
 // ceil(1024 / tiles)) rows (>= 32 k-steps per split, >= 1024 blocks); the other rows keep what
 // earlier chunks accumulated, and the epoch's slab sum reads every row.  KMIN = 32 measured on
 // n = 10: 617 -> 645 worker-steps/s, headline unchanged (profiles/r02f/wsplit.txt).
-static int wsplit(int ksteps, int Z, int tiles) {
+// cap > 0 and FLSIM_WSPLIT_FILL=1: cap = the blocks the GPU holds at once for this kernel, and the
+// split grows to fill the last round of resident blocks (same rounds, shorter blocks).  Off by
+// default: on configs[1] it moved single weight gradients by -2..+5 % and the epoch not at all
+// (776.4 vs 777.0 worker-steps/s, profiles/r03e), while the larger KMIN of the sweep in
+// profiles/r03d (fewer, longer splits) made the weight gradients slower (conv6 124 -> 107 TF/s).
+static int wsplit(int ksteps, int Z, int tiles, int cap = 0) {
     static int kmin = -1;
     if (kmin < 0) {
         const char* e = getenv("FLSIM_WSPLIT_KMIN");     // measurement override (0: always Z)
@@ -689,7 +732,32 @@ static int wsplit(int ksteps, int Z, int tiles) {
     int z = (ksteps + kmin - 1) / kmin;
     const int zb = (1024 + tiles - 1) / tiles;
     if (z < zb) z = zb;
+    static int fill = -1;
+    if (fill < 0) {
+        const char* e = getenv("FLSIM_WSPLIT_FILL");     // measurement override (1: on)
+        fill = e ? atoi(e) : 0;
+    }
+    if (fill && cap > 0 && z < Z) {
+        const long rounds = ((long)tiles * z + cap - 1) / cap;
+        const long zf = rounds * cap / tiles;
+        if (zf > z) z = (int)(zf < ksteps ? zf : ksteps);
+    }
     return z < Z ? z : Z;
+}
+
+// blocks of kernel f (block size nt, static LDS only) resident on the whole GPU at once
+static int resident_blocks(const void* f, int nt) {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = -1;
+    }
+    int per = 0;
+    if (cus <= 0 || hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, nt, 0) != hipSuccess)
+        return 0;
+    return per * cus;
 }
 
 // forward conv (also the data-gradient conv): out[m][n] for m < S*OH*OW, n < N
@@ -710,6 +778,14 @@ static int conv_like(const float* X, int S, const float* Wpk, int N, int KP, con
     bl.NR = N;
     return launch_gemm<FM, FN, WM, WN>(al, bl, epi, al.M, N, KP / GK, 1, st, kid,
                                        2.0 * al.M * N * kreal);
+}
+
+template <int IH, int IW, int CI, int PAD, int FM, int FMS, int FN, int WM, int WN, class EPI>
+static int conv_like_sz(const float* X, int S, const float* Wpk, int N, int KP, const EPI& epi,
+                        hipStream_t st, int kid, int kreal) {
+    if (S <= small_chunk_samples())
+        return conv_like<IH, IW, CI, PAD, FMS, FN, WM, WN>(X, S, Wpk, N, KP, epi, st, kid, kreal);
+    return conv_like<IH, IW, CI, PAD, FM, FN, WM, WN>(X, S, Wpk, N, KP, epi, st, kid, kreal);
 }
 
 // weight gradient: slab[z][co][kk] += sum_p dz[p][co] * im2col(X)[p][kk]  (conv padding PAD)
@@ -738,7 +814,9 @@ static int conv_wgrad(const float* dz, const float* X, int S, int CO, int KP, fl
     bl.M = M;
     EpiSlabAcc epi{slab, CO, KP, (long)CO * KP, bslab, zinit};
     const int tiles = ceil_div(CO, BM) * ceil_div(KP, BN);
-    const int zu = wsplit(ceil_div(M, GK), Z, tiles);
+    static const int cap =
+        resident_blocks((const void*)gemm_kernel<FM, FN, WM, WN, AL, BL, EpiSlabAcc>, NT);
+    const int zu = wsplit(ceil_div(M, GK), Z, tiles, cap);
     if (zused) *zused = zu;
     return launch_gemm<FM, FN, WM, WN>(al, bl, epi, CO, KP, ceil_div(M, GK), zu, st, kid,
                                        2.0 * M * CO * kreal);

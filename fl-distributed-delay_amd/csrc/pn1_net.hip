@@ -294,7 +294,7 @@ static int forward(const GradState& g, const WS& w, const float* theta, int S,
     RC((conv_pool_direct<20, 20, 96, 96, 2, 2, 6, 8, 6, 2, false>(w.a3, S, g.wf[3], 864, w.d2,
         w.i2, theta + P_OFF[7], workers, seed, SITE_DROP2, THR_P25, SCALE_P25, dropout, st,
         K_FWD4, 864)));
-    RC((conv_direct<11, 11, 96, 2, 2, 6, 8, 3, 2, false, 0>(w.d2, S, g.wf[4], 192, 864,
+    RC((conv_direct_sz<11, 11, 96, 2, 2, 1, 6, 8, 3, 2, false, 0>(w.d2, S, g.wf[4], 192, 864,
         EpiBiasRelu{w.a5, theta + P_OFF[9], S * 13 * 13, 192}, st, K_FWD5, 864)));
     // conv6 + ReLU + pool3 + dropout1 (models.py:38-40), written in torch's flatten order
     // (models.py:41) so linear1 keeps the torch weight layout; the floor-mode border row/column
@@ -303,7 +303,12 @@ static int forward(const GradState& g, const WS& w, const float* theta, int S,
         w.i3, theta + P_OFF[11], workers, seed, SITE_DROP3, THR_P25, SCALE_P25, dropout, st,
         K_FWD6, 1728)));
     // linear1 + relu + dropout2 (models.py:41-43), split-K partials then finish
-    RC((linear_fwd<4, 4, 2, 2>(w.d3, theta + P_OFF[12], w.part, S, 512, 9408, ZL1F, st, K_L1F)));
+    // small chunks (configs[1]: 640 samples = 5 x 4 tiles of 128 x 128, 80 blocks with the split)
+    // take 64 x 64 tiles: the same split, hence the same sums, with 4x the blocks
+    if (S <= 4096)
+        RC((linear_fwd<2, 2, 2, 2>(w.d3, theta + P_OFF[12], w.part, S, 512, 9408, ZL1F, st, K_L1F)));
+    else
+        RC((linear_fwd<4, 4, 2, 2>(w.d3, theta + P_OFF[12], w.part, S, 512, 9408, ZL1F, st, K_L1F)));
     RC(linear_finish(w.part, ZL1F, theta + P_OFF[13], w.e1, S, 512, workers, seed, SITE_DROP4,
                      THR_P50, SCALE_P50, dropout, st));
     // linear2 + relu + dropout2 (models.py:44-45)
@@ -375,7 +380,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC((conv_wgrad<13, 13, 192, 2, 6, 3, 2, 4, 14, true>(dz6, w.a5, S, 192, 1728, g.sw[5],
                                                         g.sb[5], GEO[5].ZW, st, K_WG6, 1728, zi(5),
                                              &zu[5])));
-    RC((conv_direct<14, 14, 192, 0, 2, 6, 8, 6, 2, false, 13>(dz6, S, g.wd[5], 192, 1728,
+    RC((conv_direct_sz<14, 14, 192, 0, 2, 1, 6, 8, 6, 2, false, 13>(dz6, S, g.wd[5], 192, 1728,
         EpiMask<true>{w.gx, w.a5, S * 13 * 13, 192}, st, K_DG6, 1728)));
     float* dz5 = w.gx;
     // ---- conv5: wgrad (input d2), bias, dgrad -> grad wrt d2 (dropout site 2), scattered through
@@ -383,7 +388,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC((conv_wgrad<11, 11, 96, 2, 6, 3, 2, 2>(dz5, w.d2, S, 192, 864, g.sw[4], g.sb[4], GEO[4].ZW,
                                              st, K_WG5, 864, zi(4),
                                              &zu[4])));
-    RC((conv_direct<13, 13, 192, 0, 2, 6, 8, 3, 2, false, 0>(dz5, S, g.wd[4], 96, 1728,
+    RC((conv_direct_sz<13, 13, 192, 0, 2, 1, 6, 8, 3, 2, false, 0>(dz5, S, g.wd[4], 96, 1728,
         EpiDropScatterRows<11, 11, 96>{w.a4, w.d2, w.i2, s25, S * 11 * 11}, st, K_DG5, 1728)));
     float* dz4 = w.a4;
     // ---- conv4: wgrad (input a3), bias, dgrad -> dz3 = . * (a3 > 0) into gx ----
@@ -399,14 +404,14 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
                                              st, K_WG3, 432, zi(2),
                                              &zu[2])));
     // (gemm_kernel: the direct-A form measured 3.87 vs 3.78 ms with this staged epilogue, r03b)
-    RC((conv_like<20, 20, 96, 0, 4, 3, 4, 1>(dz3, S, g.wd[2], 48, 864,
+    RC((conv_like_sz<20, 20, 96, 0, 4, 2, 3, 4, 1>(dz3, S, g.wd[2], 48, 864,
         EpiDropScatterRows<18, 18, 48>{w.a2, w.d1, w.i1, s25, S * 18 * 18}, st, K_DG3, 864)));
     float* dz2 = w.a2;
     // ---- conv2: wgrad (input a1), bias, dgrad -> dz1 = . * (a1 > 0) into gx ----
     RC((conv_wgrad<34, 34, 48, 2, 3, 3, 1, 1>(dz2, w.a1, S, 48, 432, g.sw[1], g.sb[1], GEO[1].ZW,
                                              st, K_WG2, 432, zi(1),
                                              &zu[1])));
-    RC((conv_direct<36, 36, 48, 0, 2, 3, 8, 3, 2, false, 0>(dz2, S, g.wd[1], 48, 432,
+    RC((conv_direct_sz<36, 36, 48, 0, 2, 1, 3, 8, 3, 2, false, 0>(dz2, S, g.wd[1], 48, 432,
         EpiMaskRows<48>{w.gx, w.a1, S * 34 * 34}, st, K_DG2, 432)));
     float* dz1 = w.gx;
     // ---- conv1: wgrad (input x0), bias ----
