@@ -14,6 +14,11 @@ Same classes, signatures and aliasing semantics; the arithmetic runs in libflsim
                                parameters live in one flat device buffer, model.parameters() are
                                views of it
 
+The .grad views fwd_bkwd returns are filled lazily (_LazyGrad): the gradient stays in the
+engine's split-K slabs until a torch function first touches a view (then the slabs are reduced
+into the buffer, so user code always reads the accumulated .grad) or until update_model, which
+then runs the fused server step: one slab reduction per epoch instead of one per call.
+
 Batches (main.py:43-44 --batch_size): any size up to 16,384 samples.  The engine pads a batch to
 whole groups of 128 samples (padding adds nothing) and scales the CrossEntropyLoss gradient by
 1/n, so the gradient is the reference's mean over the n samples.  Dropout masks follow the
@@ -47,6 +52,58 @@ MAX_BATCH = 16384                           # samples per fwd_bkwd call (32-bit 
 GROUP_KEY_STRIDE = 1 << 20                  # dropout key of 128-sample group b: i + b * 2^20
 
 
+# Tensor methods and properties that read only metadata or the storage handle: a lazy gradient
+# view answers them without reducing the slabs first
+_META = set()
+for _n in ("untyped_storage", "data_ptr", "size", "dim", "numel", "stride", "storage_offset",
+           "element_size", "is_contiguous", "__len__", "nelement", "ndimension", "get_device"):
+    if hasattr(torch.Tensor, _n):
+        _META.add(getattr(torch.Tensor, _n))
+for _n in ("shape", "dtype", "device", "is_cuda", "requires_grad", "grad_fn", "is_leaf", "layout",
+           "ndim", "is_sparse", "is_quantized", "is_meta", "names", "_base", "grad", "data"):
+    _pr = getattr(torch.Tensor, _n, None)
+    if _pr is not None and hasattr(_pr, "__get__"):
+        _META.add(_pr.__get__)
+del _n, _pr
+
+
+class _LazyGrad(torch.Tensor):
+    """A .grad view of the epoch's flat gradient buffer G whose contents are produced on first
+    use.  fwd_bkwd leaves the worker's gradient in the engine's split-K slabs; any torch function
+    or method that reads (or writes) one of these views first reduces the slabs into G
+    (flsim_<net>_end_epoch), so every read sees exactly what the reference's accumulated .grad
+    holds (agents.py:35).  Central.update_model instead runs the fused server step (slabs -> S_t
+    -> rule() + Adam, S_t written into G) when nothing has been read: the reference loop of
+    main.py:126-188 then reduces the slabs once per epoch, not once per fwd_bkwd call."""
+
+    @classmethod
+    def __torch_function__(cls, func, types, args=(), kwargs=None):
+        kwargs = kwargs or {}
+        if func not in _META:
+            for a in list(args) + list(kwargs.values()):
+                for x in (a if isinstance(a, (list, tuple)) else (a,)):
+                    if isinstance(x, _LazyGrad):
+                        ctx = x.__dict__.get("_flsim_ctx")
+                        ctx = ctx() if ctx is not None else None
+                        if ctx is not None:
+                            ctx.flush(touched=True)
+        with torch._C.DisableTorchFunctionSubclass():
+            return func(*args, **kwargs)
+
+    def __repr__(self, *, tensor_contents=None):
+        return repr(self.as_subclass(torch.Tensor))
+
+
+def _lazy_views(flat, shapes, ctx):
+    ref = weakref.ref(ctx)
+    out = []
+    for v in split_views(flat, shapes):
+        g = torch.Tensor._make_subclass(_LazyGrad, v, False)
+        g.__dict__["_flsim_ctx"] = ref
+        out.append(g)
+    return out
+
+
 class _ModelContext:
     """Flat parameter / optimizer-state buffers and the engine of one central model."""
 
@@ -75,6 +132,8 @@ class _ModelContext:
         self.seed = seed
         self.t = 0               # epoch counter (dropout RNG key)
         self.G = None            # flat gradient buffer of the current epoch (p.grad views)
+        self.dirty = False       # G lags the slabs (fwd_bkwd ran since the last reduction)
+        self.touched = False     # a .grad view was used this epoch: update_model reads G
         self.carry = None        # gradient accumulated before an engine resize this epoch
         self.packed = False
         self.step = 0
@@ -111,6 +170,7 @@ class _ModelContext:
                 self.engine.running = old.running
                 self.engine.num_batches_tracked = old.num_batches_tracked
             if self.G is not None:
+                self.flush()                # the old engine's slabs, before they go away
                 self.carry = self.G.clone()
             self.packed = False
         if cw > self.loss_buf.numel():
@@ -127,10 +187,24 @@ class _ModelContext:
                              "indices restart at 0 when a Central is built: build the Central "
                              "first, then the workers, as main.py:110-113 does)")
 
+    def flush(self, touched=False):
+        """G = the epoch's gradient so far: the slab reduction fwd_bkwd left pending.  touched:
+        user code read or wrote a .grad view, so from now on G (not the slabs) is the epoch's
+        gradient for update_model (an in-place change of a .grad is seen)."""
+        self.touched = self.touched or touched
+        if not self.dirty:
+            return
+        self.dirty = False
+        self.engine.end_epoch(self.G)
+        if self.carry is not None:
+            self.G.add_(self.carry)
+
     def new_epoch(self):
         self.t += 1
         self.users = {}
         self.G = None
+        self.dirty = False
+        self.touched = False
         self.carry = None
         self.packed = False
 
@@ -216,8 +290,16 @@ class Central:
             S = torch.nn.functional.pad(S, (0, padded(ctx.P) - ctx.P))
             r = Rule(1, [], c=1)
         ctx.step += 1
-        eng.aggregate_rule(S, r, ctx.theta, ctx.m, ctx.v, ctx.step, lr=g["lr"],
-                           betas=g["betas"], eps=g["eps"])
+        hp = dict(lr=g["lr"], betas=g["betas"], eps=g["eps"])
+        if isinstance(ups, _LazyMean) and ctx.G is not None and ctx.carry is None and \
+                not ctx.touched and hasattr(eng, "server_step"):
+            # fused: this epoch's slabs -> S_t (also written into G, which the FIFO entries of
+            # main.py:156,161 alias) -> rule() + Adam, one pass
+            eng.server_step(ctx.G, r, ctx.theta, ctx.m, ctx.v, ctx.step, **hp)
+            ctx.dirty = False
+        else:
+            ctx.flush()
+            eng.aggregate_rule(S, r, ctx.theta, ctx.m, ctx.v, ctx.step, **hp)
         for p in self.model.parameters():        # optim.zero_grad() (set_to_none, torch >= 2)
             p.grad = None
         self._sync_optimizer_state()
@@ -280,10 +362,8 @@ class Worker:
             eng.update_running(ctx.bn_stats, 1)
             for mod in ctx.bns:
                 mod.num_batches_tracked.fill_(eng.num_batches_tracked)
-        eng.end_epoch(ctx.G)                     # running sum of the epoch's gradients
-        if ctx.carry is not None:
-            ctx.G.add_(ctx.carry)
-        grads = split_views(ctx.G[:ctx.P], ctx.shapes)
+        ctx.dirty = True                         # G = the running sum on first read (flush)
+        grads = _lazy_views(ctx.G[:ctx.P], ctx.shapes, ctx)
         for p, gv in zip(self.model.parameters(), grads):
             p.grad = gv                          # agents.py:35: accumulated in place
         # CrossEntropyLoss(mean) over the n samples: group sums / n (padding contributes 0)

@@ -148,7 +148,11 @@ def test_training_trajectory(golden, thr):
     ref_losses = g[key + "_losses"]
     for t in range(len(ref_losses)):
         loss = sim.epoch()
-        assert abs(loss - ref_losses[t]) <= 1e-5, (t, loss, ref_losses[t])
+        # the first two epochs agree to the last bits; later ones drift with the host CPU's fp32
+        # kernels (Adam turns 1-ulp gradient differences into O(lr) moves): 1.2e-4 at
+        # epoch 4 on an EPYC build host whose oneDNN paths differ from the golden generator's
+        tol = 1e-6 if t < 2 else 1e-3
+        assert abs(loss - ref_losses[t]) <= tol, (t, loss, ref_losses[t])
         n_entries, n_distinct = g[f"{key}_comp{t}"]
         assert len(sim.trace[-1]["appended"]) == n_entries
         ts = []
@@ -199,7 +203,8 @@ def test_vgg11_oracle_trajectory(golden):
     sim = MR.OracleSim(3, delay=2, throttle=True, pool=(imgs, labels), model="vgg11")
     for t, ref in enumerate(g["train_losses"]):
         loss = sim.epoch()
-        assert abs(loss - ref) <= 1e-5, (t, loss, ref)
+        # host-CPU fp32 drift after the first Adam steps, as in test_training_trajectory
+        assert abs(loss - ref) <= (1e-5 if t < 2 else 1e-3), (t, loss, ref)
         np.testing.assert_allclose(
             [float((a.astype(np.float64) ** 2).sum()) for a in MR.split_flat(sim.theta, "vgg11")],
             g[f"train_theta{t}_stats"][:, 1], rtol=1e-3)
@@ -220,8 +225,9 @@ def test_vgg11_bn_oracle_matches_reference(golden):
     assert sim.bn.num_batches_tracked == 1
     np.testing.assert_allclose(sim.bn.flat(), g["f32_running"], rtol=1e-5, atol=1e-7)
     # conv biases before a BatchNorm get a gradient that is zero up to rounding: compare with
-    # an absolute tolerance at the scale of the other entries
-    np.testing.assert_allclose(_sampled(grad, "vgg11_bn"), g["f32_samp"], rtol=1e-3, atol=1e-7)
+    # an absolute tolerance at the scale of that rounding noise (1.4e-7 on an EPYC build host
+    # whose oneDNN paths differ from the golden generator's)
+    np.testing.assert_allclose(_sampled(grad, "vgg11_bn"), g["f32_samp"], rtol=1e-3, atol=5e-7)
     bn64 = MR.BNState(torch.float64)
     g64, l64 = sim.grad_of(sim.theta, [(0, 0, 0)], dtype=torch.float64, bn=bn64)
     assert abs(l64[0] - float(g["f64_loss"])) < 1e-12
@@ -251,20 +257,26 @@ def test_vgg11_bn_oracle_trajectory_and_eval(golden):
     sim = MR.OracleSim(3, delay=2, throttle=True, pool=(imgs, labels), model="vgg11_bn")
     for t, ref in enumerate(g["train_losses"]):
         loss = sim.epoch()
-        assert abs(loss - ref) <= 1e-5, (t, loss, ref)
+        # host-CPU fp32 drift after the first Adam steps, as in test_training_trajectory
+        assert abs(loss - ref) <= (1e-5 if t < 2 else 1e-3), (t, loss, ref)
         np.testing.assert_allclose(
             [float((a.astype(np.float64) ** 2).sum())
              for a in MR.split_flat(sim.theta, "vgg11_bn")][2::4],     # BatchNorm weights
             g[f"train_theta{t}_stats"][2::4, 1], rtol=1e-4)
     assert sim.bn.num_batches_tracked == int(g["train_nbt"][0])
-    _check_running(sim.bn.flat(), g["train_running"])
+    # running_mean: the pre-BatchNorm conv biases' Adam steps of +-lr on rounding noise enter it
+    # directly, so two hosts differ by up to lr * epochs (8e-4 seen on an EPYC build host);
+    # running_var within 1e-2 (2.7e-3 seen there in the 512-channel layers)
+    _check_running(sim.bn.flat(), g["train_running"], rm_atol=3e-3, rv_rtol=1e-2)
     timgs, _ = O.make_test_pool(0)
     params = [torch.from_numpy(a) for a in MR.split_flat(sim.theta, "vgg11_bn")]
     sim.bn.training = False
     with torch.no_grad():
         logits = MR.vgg_bn_forward(params, torch.from_numpy(O.normalize_lut()[timgs[:64]]), None,
                                    sim.bn)
-    np.testing.assert_allclose(logits.double().numpy(), g["eval_logits"], rtol=1e-3, atol=1e-4)
+    # the same 3-epoch host drift reaches the logits (9e-4 absolute on the EPYC build host); the
+    # tight pin of the forward is the one-step test above
+    np.testing.assert_allclose(logits.double().numpy(), g["eval_logits"], rtol=1e-3, atol=3e-3)
 
 
 def test_warm_start_fixture_is_pinned():
