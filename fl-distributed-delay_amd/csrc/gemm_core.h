@@ -108,12 +108,7 @@ struct IsStaged : std::false_type {};
 template <class E>
 struct IsStaged<E, std::void_t<decltype(E::STAGED)>> : std::bool_constant<E::STAGED> {};
 
-// PF = register prefetch depth: 1 = the loads of tile ks + 2 are issued at step ks and written to
-// LDS at step ks + 1 (one k-step of latency budget); 2 = two register sets alternate, the loads of
-// tile ks + 3 are issued at step ks and written at step ks + 2 (two k-steps of budget, for the
-// weight gradients whose operand re-reads miss L2: profiles/r03a/pmc).  The MFMA order is the
-// same, so both give identical results.
-template <int FM, int FN, int WAVES_M, int WAVES_N, class AL, class BL, class EPI, int PF = 1>
+template <int FM, int FN, int WAVES_M, int WAVES_N, class AL, class BL, class EPI>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N)
 gemm_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, int tiles_m,
             int tiles_n) {
@@ -174,78 +169,10 @@ gemm_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, int t
     f32x4 rb[BL::UNITS];
     constexpr int BUF = A_FL + B_FL;
 
-    // one k-step of MFMAs on LDS buffer `cur` (+ the fused bias-gradient column sums)
-    auto step_mfma = [&](int cur) {
-        const float* A = lds + cur * BUF;
-        const float* B = A + A_FL;
-        if constexpr (EPI::ASUM) {
-            static_assert(!AL::KC, "ASUM needs a k-major A tile");
-            if (tn == 0 && tid < BM) {
-#pragma unroll
-                for (int k = 0; k < GK; ++k) asum += A[k * KMTile<BM>::STRIDE + tid];
-            }
-        }
-        f32x4 af[FM], bf[FN];
-#pragma unroll
-        for (int i = 0; i < FM; ++i) af[i] = read_frag<AL::KC, BM>(A, wm * 16 * FM + 16 * i, lane);
-#pragma unroll
-        for (int j = 0; j < FN; ++j) bf[j] = read_frag<BL::KC, BN>(B, wn * 16 * FN + 16 * j, lane);
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk)
-#pragma unroll
-            for (int i = 0; i < FM; ++i)
-#pragma unroll
-                for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(af[i][kk], bf[j][kk], acc[i][j]);
-    };
-
     // Staging pipeline: the registers hold the NEXT tile's loads for a whole k-step.  At the top
     // of step ks (after the barrier that ended step ks-1, so nobody still reads that buffer) the
     // tile ks+1 loaded during step ks-1 is written to the other LDS buffer and the loads of tile
     // ks+2 are issued at once; the MFMAs of step ks then hide their latency.
-    if constexpr (PF == 2) {
-        // two register sets: set 0 holds odd-offset tiles (ks0 + 1, + 3, ...), set 1 even ones;
-        // loads past the split re-read its last tile (unconditional loads keep the compiler from
-        // serialising the prefetch on a phi), and those values are never stored
-        f32x4 ra1[AL::UNITS], rb1[BL::UNITS];
-        const int kl = ks1 - 1;
-        auto kc = [&](int k) { return k < kl ? k : kl; };
-        if (ks0 < ks1) {
-            al.load(ks0, ra);
-            bl.load(ks0, rb);
-            al.store(lds, ra);
-            bl.store(lds + A_FL, rb);
-            al.load(kc(ks0 + 1), ra);
-            bl.load(kc(ks0 + 1), rb);
-            al.load(kc(ks0 + 2), ra1);
-            bl.load(kc(ks0 + 2), rb1);
-        }
-        __syncthreads();
-        if constexpr (WAVES_M * WAVES_N == 8) {
-            if (wave >= 4) __builtin_amdgcn_s_setprio(1);
-        }
-        int cur = 0;
-        for (int ks = ks0; ks < ks1; ks += 2) {
-            if (ks + 1 < ks1) {
-                al.store(lds + (cur ^ 1) * BUF, ra);
-                bl.store(lds + (cur ^ 1) * BUF + A_FL, rb);
-                al.load(kc(ks + 3), ra);
-                bl.load(kc(ks + 3), rb);
-            }
-            step_mfma(cur);
-            __syncthreads();
-            cur ^= 1;
-            if (ks + 1 >= ks1) break;
-            if (ks + 2 < ks1) {
-                al.store(lds + (cur ^ 1) * BUF, ra1);
-                bl.store(lds + (cur ^ 1) * BUF + A_FL, rb1);
-                al.load(kc(ks + 4), ra1);
-                bl.load(kc(ks + 4), rb1);
-            }
-            step_mfma(cur);
-            __syncthreads();
-            cur ^= 1;
-        }
-    } else {
     if (ks0 < ks1) {
         al.load(ks0, ra);
         bl.load(ks0, rb);
@@ -273,12 +200,30 @@ gemm_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, int t
                 bl.load(ks + 2, rb);
             }
         }
-        // bias gradient (EPI::ASUM) fused into the weight gradient: column sums of the KM dZ
-        // tile (rows = reduction index), accumulated by the n-tile-0 blocks in K order
-        step_mfma(cur);
+        const float* A = lds + cur * BUF;
+        const float* B = A + A_FL;
+        if constexpr (EPI::ASUM) {
+            // bias gradient fused into the weight gradient: column sums of the KM dZ tile
+            // (rows = reduction index), accumulated by the n-tile-0 blocks in K order
+            static_assert(!AL::KC, "ASUM needs a k-major A tile");
+            if (tn == 0 && tid < BM) {
+#pragma unroll
+                for (int k = 0; k < GK; ++k) asum += A[k * KMTile<BM>::STRIDE + tid];
+            }
+        }
+        f32x4 af[FM], bf[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) af[i] = read_frag<AL::KC, BM>(A, wm * 16 * FM + 16 * i, lane);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bf[j] = read_frag<BL::KC, BN>(B, wn * 16 * FN + 16 * j, lane);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(af[i][kk], bf[j][kk], acc[i][j]);
         __syncthreads();
         cur ^= 1;
-    }
     }
 
     if constexpr (EPI::ASUM) {

@@ -609,7 +609,7 @@ static int fin_sum(const float* slab, int Z, long n, float* out, hipStream_t st,
 // =============================================================================================
 // GEMM launch helpers
 // =============================================================================================
-template <int FM, int FN, int WM, int WN, class AL, class BL, class EPI, int PF = 1>
+template <int FM, int FN, int WM, int WN, class AL, class BL, class EPI>
 static int launch_gemm(const AL& al, const BL& bl, const EPI& epi, int M, int N, int ksteps, int Z,
                        hipStream_t st, int kid, double alg_flops) {
     constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
@@ -617,8 +617,8 @@ static int launch_gemm(const AL& al, const BL& bl, const EPI& epi, int M, int N,
     const int tm = ceil_div(M, BM), tn = ceil_div(N, BN);
     dim3 grid(tm * tn * Z);
     const ProbeSlot ps = probe_begin();
-    hipExtLaunchKernelGGL((gemm_kernel<FM, FN, WM, WN, AL, BL, EPI, PF>), grid, dim3(64 * WM * WN),
-                          0, st, ps.start, ps.stop, 0, al, bl, epi, ksteps, per, tm, tn);
+    hipExtLaunchKernelGGL((gemm_kernel<FM, FN, WM, WN, AL, BL, EPI>), grid, dim3(64 * WM * WN), 0,
+                          st, ps.start, ps.stop, 0, al, bl, epi, ksteps, per, tm, tn);
     FLSIM_LAUNCH_CHECK();
     return probe_end(ps, kid, alg_flops);
 }
@@ -760,16 +760,6 @@ static int resident_blocks(const void* f, int nt) {
     return per * cus;
 }
 
-// register prefetch depth of the conv weight-gradient GEMMs (gemm_kernel PF; FLSIM_WG_PF)
-static int wgrad_prefetch() {
-    static int pf = -1;
-    if (pf < 0) {
-        const char* e = getenv("FLSIM_WG_PF");
-        pf = e ? atoi(e) : 1;
-    }
-    return pf;
-}
-
 // forward conv (also the data-gradient conv): out[m][n] for m < S*OH*OW, n < N
 // (OHX > 0: explicit output size, see Im2colKC)
 template <int IH, int IW, int CI, int PAD, int FM, int FN, int WM, int WN, class EPI, int OHX = 0>
@@ -828,10 +818,6 @@ static int conv_wgrad(const float* dz, const float* X, int S, int CO, int KP, fl
         resident_blocks((const void*)gemm_kernel<FM, FN, WM, WN, AL, BL, EpiSlabAcc>, NT);
     const int zu = wsplit(ceil_div(M, GK), Z, tiles, cap);
     if (zused) *zused = zu;
-    if (wgrad_prefetch() == 2)
-        return launch_gemm<FM, FN, WM, WN, AL, BL, EpiSlabAcc, 2>(al, bl, epi, CO, KP,
-                                                                  ceil_div(M, GK), zu, st, kid,
-                                                                  2.0 * M * CO * kreal);
     return launch_gemm<FM, FN, WM, WN>(al, bl, epi, CO, KP, ceil_div(M, GK), zu, st, kid,
                                        2.0 * M * CO * kreal);
 }
