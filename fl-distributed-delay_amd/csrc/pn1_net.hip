@@ -338,17 +338,109 @@ static EpochRows* epoch_rows(const void* gradstate) {
     return it == g_rows.end() ? nullptr : &it->second;
 }
 
-// the plan with each tracked segment limited to its rows written this epoch
+// Chunk pipelining (flsim_pn1_fwd_bwd_chunk_async): chunk i's forward runs on the caller's stream
+// while chunk i-1's backward runs on the gradstate's own backward stream, so the HBM-bound kernels
+// (conv1, the batch draw, pool scatter, the head) and every GEMM's last partial round of blocks
+// of one pass fill the other's gaps.  Two workspaces alternate: a forward waits for the backward
+// that last read its workspace; backwards stay in order on one stream (the slab accumulation
+// order is the synchronous path's).  Every other entry point on the gradstate first joins the
+// caller's stream to the outstanding backward work (pipe_join), so the packing of the next
+// epoch's weights, the slab reduction and the evaluations see a finished epoch.
+struct Pipe {
+    hipStream_t bs = nullptr;
+    hipEvent_t fwd_done = nullptr, bwd_tail = nullptr;
+    std::unordered_map<const void*, hipEvent_t> ws_free;   // workspace -> its last backward
+    bool pending = false;
+};
+static std::mutex g_pipe_mu;
+static std::unordered_map<const void*, Pipe> g_pipes;
+
+static int pipe_join(const void* gradstate, hipStream_t st) {
+    std::lock_guard<std::mutex> lk(g_pipe_mu);
+    auto it = g_pipes.find(gradstate);
+    if (it == g_pipes.end() || !it->second.pending) return 0;
+    Pipe& p = it->second;
+    FLSIM_CHECK_HIP(hipEventRecord(p.bwd_tail, p.bs));
+    FLSIM_CHECK_HIP(hipStreamWaitEvent(st, p.bwd_tail, 0));
+    p.pending = false;
+    return 0;
+}
+
+static void pipe_release(const void* gradstate) {
+    std::lock_guard<std::mutex> lk(g_pipe_mu);
+    auto it = g_pipes.find(gradstate);
+    if (it == g_pipes.end()) return;
+    Pipe& p = it->second;
+    (void)hipStreamSynchronize(p.bs);
+    for (auto& kv : p.ws_free) (void)hipEventDestroy(kv.second);
+    (void)hipEventDestroy(p.fwd_done);
+    (void)hipEventDestroy(p.bwd_tail);
+    (void)hipStreamDestroy(p.bs);
+    g_pipes.erase(it);
+}
+
+// the plan replanned over each tracked segment's rows written this epoch: a small chunk
+// (configs[1]: conv1..conv5 write 18-41 % of their Z rows) otherwise leaves most of the units of a
+// full-Z plan empty, each still taking part in its tile's partial hand-off.  The replanned units
+// and tiles never exceed the full plan's, so the counters and partials laid out for it suffice.
 static StepPlan plan_in_use(const GradState& g, const void* gradstate) {
-    StepPlan p = g.plan;
     const EpochRows* er = epoch_rows(gradstate);
-    if (!er) return p;
-    for (int i = 0; i < p.nseg; ++i)
-        if (p.seg[i].group >= 0) {
-            const int z = er->z[p.seg[i].group];
-            p.seg[i].zlim = z < p.seg[i].Z ? z : p.seg[i].Z;
+    if (!er) return g.plan;
+    SegSpec specs[STEP_MAX_SEG];
+    const int n = pn1_segments(g, reinterpret_cast<const float*>(gradstate), specs);
+    int zin[STEP_MAX_SEG];
+    for (int i = 0; i < n; ++i) {
+        zin[i] = specs[i].Z;
+        if (specs[i].group >= 0) {
+            const int z = er->z[specs[i].group];
+            zin[i] = z < specs[i].Z ? z : specs[i].Z;
+            specs[i].Z = zin[i] > 0 ? zin[i] : 1;
         }
+    }
+    StepPlan p;
+    plan_step(specs, n, &p);
+    // plan_step orders the segments by class: match them back by slab offset for zlim
+    for (int i = 0; i < p.nseg; ++i)
+        for (int j = 0; j < n; ++j)
+            if (specs[j].slab_off == p.seg[i].slab_off) p.seg[i].zlim = zin[j];
     return p;
+}
+
+// Small chunks run each layer's weight gradient on a second stream beside its data gradient (the
+// two read the same dZ and write different outputs): at 640 samples (configs[1]) or a 128-sample
+// fwd_bkwd call every GEMM is a few rounds of blocks, and the other one fills the last, partial
+// round.  The side stream joins back before a data gradient overwrites a buffer a queued weight
+// gradient still reads (gx holds dz5, dz3, dz1 in turn) and at the end of the backward pass.
+// One non-blocking side stream and two events per device, created on first use.
+struct SideStream {
+    hipStream_t s = nullptr;
+    hipEvent_t to_side = nullptr, to_main = nullptr;
+};
+static SideStream* side_stream() {
+    static std::mutex mu;
+    static std::unordered_map<int, SideStream> per_dev;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    SideStream& ss = per_dev[dev];
+    if (!ss.s) {
+        if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&ss.to_side, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&ss.to_main, hipEventDisableTiming) != hipSuccess) {
+            ss = SideStream{};
+            return nullptr;
+        }
+    }
+    return &ss;
+}
+static bool concurrent_backward(int S) {
+    static int smax = -1;
+    if (smax < 0) {
+        // measurement override: the largest chunk (samples) that runs the two streams; 0: off
+        const char* e = getenv("FLSIM_CONCURRENT_BWD");
+        smax = e ? atoi(e) : 2048;
+    }
+    return S <= smax;
 }
 
 static int backward(const GradState& g, const WS& w, const float* theta, int S, int dropout,
@@ -358,15 +450,31 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     int zu[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const float s25 = dropout ? SCALE_P25 : 1.f;
     const float s50 = dropout ? SCALE_P50 : 1.f;
+    SideStream* ss = concurrent_backward(S) ? side_stream() : nullptr;
+    hipStream_t sw = ss ? ss->s : st;              // the weight gradients' stream
+    auto fork = [&]() -> int {                     // sw sees everything queued on st so far
+        if (!ss) return 0;
+        FLSIM_CHECK_HIP(hipEventRecord(ss->to_side, st));
+        FLSIM_CHECK_HIP(hipStreamWaitEvent(ss->s, ss->to_side, 0));
+        return 0;
+    };
+    auto join = [&]() -> int {                     // st waits for everything queued on sw
+        if (!ss) return 0;
+        FLSIM_CHECK_HIP(hipEventRecord(ss->to_main, ss->s));
+        FLSIM_CHECK_HIP(hipStreamWaitEvent(st, ss->to_main, 0));
+        return 0;
+    };
     // ---- linear3 weight/bias (head already produced dlog, dh2) ----
     RC(head_wgrad<256>(w.dlog, w.e2, g.l3w, g.l3b, S, ZH, st));
     // ---- linear2: wgrad, bias, dgrad (-> dh1 through dropout/relu of linear1) ----
-    RC((linear_wgrad<4, 4, 2, 2>(w.dh2, w.e1, g.l2w, g.l2b, S, 256, 512, ZL2W, st, K_L2W, zi(7),
+    RC(fork());
+    RC((linear_wgrad<4, 4, 2, 2>(w.dh2, w.e1, g.l2w, g.l2b, S, 256, 512, ZL2W, sw, K_L2W, zi(7),
                                  &zu[7])));
     RC((linear_dgrad<2, 2, 2, 2>(w.dh2, theta + P_OFF[14], w.dh1, w.e1, s50, S, 256, 512, st,
                                  K_L2D)));
     // ---- linear1: wgrad, bias, dgrad (-> gradient wrt d3 through dropout1 site 3) ----
-    RC((linear_wgrad<4, 4, 2, 2>(w.dh1, w.d3, g.l1w, g.l1b, S, 512, 9408, ZL1W, st, K_L1W, zi(6),
+    RC(fork());
+    RC((linear_wgrad<4, 4, 2, 2>(w.dh1, w.d3, g.l1w, g.l1b, S, 512, 9408, ZL1W, sw, K_L1W, zi(6),
                                  &zu[6])));
     RC((linear_dgrad<4, 4, 2, 2>(w.dh1, theta + P_OFF[12], w.gy, w.d3, s25, S, 512, 9408, st,
                                  K_L1D)));
@@ -377,39 +485,46 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC((pool_scatter<14, 14, 192, true>(w.gy, w.i3, w.a6, S, st)));
     float* dz6 = w.a6;
     // ---- conv6: wgrad (input a5), bias, dgrad -> dz5 = . * (a5 > 0) into gx ----
+    RC(fork());
     RC((conv_wgrad<13, 13, 192, 2, 6, 3, 2, 4, 14, true>(dz6, w.a5, S, 192, 1728, g.sw[5],
-                                                        g.sb[5], GEO[5].ZW, st, K_WG6, 1728, zi(5),
+                                                        g.sb[5], GEO[5].ZW, sw, K_WG6, 1728, zi(5),
                                              &zu[5])));
     RC((conv_direct_sz<14, 14, 192, 0, 2, 1, 6, 8, 6, 2, false, 13>(dz6, S, g.wd[5], 192, 1728,
         EpiMask<true>{w.gx, w.a5, S * 13 * 13, 192}, st, K_DG6, 1728)));
     float* dz5 = w.gx;
     // ---- conv5: wgrad (input d2), bias, dgrad -> grad wrt d2 (dropout site 2), scattered through
     //      pool2 straight into dz4 (a4 buffer; EpiDropScatterRows, no gy round trip) ----
+    RC(fork());
     RC((conv_wgrad<11, 11, 96, 2, 6, 3, 2, 2>(dz5, w.d2, S, 192, 864, g.sw[4], g.sb[4], GEO[4].ZW,
-                                             st, K_WG5, 864, zi(4),
+                                             sw, K_WG5, 864, zi(4),
                                              &zu[4])));
     RC((conv_direct_sz<13, 13, 192, 0, 2, 1, 6, 8, 3, 2, false, 0>(dz5, S, g.wd[4], 96, 1728,
         EpiDropScatterRows<11, 11, 96>{w.a4, w.d2, w.i2, s25, S * 11 * 11}, st, K_DG5, 1728)));
     float* dz4 = w.a4;
     // ---- conv4: wgrad (input a3), bias, dgrad -> dz3 = . * (a3 > 0) into gx ----
+    RC(join());                                   // conv5's wgrad reads gx = dz5: done first
+    RC(fork());
     RC((conv_wgrad<20, 20, 96, 2, 3, 3, 2, 2>(dz4, w.a3, S, 96, 864, g.sw[3], g.sb[3], GEO[3].ZW,
-                                             st, K_WG4, 864, zi(3),
+                                             sw, K_WG4, 864, zi(3),
                                              &zu[3])));
     RC((conv_direct<22, 22, 96, 0, 2, 6, 8, 3, 2, false, 0>(dz4, S, g.wd[3], 96, 864,
         EpiMask<true>{w.gx, w.a3, S * 20 * 20, 96}, st, K_DG4, 864)));
     float* dz3 = w.gx;
     // ---- conv3: wgrad (input d1), bias, dgrad -> grad wrt d1 (site 1), scattered through pool1
     //      straight into dz2 (a2 buffer) ----
+    RC(fork());
     RC((conv_wgrad<18, 18, 48, 2, 3, 3, 2, 1>(dz3, w.d1, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW,
-                                             st, K_WG3, 432, zi(2),
+                                             sw, K_WG3, 432, zi(2),
                                              &zu[2])));
     // (gemm_kernel: the direct-A form measured 3.87 vs 3.78 ms with this staged epilogue, r03b)
     RC((conv_like_sz<20, 20, 96, 0, 4, 2, 3, 4, 1>(dz3, S, g.wd[2], 48, 864,
         EpiDropScatterRows<18, 18, 48>{w.a2, w.d1, w.i1, s25, S * 18 * 18}, st, K_DG3, 864)));
     float* dz2 = w.a2;
     // ---- conv2: wgrad (input a1), bias, dgrad -> dz1 = . * (a1 > 0) into gx ----
+    RC(join());                                   // conv3's wgrad reads gx = dz3: done first
+    RC(fork());
     RC((conv_wgrad<34, 34, 48, 2, 3, 3, 1, 1>(dz2, w.a1, S, 48, 432, g.sw[1], g.sb[1], GEO[1].ZW,
-                                             st, K_WG2, 432, zi(1),
+                                             sw, K_WG2, 432, zi(1),
                                              &zu[1])));
     RC((conv_direct_sz<36, 36, 48, 0, 2, 1, 3, 8, 3, 2, false, 0>(dz2, S, g.wd[1], 48, 432,
         EpiMaskRows<48>{w.gx, w.a1, S * 34 * 34}, st, K_DG2, 432)));
@@ -418,6 +533,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     // (3 waves of 16 rows each: 0.272 vs 0.325 ms for one 48x48 wave, profiles/r01c/lab_conv1.txt)
     RC((conv_wgrad<32, 32, 4, 2, 1, 3, 3, 1>(dz1, w.x0, S, 48, 48, g.sw[0], g.sb[0], GEO[0].ZW, st,
                                             K_WG1, 27, zi(0), &zu[0])));
+    RC(join());                                   // the next chunk's forward rewrites a1, a2
     if (er)
         for (int i = 0; i < 8; ++i)
             if (zu[i] > er->z[i]) er->z[i] = zu[i];
@@ -454,6 +570,7 @@ int flsim_pn1_workspace_offset(int which, int samples, long* offset_bytes) {
 
 int flsim_pn1_begin_epoch(void* gradstate, const float* theta, hipStream_t stream) {
     FLSIM_REQUIRE(gradstate && theta, "null pointer");
+    RC(pipe_join(gradstate, stream));
     GradState g = gs_layout((float*)gradstate);
     RC(pack_weights(g, theta, stream));
     // only the head's slabs (k_head_wgrad accumulates) and the step's tile counters are cleared;
@@ -469,6 +586,7 @@ int flsim_pn1_begin_epoch(void* gradstate, const float* theta, hipStream_t strea
 // forget the gradstate's slab-row table (the engine that owns the buffer is going away; the
 // caching allocator may hand the same address to a new engine)
 void flsim_pn1_release(void* gradstate) {
+    pipe_release(gradstate);
     std::lock_guard<std::mutex> lk(g_rows_mu);
     g_rows.erase(gradstate);
 }
@@ -505,12 +623,59 @@ int flsim_pn1_fwd_bwd_chunk(void* gradstate, void* workspace, int max_samples, c
     FLSIM_REQUIRE(S <= max_samples, "chunk of %d samples exceeds workspace (%d)", S, max_samples);
     FLSIM_REQUIRE(S <= 16384, "chunk of %d samples exceeds the 32-bit index budget", S);
     FLSIM_REQUIRE(len_a > 0 && len_b > 0, "empty class list");
+    RC(pipe_join(gradstate, stream));
     WS w = ws_layout((char*)workspace, max_samples);
     hipLaunchKernelGGL(k_fill_batch, dim3(S), dim3(256), 0, stream, pool, labels, list_a, len_a,
                        list_b, len_b, workers, n_workers_total, seed, lut, w.x0, w.y);
     FLSIM_LAUNCH_CHECK();
     return run_chunk(gradstate, w, theta, workers, n_chunk_workers, seed, dropout, backward_pass,
                      worker_loss, stream);
+}
+
+// the same chunk, pipelined: fill + forward + head on `stream`, the backward on the gradstate's
+// backward stream after this forward and after the previous chunk's backward; `workspace` must
+// not be the one the previous call used (alternate two).  Losses are ordered on `stream`; the
+// gradients are complete for any later entry point on the gradstate (pipe_join).
+int flsim_pn1_fwd_bwd_chunk_async(void* gradstate, void* workspace, int max_samples,
+                                  const float* theta, const uint8_t* pool, const int32_t* labels,
+                                  const int32_t* list_a, int len_a, const int32_t* list_b,
+                                  int len_b, const float* lut, const WorkerRec* workers,
+                                  int n_chunk_workers, int n_workers_total, uint64_t seed,
+                                  int dropout, float* worker_loss, hipStream_t stream) {
+    FLSIM_REQUIRE(gradstate && workspace && theta && pool && labels && list_a && list_b && lut &&
+                  workers && worker_loss, "null pointer");
+    FLSIM_REQUIRE(n_chunk_workers > 0, "empty chunk");
+    const int S = n_chunk_workers * SAMPLES_PER_WORKER;
+    FLSIM_REQUIRE(S <= max_samples, "chunk of %d samples exceeds workspace (%d)", S, max_samples);
+    FLSIM_REQUIRE(S <= 16384, "chunk of %d samples exceeds the 32-bit index budget", S);
+    FLSIM_REQUIRE(len_a > 0 && len_b > 0, "empty class list");
+    EpochRows* er = epoch_rows(gradstate);
+    FLSIM_REQUIRE(er, "backward pass without flsim_pn1_begin_epoch on this gradstate");
+    std::lock_guard<std::mutex> lk(g_pipe_mu);
+    Pipe& p = g_pipes[gradstate];
+    if (!p.bs) {
+        FLSIM_CHECK_HIP(hipStreamCreateWithFlags(&p.bs, hipStreamNonBlocking));
+        FLSIM_CHECK_HIP(hipEventCreateWithFlags(&p.fwd_done, hipEventDisableTiming));
+        FLSIM_CHECK_HIP(hipEventCreateWithFlags(&p.bwd_tail, hipEventDisableTiming));
+    }
+    hipEvent_t& ws_ev = p.ws_free[workspace];
+    if (!ws_ev) FLSIM_CHECK_HIP(hipEventCreateWithFlags(&ws_ev, hipEventDisableTiming));
+    else FLSIM_CHECK_HIP(hipStreamWaitEvent(stream, ws_ev, 0));   // its last backward is done
+    WS w = ws_layout((char*)workspace, max_samples);
+    GradState g = gs_layout((float*)gradstate);
+    hipLaunchKernelGGL(k_fill_batch, dim3(S), dim3(256), 0, stream, pool, labels, list_a, len_a,
+                       list_b, len_b, workers, n_workers_total, seed, lut, w.x0, w.y);
+    FLSIM_LAUNCH_CHECK();
+    RC(forward(g, w, theta, S, workers, seed, dropout, stream));
+    RC(head_and_loss<256>(w.e2, theta + P_OFF[16], theta + P_OFF[17], w.y, w.loss_s, w.dlog, w.dh2,
+                          S, 1, dropout ? SCALE_P50 : 1.f, 1.f / SAMPLES_PER_WORKER, worker_loss,
+                          stream, workers));
+    FLSIM_CHECK_HIP(hipEventRecord(p.fwd_done, stream));
+    FLSIM_CHECK_HIP(hipStreamWaitEvent(p.bs, p.fwd_done, 0));
+    RC(backward(g, w, theta, S, dropout, p.bs, er));
+    FLSIM_CHECK_HIP(hipEventRecord(ws_ev, p.bs));
+    p.pending = true;
+    return 0;
 }
 
 // explicit batch (the Worker.fwd_bkwd(inp, outp) facade, agents.py:32-35): x NCHW fp32, y int64,
@@ -528,6 +693,7 @@ int flsim_pn1_fwd_bwd_input(void* gradstate, void* workspace, int max_samples, c
     FLSIM_REQUIRE(S <= max_samples, "batch of %d samples exceeds workspace (%d)", n_samples,
                   max_samples);
     FLSIM_REQUIRE(S <= 16384, "batch of %d samples exceeds the 32-bit index budget", n_samples);
+    RC(pipe_join(gradstate, stream));
     WS w = ws_layout((char*)workspace, max_samples);
     hipLaunchKernelGGL(k_load_input, dim3(S), dim3(256), 0, stream, x, y, n_samples, w.x0, w.y);
     FLSIM_LAUNCH_CHECK();
@@ -544,6 +710,7 @@ int flsim_pn1_eval_input(void* gradstate, void* workspace, int max_samples, cons
     FLSIM_REQUIRE(max_samples >= SAMPLES_PER_WORKER && max_samples % SAMPLES_PER_WORKER == 0,
                   "max_samples must be a positive multiple of %d", SAMPLES_PER_WORKER);
     GradState g = gs_layout((float*)gradstate);
+    RC(pipe_join(gradstate, stream));
     WS w = ws_layout((char*)workspace, max_samples);
     RC(pack_weights(g, theta, stream));
     const int cap = max_samples < 16384 ? max_samples : 16384;
@@ -571,6 +738,7 @@ int flsim_pn1_eval_pool(void* gradstate, void* workspace, int max_samples, const
     FLSIM_REQUIRE(max_samples >= SAMPLES_PER_WORKER && max_samples % SAMPLES_PER_WORKER == 0,
                   "max_samples must be a positive multiple of %d", SAMPLES_PER_WORKER);
     GradState g = gs_layout((float*)gradstate);
+    RC(pipe_join(gradstate, stream));
     WS w = ws_layout((char*)workspace, max_samples);
     RC(pack_weights(g, theta, stream));
     const int cap = max_samples < 16384 ? max_samples : 16384;   // 32-bit index budget
@@ -590,6 +758,7 @@ int flsim_pn1_eval_pool(void* gradstate, void* workspace, int max_samples, const
 // S_t (torch named_parameters layout, P floats) = sum of the epoch's slabs (fixed order)
 int flsim_pn1_end_epoch(void* gradstate, float* grad_out, hipStream_t stream) {
     FLSIM_REQUIRE(gradstate && grad_out, "null pointer");
+    RC(pipe_join(gradstate, stream));
     GradState g = gs_layout((float*)gradstate);
     return slab_step_launch((float*)gradstate, plan_in_use(g, gradstate), g.cnt_off, g.part_off,
                             grad_out, nullptr, nullptr, nullptr, nullptr, nullptr, P_TOTAL, stream);
@@ -600,6 +769,7 @@ int flsim_pn1_server_step(void* gradstate, float* S_out, const flsim_rule* rule,
                           float* m, float* v, long step, double lr, double beta1, double beta2,
                           double eps, hipStream_t stream) {
     FLSIM_REQUIRE(gradstate && rule && p && m && v, "null pointer");
+    RC(pipe_join(gradstate, stream));
     GradState g = gs_layout((float*)gradstate);
     RuleProg R;
     RC(make_rule(rule, &R));

@@ -33,6 +33,7 @@ EXPORTS = [
     "flsim_cascade_program", "flsim_cascade_eval_host",
     "flsim_probe_enable", "flsim_probe_read", "flsim_probe_disable",
     "flsim_probe_kernel_count", "flsim_probe_kernel_name", "flsim_pn1_release",
+    "flsim_pn1_fwd_bwd_chunk_async",
     "flsim_aggregate_adam_rule_push",
 ]
 
@@ -100,6 +101,9 @@ def lib():
     L.flsim_vgg11_bn_update_running.argtypes = [vp, vp, ctypes.c_int, vp]
     L.flsim_pn1_release.argtypes = [vp]
     L.flsim_pn1_release.restype = None
+    L.flsim_pn1_fwd_bwd_chunk_async.argtypes = [
+        vp, vp, ctypes.c_int, vp, vp, vp, vp, ctypes.c_int, vp, ctypes.c_int, vp, vp,
+        ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_int, vp, vp]
     L.flsim_aggregate_adam.argtypes = [
         vp, ctypes.c_int, vp, ctypes.c_int, vp, vp, vp, ctypes.c_long, vp, ctypes.c_int,
         ctypes.c_long, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp]

@@ -133,6 +133,22 @@ class NetEngine:
             int(n_chunk), int(n_workers_total), ctypes.c_uint64(seed), int(bool(dropout)),
             int(bool(backward)), ptr(loss_out), *self._stats_arg(stats_out), stream_ptr()))
 
+    # pipelined chunks (PN1Engine): chunk i's forward on the current stream overlaps chunk i-1's
+    # backward on the library's backward stream; two workspaces alternate
+    PIPELINE = False
+
+    def run_chunk_async(self, theta, pool, workers_dev, n_chunk, n_workers_total, seed, dropout,
+                        loss_out, slot):
+        if getattr(self, "workspace2", None) is None:
+            self.workspace2 = torch.empty_like(self.workspace)
+        ws = self.workspace if slot % 2 == 0 else self.workspace2
+        check(lib().flsim_pn1_fwd_bwd_chunk_async(
+            ptr(self.gradstate), ptr(ws), self.max_samples, ptr(theta),
+            ptr(pool.imgs), ptr(pool.labels), ptr(pool.list_a), int(pool.list_a.numel()),
+            ptr(pool.list_b), int(pool.list_b.numel()), ptr(pool.lut), ptr(workers_dev),
+            int(n_chunk), int(n_workers_total), ctypes.c_uint64(seed), int(bool(dropout)),
+            ptr(loss_out), stream_ptr()))
+
     def evaluate_input(self, theta, x):
         """Predictions for an explicit NCHW fp32 batch (util.py:31-45's model(images) in eval
         mode): device int32 tensor of argmax indices."""
@@ -211,6 +227,7 @@ class NetEngine:
 class PN1Engine(NetEngine):
     PREFIX = "pn1"
     MODEL = "PerformantNet1"
+    PIPELINE = True
     SHAPES = PN1_SHAPES
     FLOP_PER_WORKER_STEP = 147_641_499_648
     WORKSPACE = ("x0 a1 a2 d1 a3 a4 d2 a5 a6 d3 e1 e2 dh1 dh2 gx gy loss_s dlog y i1 i2 i3").split()

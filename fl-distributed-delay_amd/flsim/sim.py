@@ -76,6 +76,9 @@ class FLSimulation:
         # (flsim_<net>_server_step); keep_S also writes S_t into comm[:P] (tests, debugging)
         self.fused = bool(fused)
         self.keep_S = bool(keep_S)
+        # pipelined chunks (PN1): FLSIM_PIPELINE=0 turns it off (measurement)
+        import os
+        self.pipeline = os.environ.get("FLSIM_PIPELINE", "1") != "0"
         self.group = group
         self.model = model
         # --batch_size B (main.py:43-44): every worker-step is G = ceil(B/128) 128-sample groups
@@ -268,7 +271,16 @@ class FLSimulation:
             stats.zero_()
         eng.begin_epoch(self.theta)
         wt = self._worker_table(t, active[lo:hi], ks)      # one async upload per epoch
-        for c0, c1 in self.chunks(lo * G, hi * G):
+        chunks = self.chunks(lo * G, hi * G)
+        # several chunks: pipelined (chunk i's forward beside chunk i-1's backward, two
+        # workspaces); the library joins the backward stream at end_epoch / server_step
+        pipe = self.pipeline and len(chunks) > 1 and getattr(eng, "PIPELINE", False) and \
+            not self.nstat
+        for j, (c0, c1) in enumerate(chunks):
+            if pipe:
+                eng.run_chunk_async(self.theta, self.pool, wt[c0 - lo * G:c1 - lo * G], c1 - c0,
+                                    self.n, self.seed, self.dropout, losses[c0:c1], j)
+                continue
             kw = {"stats_out": stats[c0:c1]} if self.nstat else {}
             eng.run_chunk(self.theta, self.pool, wt[c0 - lo * G:c1 - lo * G], c1 - c0, self.n,
                           self.seed, self.dropout, losses[c0:c1], **kw)

@@ -78,6 +78,19 @@ int flsim_pn1_fwd_bwd_chunk(void* gradstate, void* workspace, int max_samples, c
                             const WorkerRec* workers, int n_chunk_workers, int n_workers_total,
                             uint64_t seed, int dropout, int backward_pass, float* worker_loss,
                             flsim_stream_t stream);
+/* pipelined variant of flsim_pn1_fwd_bwd_chunk (backward_pass always 1), the engine side of the
+ * same main.py:137-178 worker loop: the batch draw, forward and loss run on `stream`, the
+ * backward on the gradstate's own backward stream after this forward and after the previous
+ * call's backward, so one chunk's forward overlaps the previous chunk's backward.  Successive
+ * calls must alternate two workspaces (a forward waits for the backward that last used its
+ * workspace).  Every other flsim_pn1_* entry point on the gradstate first makes `stream` wait
+ * for the outstanding backward work, so end_epoch / server_step / begin_epoch see all chunks. */
+int flsim_pn1_fwd_bwd_chunk_async(void* gradstate, void* workspace, int max_samples,
+                                  const float* theta, const uint8_t* pool, const int32_t* labels,
+                                  const int32_t* list_a, int len_a, const int32_t* list_b,
+                                  int len_b, const float* lut, const WorkerRec* workers,
+                                  int n_chunk_workers, int n_workers_total, uint64_t seed,
+                                  int dropout, float* worker_loss, flsim_stream_t stream);
 /* explicit batch variant (Worker.fwd_bkwd(inp, outp), agents.py:32): x NCHW fp32 [n][3][32][32],
  * y int64 [n], any n >= 1 (main.py:43-44 --batch_size; at most 16384): padded to whole groups of
  * 128 samples that add nothing; the gradient is CrossEntropyLoss's mean over the n samples
