@@ -76,9 +76,11 @@ class FLSimulation:
         # (flsim_<net>_server_step); keep_S also writes S_t into comm[:P] (tests, debugging)
         self.fused = bool(fused)
         self.keep_S = bool(keep_S)
-        # pipelined chunks (PN1): FLSIM_PIPELINE=0 turns it off (measurement)
+        # pipelined chunks (PN1), FLSIM_PIPELINE=1: off by default -- +0.4 % on the headline
+        # (961 -> 965 worker-steps/s, profiles/r03d) but the per-kernel live timing then measures
+        # overlapped kernels
         import os
-        self.pipeline = os.environ.get("FLSIM_PIPELINE", "1") != "0"
+        self.pipeline = os.environ.get("FLSIM_PIPELINE", "0") != "0"
         self.group = group
         self.model = model
         # --batch_size B (main.py:43-44): every worker-step is G = ceil(B/128) 128-sample groups
