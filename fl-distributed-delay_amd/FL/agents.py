@@ -134,6 +134,11 @@ class _ModelContext:
         self.G = None            # flat gradient buffer of the current epoch (p.grad views)
         self.dirty = False       # G lags the slabs (fwd_bkwd ran since the last reduction)
         self.touched = False     # a .grad view was used this epoch: update_model reads G
+        # pipelined fwd_bkwd (PN1): a call's backward runs beside the next call's forward;
+        # FLSIM_FACADE_PIPELINE=0 turns it off
+        import os
+        self.pipeline = os.environ.get("FLSIM_FACADE_PIPELINE", "1") != "0"
+        self.slot = 0
         self.carry = None        # gradient accumulated before an engine resize this epoch
         self.packed = False
         self.step = 0
@@ -356,8 +361,16 @@ class Worker:
                 raise NotImplementedError("vgg11_bn: the HIP engine runs BatchNorm in train mode "
                                           "on 128-sample batches (main.py:43-44, 132)")
             kw = {"stats_out": ctx.bn_stats}
-        eng.run_input(theta, inp.to(ctx.device, torch.float32), outp.to(ctx.device), wt,
-                      ctx.seed, self.model.training, lb, **kw)
+        x = inp.to(ctx.device, torch.float32)
+        if ctx.bn_stats is None and getattr(eng, "PIPELINE", False) and ctx.pipeline:
+            # the backward overlaps the next call's forward (the loss below needs only this
+            # forward); the .grad views join it on first use, update_model in its server step
+            ctx.slot ^= 1
+            eng.run_input_async(theta, x, outp.to(ctx.device), wt, ctx.seed, self.model.training,
+                                lb, ctx.slot)
+        else:
+            eng.run_input(theta, x, outp.to(ctx.device), wt, ctx.seed, self.model.training, lb,
+                          **kw)
         if ctx.bn_stats is not None:             # nn.BatchNorm2d's running update, this call
             eng.update_running(ctx.bn_stats, 1)
             for mod in ctx.bns:

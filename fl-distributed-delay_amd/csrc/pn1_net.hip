@@ -636,19 +636,13 @@ int flsim_pn1_fwd_bwd_chunk(void* gradstate, void* workspace, int max_samples, c
 // backward stream after this forward and after the previous chunk's backward; `workspace` must
 // not be the one the previous call used (alternate two).  Losses are ordered on `stream`; the
 // gradients are complete for any later entry point on the gradstate (pipe_join).
-int flsim_pn1_fwd_bwd_chunk_async(void* gradstate, void* workspace, int max_samples,
-                                  const float* theta, const uint8_t* pool, const int32_t* labels,
-                                  const int32_t* list_a, int len_a, const int32_t* list_b,
-                                  int len_b, const float* lut, const WorkerRec* workers,
-                                  int n_chunk_workers, int n_workers_total, uint64_t seed,
-                                  int dropout, float* worker_loss, hipStream_t stream) {
-    FLSIM_REQUIRE(gradstate && workspace && theta && pool && labels && list_a && list_b && lut &&
-                  workers && worker_loss, "null pointer");
-    FLSIM_REQUIRE(n_chunk_workers > 0, "empty chunk");
-    const int S = n_chunk_workers * SAMPLES_PER_WORKER;
-    FLSIM_REQUIRE(S <= max_samples, "chunk of %d samples exceeds workspace (%d)", S, max_samples);
-    FLSIM_REQUIRE(S <= 16384, "chunk of %d samples exceeds the 32-bit index budget", S);
-    FLSIM_REQUIRE(len_a > 0 && len_b > 0, "empty class list");
+}  // extern "C"
+
+// one pipelined pass: `front` (batch fill, forward, loss) on `stream`, then the backward on the
+// gradstate's backward stream; a forward waits for the backward that last read its workspace
+template <class Front>
+static int run_pipelined(void* gradstate, void* workspace, int max_samples, const float* theta,
+                         int S, int dropout, hipStream_t stream, Front&& front) {
     EpochRows* er = epoch_rows(gradstate);
     FLSIM_REQUIRE(er, "backward pass without flsim_pn1_begin_epoch on this gradstate");
     std::lock_guard<std::mutex> lk(g_pipe_mu);
@@ -663,19 +657,65 @@ int flsim_pn1_fwd_bwd_chunk_async(void* gradstate, void* workspace, int max_samp
     else FLSIM_CHECK_HIP(hipStreamWaitEvent(stream, ws_ev, 0));   // its last backward is done
     WS w = ws_layout((char*)workspace, max_samples);
     GradState g = gs_layout((float*)gradstate);
-    hipLaunchKernelGGL(k_fill_batch, dim3(S), dim3(256), 0, stream, pool, labels, list_a, len_a,
-                       list_b, len_b, workers, n_workers_total, seed, lut, w.x0, w.y);
-    FLSIM_LAUNCH_CHECK();
-    RC(forward(g, w, theta, S, workers, seed, dropout, stream));
-    RC(head_and_loss<256>(w.e2, theta + P_OFF[16], theta + P_OFF[17], w.y, w.loss_s, w.dlog, w.dh2,
-                          S, 1, dropout ? SCALE_P50 : 1.f, 1.f / SAMPLES_PER_WORKER, worker_loss,
-                          stream, workers));
+    RC(front(g, w));
     FLSIM_CHECK_HIP(hipEventRecord(p.fwd_done, stream));
     FLSIM_CHECK_HIP(hipStreamWaitEvent(p.bs, p.fwd_done, 0));
     RC(backward(g, w, theta, S, dropout, p.bs, er));
     FLSIM_CHECK_HIP(hipEventRecord(ws_ev, p.bs));
     p.pending = true;
     return 0;
+}
+
+extern "C" {
+
+int flsim_pn1_fwd_bwd_chunk_async(void* gradstate, void* workspace, int max_samples,
+                                  const float* theta, const uint8_t* pool, const int32_t* labels,
+                                  const int32_t* list_a, int len_a, const int32_t* list_b,
+                                  int len_b, const float* lut, const WorkerRec* workers,
+                                  int n_chunk_workers, int n_workers_total, uint64_t seed,
+                                  int dropout, float* worker_loss, hipStream_t stream) {
+    FLSIM_REQUIRE(gradstate && workspace && theta && pool && labels && list_a && list_b && lut &&
+                  workers && worker_loss, "null pointer");
+    FLSIM_REQUIRE(n_chunk_workers > 0, "empty chunk");
+    const int S = n_chunk_workers * SAMPLES_PER_WORKER;
+    FLSIM_REQUIRE(S <= max_samples, "chunk of %d samples exceeds workspace (%d)", S, max_samples);
+    FLSIM_REQUIRE(S <= 16384, "chunk of %d samples exceeds the 32-bit index budget", S);
+    FLSIM_REQUIRE(len_a > 0 && len_b > 0, "empty class list");
+    return run_pipelined(gradstate, workspace, max_samples, theta, S, dropout, stream,
+                         [&](const GradState& g, const WS& w) -> int {
+        hipLaunchKernelGGL(k_fill_batch, dim3(S), dim3(256), 0, stream, pool, labels, list_a,
+                           len_a, list_b, len_b, workers, n_workers_total, seed, lut, w.x0, w.y);
+        FLSIM_LAUNCH_CHECK();
+        RC(forward(g, w, theta, S, workers, seed, dropout, stream));
+        return head_and_loss<256>(w.e2, theta + P_OFF[16], theta + P_OFF[17], w.y, w.loss_s,
+                                  w.dlog, w.dh2, S, 1, dropout ? SCALE_P50 : 1.f,
+                                  1.f / SAMPLES_PER_WORKER, worker_loss, stream, workers);
+    });
+}
+
+// the explicit-batch form pipelined (the Worker.fwd_bkwd facade): the call's loss is ready on
+// `stream` after its forward; its backward overlaps the next call's forward
+int flsim_pn1_fwd_bwd_input_async(void* gradstate, void* workspace, int max_samples,
+                                  const float* theta, const float* x, const int64_t* y,
+                                  int n_samples, const WorkerRec* workers, uint64_t seed,
+                                  int dropout, float* worker_loss, hipStream_t stream) {
+    FLSIM_REQUIRE(gradstate && workspace && theta && x && y && workers && worker_loss,
+                  "null pointer");
+    FLSIM_REQUIRE(n_samples > 0, "empty batch");
+    const int S = ceil_div(n_samples, SAMPLES_PER_WORKER) * SAMPLES_PER_WORKER;
+    FLSIM_REQUIRE(S <= max_samples, "batch of %d samples exceeds workspace (%d)", n_samples,
+                  max_samples);
+    FLSIM_REQUIRE(S <= 16384, "batch of %d samples exceeds the 32-bit index budget", n_samples);
+    return run_pipelined(gradstate, workspace, max_samples, theta, S, dropout, stream,
+                         [&](const GradState& g, const WS& w) -> int {
+        hipLaunchKernelGGL(k_load_input, dim3(S), dim3(256), 0, stream, x, y, n_samples, w.x0,
+                           w.y);
+        FLSIM_LAUNCH_CHECK();
+        RC(forward(g, w, theta, S, workers, seed, dropout, stream));
+        return head_and_loss<256>(w.e2, theta + P_OFF[16], theta + P_OFF[17], w.y, w.loss_s,
+                                  w.dlog, w.dh2, S, 1, dropout ? SCALE_P50 : 1.f,
+                                  1.f / (float)n_samples, worker_loss, stream, workers);
+    });
 }
 
 // explicit batch (the Worker.fwd_bkwd(inp, outp) facade, agents.py:32-35): x NCHW fp32, y int64,

@@ -33,7 +33,7 @@ EXPORTS = [
     "flsim_cascade_program", "flsim_cascade_eval_host",
     "flsim_probe_enable", "flsim_probe_read", "flsim_probe_disable",
     "flsim_probe_kernel_count", "flsim_probe_kernel_name", "flsim_pn1_release",
-    "flsim_pn1_fwd_bwd_chunk_async",
+    "flsim_pn1_fwd_bwd_chunk_async", "flsim_pn1_fwd_bwd_input_async",
     "flsim_aggregate_adam_rule_push",
 ]
 
@@ -104,6 +104,8 @@ def lib():
     L.flsim_pn1_fwd_bwd_chunk_async.argtypes = [
         vp, vp, ctypes.c_int, vp, vp, vp, vp, ctypes.c_int, vp, ctypes.c_int, vp, vp,
         ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_int, vp, vp]
+    L.flsim_pn1_fwd_bwd_input_async.argtypes = [
+        vp, vp, ctypes.c_int, vp, vp, vp, ctypes.c_int, vp, ctypes.c_uint64, ctypes.c_int, vp, vp]
     L.flsim_aggregate_adam.argtypes = [
         vp, ctypes.c_int, vp, ctypes.c_int, vp, vp, vp, ctypes.c_long, vp, ctypes.c_int,
         ctypes.c_long, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp]

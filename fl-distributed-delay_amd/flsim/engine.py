@@ -149,6 +149,19 @@ class NetEngine:
             int(n_chunk), int(n_workers_total), ctypes.c_uint64(seed), int(bool(dropout)),
             ptr(loss_out), stream_ptr()))
 
+    def run_input_async(self, theta, x, y, workers_dev, seed, dropout, loss_out, slot):
+        """run_input with the backward pipelined (PN1Engine): the loss is ready on the current
+        stream after the forward; the gradient is complete for every later entry point."""
+        if getattr(self, "workspace2", None) is None:
+            self.workspace2 = torch.empty_like(self.workspace)
+        ws = self.workspace if slot % 2 == 0 else self.workspace2
+        x = x.contiguous()
+        y = y.to(torch.int64).contiguous()
+        check(lib().flsim_pn1_fwd_bwd_input_async(
+            ptr(self.gradstate), ptr(ws), self.max_samples, ptr(theta), ptr(x), ptr(y),
+            int(x.shape[0]), ptr(workers_dev), ctypes.c_uint64(seed), int(bool(dropout)),
+            ptr(loss_out), stream_ptr()))
+
     def evaluate_input(self, theta, x):
         """Predictions for an explicit NCHW fp32 batch (util.py:31-45's model(images) in eval
         mode): device int32 tensor of argmax indices."""

@@ -91,6 +91,14 @@ int flsim_pn1_fwd_bwd_chunk_async(void* gradstate, void* workspace, int max_samp
                                   int len_b, const float* lut, const WorkerRec* workers,
                                   int n_chunk_workers, int n_workers_total, uint64_t seed,
                                   int dropout, float* worker_loss, flsim_stream_t stream);
+/* pipelined form of flsim_pn1_fwd_bwd_input (backward_pass always 1; the facade's
+ * Worker.fwd_bkwd, agents.py:32-40): worker_loss is ready on `stream` after the forward, and the
+ * backward overlaps the next call's forward.  Same workspace alternation and join rule as
+ * flsim_pn1_fwd_bwd_chunk_async. */
+int flsim_pn1_fwd_bwd_input_async(void* gradstate, void* workspace, int max_samples,
+                                  const float* theta, const float* x, const int64_t* y,
+                                  int n_samples, const WorkerRec* workers, uint64_t seed,
+                                  int dropout, float* worker_loss, flsim_stream_t stream);
 /* explicit batch variant (Worker.fwd_bkwd(inp, outp), agents.py:32): x NCHW fp32 [n][3][32][32],
  * y int64 [n], any n >= 1 (main.py:43-44 --batch_size; at most 16384): padded to whole groups of
  * 128 samples that add nothing; the gradient is CrossEntropyLoss's mean over the n samples
