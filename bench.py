@@ -325,6 +325,14 @@ def main():
                         per_kernel={k: dict(launches=c, avg_ms=round(m / c, 4),
                                             tflops=round(f / (m / 1e3) / 1e12, 1))
                                     for k, (c, m, f) in sorted(kern.items())})
+        # chunks of <= FLSIM_CONCURRENT_BWD samples (default 2048: configs[1]) run each weight
+        # gradient on a second stream beside its data gradient, and FLSIM_PIPELINE=1 overlaps a
+        # chunk's forward with the previous chunk's backward: the per-kernel durations then
+        # include the other stream's share of the chip
+        conc = int(os.environ.get("FLSIM_CONCURRENT_BWD", "2048"))
+        roofline["overlapped_streams"] = bool(
+            (args.model == "PerformantNet1" and sim.engine.max_samples <= conc) or
+            os.environ.get("FLSIM_PIPELINE", "0") != "0")
     agg = None
     if agg_rec:
         cnt, ms, byts = agg_rec

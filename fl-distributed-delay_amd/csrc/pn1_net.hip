@@ -305,7 +305,9 @@ static int forward(const GradState& g, const WS& w, const float* theta, int S,
     // linear1 + relu + dropout2 (models.py:41-43), split-K partials then finish
     // small chunks (configs[1]: 640 samples = 5 x 4 tiles of 128 x 128, 80 blocks with the split)
     // take 64 x 64 tiles: the same split, hence the same sums, with 4x the blocks
-    if (S <= 4096)
+    if (S <= 2048)          // 32 x 64 tiles: 640 blocks at configs[1]'s 640 samples
+        RC((linear_fwd<1, 2, 2, 2>(w.d3, theta + P_OFF[12], w.part, S, 512, 9408, ZL1F, st, K_L1F)));
+    else if (S <= 4096)
         RC((linear_fwd<2, 2, 2, 2>(w.d3, theta + P_OFF[12], w.part, S, 512, 9408, ZL1F, st, K_L1F)));
     else
         RC((linear_fwd<4, 4, 2, 2>(w.d3, theta + P_OFF[12], w.part, S, 512, 9408, ZL1F, st, K_L1F)));
@@ -476,8 +478,12 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC(fork());
     RC((linear_wgrad<4, 4, 2, 2>(w.dh1, w.d3, g.l1w, g.l1b, S, 512, 9408, ZL1W, sw, K_L1W, zi(6),
                                  &zu[6])));
-    RC((linear_dgrad<4, 4, 2, 2>(w.dh1, theta + P_OFF[12], w.gy, w.d3, s25, S, 512, 9408, st,
-                                 K_L1D)));
+    if (S <= 2048)          // 64 x 128 tiles: twice the blocks of 128 x 128 on a small chunk
+        RC((linear_dgrad<2, 4, 2, 2>(w.dh1, theta + P_OFF[12], w.gy, w.d3, s25, S, 512, 9408, st,
+                                     K_L1D)));
+    else
+        RC((linear_dgrad<4, 4, 2, 2>(w.dh1, theta + P_OFF[12], w.gy, w.d3, s25, S, 512, 9408, st,
+                                     K_L1D)));
     // ---- pool3 backward -> dz6 (a6 buffer: conv6 fwd no longer writes it) ----
     // Row/column 14 of conv6's 15x15 output is never pooled (floor mode), so its dz is zero: dz6
     // is stored compact as [S][14][14][192].  The weight gradient then runs over those rows as

@@ -201,6 +201,13 @@ static void conv_wgrad(const char* tag, const float* dz, const float* X, float* 
         printf("%-24s skipped: Z * CO * KP exceeds the lab's slab capacity\n", tag);
         return;
     }
+    if (Z == 0) {   // the product's split for this chunk (net_kernels.h wsplit: >= 32 k-steps
+                    // per split, >= 1024 blocks)
+        const int tiles = ceil_div(CO, BM) * ceil_div(KP, BN);
+        const int ks = ceil_div(M, GK);
+        Z = (ks + 31) / 32;
+        if (Z < (1024 + tiles - 1) / tiles) Z = (1024 + tiles - 1) / tiles;
+    }
     AL al;
     al.P = dz;
     al.ld = CO;
@@ -315,6 +322,24 @@ int main(int argc, char** argv) {
     G("wgx4 96x96 4w", 20, 96, 96, 1024, 3, 3, 2, 2, 1, 0, 0)
     G("wgx4 96x288 6w", 20, 96, 96, 1024, 3, 3, 2, 6, 1, 0, 0)
     G("wgx4 48x288 6w", 20, 96, 96, 1024, 3, 3, 1, 6, 1, 0, 0)
+    // round 3: small chunks (FLSIM_LAB_S=640, configs[1]), product splits (Z = 0)
+    G("s6 wg2 48x48 1w", 34, 48, 48, 0, 3, 3, 1, 1, 1, 0, 0)
+    G("s6 wg2 48x96 2w", 34, 48, 48, 0, 3, 3, 1, 2, 1, 0, 0)
+    G("s6 wg2 48x144 3w", 34, 48, 48, 0, 3, 3, 1, 3, 1, 0, 0)
+    G("s6 wg2 48x144 1w", 34, 48, 48, 0, 3, 9, 1, 1, 1, 0, 0)
+    G("s6 wg3 96x48 2w", 18, 48, 96, 0, 3, 3, 2, 1, 1, 0, 0)
+    G("s6 wg3 96x96 4w", 18, 48, 96, 0, 3, 3, 2, 2, 1, 0, 0)
+    G("s6 wg3 48x48 1w", 18, 48, 96, 0, 3, 3, 1, 1, 1, 0, 0)
+    G("s6 wg3 48x144 3w", 18, 48, 96, 0, 3, 3, 1, 3, 1, 0, 0)
+    G("s6 wg4 96x96 4w", 20, 96, 96, 0, 3, 3, 2, 2, 1, 0, 0)
+    G("s6 wg4 96x48 2w", 20, 96, 96, 0, 3, 3, 2, 1, 1, 0, 0)
+    G("s6 wg4 48x96 2w", 20, 96, 96, 0, 3, 3, 1, 2, 1, 0, 0)
+    G("s6 wg5 192x96 4w", 11, 96, 192, 0, 6, 3, 2, 2, 1, 0, 0)
+    G("s6 wg5 96x96 4w", 11, 96, 192, 0, 3, 3, 2, 2, 1, 0, 0)
+    G("s6 wg5 192x48 2w", 11, 96, 192, 0, 6, 3, 2, 1, 1, 0, 0)
+    G("s6 wg6 192x192 8w", 13, 192, 192, 0, 6, 3, 2, 4, 1, 0, 0)
+    G("s6 wg6 192x96 4w", 13, 192, 192, 0, 6, 3, 2, 2, 1, 0, 0)
+    G("s6 wg6 96x96 4w", 13, 192, 192, 0, 3, 3, 2, 2, 1, 0, 0)
     // vgg11 (padding 1), the product's 128x128 4-wave tile against others
     F("vfwd2 128x128 4w", 16, 64, 1, 128, 4, 4, 2, 2, 1, 0)
     F("vfwd2 128x128 8w", 16, 64, 1, 128, 2, 4, 4, 2, 1, 0)
