@@ -822,6 +822,21 @@ static int conv_wgrad(const float* dz, const float* X, int S, int CO, int KP, fl
                                        2.0 * M * CO * kreal);
 }
 
+// conv_wgrad with a second tile for chunks of at most small_chunk_samples() samples
+// (profiles/r03f/lab_s640_wgrad.txt: at 640 samples 96x96 4-wave tiles beat the 128-worker
+// chunk's larger ones on conv3/5/6 by 3-10 %, 48x144 beats 48x48 on conv2 by 4 %)
+template <int IH, int IW, int CI, int PAD, int FM, int FN, int WM, int WN, int FMS, int FNS,
+          int WMS, int WNS, int VO = 0, bool DZC = false>
+static int conv_wgrad_sz(const float* dz, const float* X, int S, int CO, int KP, float* slab,
+                         float* bslab, int Z, hipStream_t st, int kid, int kreal, int zinit,
+                         int* zused) {
+    if (S <= small_chunk_samples())
+        return conv_wgrad<IH, IW, CI, PAD, FMS, FNS, WMS, WNS, VO, DZC>(
+            dz, X, S, CO, KP, slab, bslab, Z, st, kid, kreal, zinit, zused);
+    return conv_wgrad<IH, IW, CI, PAD, FM, FN, WM, WN, VO, DZC>(dz, X, S, CO, KP, slab, bslab, Z,
+                                                                st, kid, kreal, zinit, zused);
+}
+
 // forward conv fused with bias + ReLU + 2x2 max-pool (+ dropout: keep iff philox >= thr, kept
 // values * scale): GEMM rows in pool-window order
 template <int IH, int IW, int CI, int CO, int PAD, int FM, int FN, int WM, int WN, bool NCHW_OUT>

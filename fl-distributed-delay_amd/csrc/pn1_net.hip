@@ -492,7 +492,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     float* dz6 = w.a6;
     // ---- conv6: wgrad (input a5), bias, dgrad -> dz5 = . * (a5 > 0) into gx ----
     RC(fork());
-    RC((conv_wgrad<13, 13, 192, 2, 6, 3, 2, 4, 14, true>(dz6, w.a5, S, 192, 1728, g.sw[5],
+    RC((conv_wgrad_sz<13, 13, 192, 2, 6, 3, 2, 4, 3, 3, 2, 2, 14, true>(dz6, w.a5, S, 192, 1728, g.sw[5],
                                                         g.sb[5], GEO[5].ZW, sw, K_WG6, 1728, zi(5),
                                              &zu[5])));
     RC((conv_direct_sz<14, 14, 192, 0, 2, 1, 6, 8, 6, 2, false, 13>(dz6, S, g.wd[5], 192, 1728,
@@ -501,7 +501,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     // ---- conv5: wgrad (input d2), bias, dgrad -> grad wrt d2 (dropout site 2), scattered through
     //      pool2 straight into dz4 (a4 buffer; EpiDropScatterRows, no gy round trip) ----
     RC(fork());
-    RC((conv_wgrad<11, 11, 96, 2, 6, 3, 2, 2>(dz5, w.d2, S, 192, 864, g.sw[4], g.sb[4], GEO[4].ZW,
+    RC((conv_wgrad_sz<11, 11, 96, 2, 6, 3, 2, 2, 3, 3, 2, 2>(dz5, w.d2, S, 192, 864, g.sw[4], g.sb[4], GEO[4].ZW,
                                              sw, K_WG5, 864, zi(4),
                                              &zu[4])));
     RC((conv_direct_sz<13, 13, 192, 0, 2, 1, 6, 8, 3, 2, false, 0>(dz5, S, g.wd[4], 96, 1728,
@@ -519,7 +519,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     // ---- conv3: wgrad (input d1), bias, dgrad -> grad wrt d1 (site 1), scattered through pool1
     //      straight into dz2 (a2 buffer) ----
     RC(fork());
-    RC((conv_wgrad<18, 18, 48, 2, 3, 3, 2, 1>(dz3, w.d1, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW,
+    RC((conv_wgrad_sz<18, 18, 48, 2, 3, 3, 2, 1, 3, 3, 2, 2>(dz3, w.d1, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW,
                                              sw, K_WG3, 432, zi(2),
                                              &zu[2])));
     // (gemm_kernel: the direct-A form measured 3.87 vs 3.78 ms with this staged epilogue, r03b)
@@ -529,7 +529,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     // ---- conv2: wgrad (input a1), bias, dgrad -> dz1 = . * (a1 > 0) into gx ----
     RC(join());                                   // conv3's wgrad reads gx = dz3: done first
     RC(fork());
-    RC((conv_wgrad<34, 34, 48, 2, 3, 3, 1, 1>(dz2, w.a1, S, 48, 432, g.sw[1], g.sb[1], GEO[1].ZW,
+    RC((conv_wgrad_sz<34, 34, 48, 2, 3, 3, 1, 1, 3, 3, 1, 3>(dz2, w.a1, S, 48, 432, g.sw[1], g.sb[1], GEO[1].ZW,
                                              sw, K_WG2, 432, zi(1),
                                              &zu[1])));
     RC((conv_direct_sz<36, 36, 48, 0, 2, 1, 3, 8, 3, 2, false, 0>(dz2, S, g.wd[1], 48, 432,

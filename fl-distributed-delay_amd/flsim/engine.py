@@ -126,6 +126,7 @@ class NetEngine:
                   loss_out, backward=True, stats_out=None):
         """stats_out (BatchNorm models): device float[n_chunk][STATS_PER_WORKER] for the
         per-call statistics that update_running() folds into the running buffers."""
+        self.last_workspace = self.workspace
         check(self._fn("fwd_bwd_chunk")(
             ptr(self.gradstate), ptr(self.workspace), self.max_samples, ptr(theta),
             ptr(pool.imgs), ptr(pool.labels), ptr(pool.list_a), int(pool.list_a.numel()),
@@ -142,6 +143,7 @@ class NetEngine:
         if getattr(self, "workspace2", None) is None:
             self.workspace2 = torch.empty_like(self.workspace)
         ws = self.workspace if slot % 2 == 0 else self.workspace2
+        self.last_workspace = ws
         check(lib().flsim_pn1_fwd_bwd_chunk_async(
             ptr(self.gradstate), ptr(ws), self.max_samples, ptr(theta),
             ptr(pool.imgs), ptr(pool.labels), ptr(pool.list_a), int(pool.list_a.numel()),
@@ -155,6 +157,7 @@ class NetEngine:
         if getattr(self, "workspace2", None) is None:
             self.workspace2 = torch.empty_like(self.workspace)
         ws = self.workspace if slot % 2 == 0 else self.workspace2
+        self.last_workspace = ws
         x = x.contiguous()
         y = y.to(torch.int64).contiguous()
         check(lib().flsim_pn1_fwd_bwd_input_async(
@@ -169,6 +172,7 @@ class NetEngine:
         n = int(x.shape[0])
         pred = torch.empty(n, dtype=torch.int32, device=self.device)
         extra = (ptr(self.running),) if self.STATS_PER_WORKER else ()
+        self.last_workspace = self.workspace
         check(self._fn("eval_input")(ptr(self.gradstate), ptr(self.workspace), self.max_samples,
                                      ptr(theta), ptr(x), n, *extra, ptr(pred), stream_ptr()))
         return pred
@@ -177,6 +181,7 @@ class NetEngine:
                   stats_out=None):
         x = x.contiguous()
         y = y.to(torch.int64).contiguous()
+        self.last_workspace = self.workspace
         check(self._fn("fwd_bwd_input")(
             ptr(self.gradstate), ptr(self.workspace), self.max_samples, ptr(theta), ptr(x), ptr(y),
             int(x.shape[0]), ptr(workers_dev), ctypes.c_uint64(seed), int(bool(dropout)),
@@ -188,6 +193,7 @@ class NetEngine:
         n = int(pool.imgs.shape[0]) - first if n_images is None else int(n_images)
         pred = torch.empty(n, dtype=torch.int32, device=self.device)
         extra = (ptr(self.running),) if self.STATS_PER_WORKER else ()
+        self.last_workspace = self.workspace
         check(self._fn("eval_pool")(
             ptr(self.gradstate), ptr(self.workspace), self.max_samples, ptr(theta), ptr(pool.imgs),
             int(first), n, ptr(pool.lut), *extra, ptr(pred), stream_ptr()))
@@ -219,7 +225,9 @@ class NetEngine:
         off = ctypes.c_long()
         check(self._fn("workspace_offset")(which, self.max_samples, ctypes.byref(off)))
         n = int(np.prod(shape)) * torch.tensor([], dtype=dtype).element_size()
-        return self.workspace[off.value:off.value + n].view(dtype).view(shape)
+        ws = getattr(self, "last_workspace", None)      # the last pass's (pipelined: alternating)
+        ws = self.workspace if ws is None else ws
+        return ws[off.value:off.value + n].view(dtype).view(shape)
 
     # -- server step ------------------------------------------------------------------------------
     def aggregate_adam(self, S, c, stale, theta, m, v, step, lr=1e-3, betas=(0.9, 0.999),
