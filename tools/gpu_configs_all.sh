@@ -12,7 +12,8 @@ run() {   # name, timeout, bench args...
         2> gpurun_out/bench_${TAG}_$name.err || { echo "$name failed $?"; tail -5 gpurun_out/bench_${TAG}_$name.err; return 1; }
     python3 -c "import json,sys; d=json.load(open('gpurun_out/bench_${TAG}_$name.json')); a=d.get('aggregation') or {}; print('$name', d['value'], 'ws/s', d['ms_per_step'], 'ms/epoch', 'agg', a.get('probe'), a.get('frac'), a.get('avg_launch_us'))"
 }
-timeout -k 10 300 python -u tools/make_warm_start.py --epochs 500 --out gpurun_out/warm_start.pt \
+# configs[1]'s warm start: the sha-pinned fixture of the trajectory test (tests/golden/warm_n10.npz)
+timeout -k 10 120 python -u tools/warm_start_file.py --out gpurun_out/warm_start.pt \
     > gpurun_out/make_warm_start_$TAG.log 2>&1 || { echo "warm start failed"; exit 1; }
 run configs1_warm 300 --n_workers 10 --delay 50 --model_file gpurun_out/warm_start.pt --steps 200 --warmup 10 || exit 1
 run configs2_d500 300 --n_workers 1024 --delay 500 --steps 8 --warmup 2 || exit 1
