@@ -155,6 +155,12 @@ def cpu_baseline(n, delay, throttle, model="PerformantNet1", configs0_epochs=3):
         p.grad = f
     opt.step()
     dt = time.perf_counter() - t0
+    # a second, shorter sample of the same per-worker loop (the first 128 of those workers) as a
+    # repeat of the measurement: the CPU rate varies with the box and its neighbours
+    nr = min(128, len(items))
+    t2 = time.perf_counter()
+    sim.grad_of(sim.theta, items[:nr])
+    rep = dict(worker_steps=nr, value=round(nr / (time.perf_counter() - t2), 3))
     c0 = None
     if configs0_epochs:
         s0 = MR.OracleSim(10, delay=50, throttle=False, pool=pool, model=model)
@@ -173,7 +179,7 @@ def cpu_baseline(n, delay, throttle, model="PerformantNet1", configs0_epochs=3):
                        f"(n={n}, d={delay}, {'throttle' if throttle else 'no throttle'}) + rule() "
                        f"over the {k} entries + one Adam step; torch CPU, {info['threads']} threads, "
                        f"{dt:.1f} s",
-                host=info, configs0=c0)
+                repeat=rep, host=info, configs0=c0)
 
 
 def stream_step_probe(sim, iters=20):
