@@ -38,6 +38,7 @@ There is no CPU fallback.
 """
 from __future__ import annotations
 
+import os
 import weakref
 
 import numpy as np
@@ -80,12 +81,14 @@ class _LazyGrad(torch.Tensor):
     def __torch_function__(cls, func, types, args=(), kwargs=None):
         kwargs = kwargs or {}
         if func not in _META:
+            seen = []
             for a in list(args) + list(kwargs.values()):
                 for x in (a if isinstance(a, (list, tuple)) else (a,)):
                     if isinstance(x, _LazyGrad):
                         ctx = x.__dict__.get("_flsim_ctx")
                         ctx = ctx() if ctx is not None else None
-                        if ctx is not None:
+                        if ctx is not None and all(c is not ctx for c in seen):
+                            seen.append(ctx)
                             ctx.flush(touched=True)
         with torch._C.DisableTorchFunctionSubclass():
             return func(*args, **kwargs)
@@ -136,7 +139,6 @@ class _ModelContext:
         self.touched = False     # a .grad view was used this epoch: update_model reads G
         # pipelined fwd_bkwd (PN1): a call's backward runs beside the next call's forward;
         # FLSIM_FACADE_PIPELINE=0 turns it off
-        import os
         self.pipeline = os.environ.get("FLSIM_FACADE_PIPELINE", "1") != "0"
         self.slot = 0
         self.carry = None        # gradient accumulated before an engine resize this epoch

@@ -18,6 +18,8 @@ Per epoch t (one "server step"):
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -79,7 +81,6 @@ class FLSimulation:
         # pipelined chunks (PN1), FLSIM_PIPELINE=1: off by default -- +0.4 % on the headline
         # (961 -> 965 worker-steps/s, profiles/r03d) but the per-kernel live timing then measures
         # overlapped kernels
-        import os
         self.pipeline = os.environ.get("FLSIM_PIPELINE", "0") != "0"
         self.group = group
         self.model = model
