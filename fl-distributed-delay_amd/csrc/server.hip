@@ -21,13 +21,9 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include <mutex>
-#include <unordered_map>
-
 #include "common.h"
 #include "flsim.h"
 #include "probe.h"
-
 #include "slabstep.h"
 
 #ifndef FLSIM_SEQ_EARLY_EXIT
@@ -860,37 +856,6 @@ int make_rule(const flsim_rule* r, RuleProg* R) {
     return 0;
 }
 
-// general-order server step on two streams (FLSIM_STEP_SEQ_STREAMS, measurement toggle)
-struct SeqStreams {
-    hipStream_t s = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
-};
-static bool seq_two_streams() {
-    static int on = -1;
-    if (on < 0) {
-        const char* e = getenv("FLSIM_STEP_SEQ_STREAMS");
-        on = e ? atoi(e) : 0;
-    }
-    return on != 0;
-}
-static SeqStreams* seq_streams() {
-    static std::mutex mu;
-    static std::unordered_map<int, SeqStreams> per_dev;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    std::lock_guard<std::mutex> lk(mu);
-    SeqStreams& ss = per_dev[dev];
-    if (!ss.s) {
-        if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&ss.join, hipEventDisableTiming) != hipSuccess) {
-            ss = SeqStreams{};
-            return nullptr;
-        }
-    }
-    return &ss;
-}
-
 int slab_step_launch(float* gradstate, const StepPlan& plan, long cnt_off, long part_off,
                      float* S_out, const RuleProg* rule, const AdamConst* ac, float* p, float* m,
                      float* v, long P, hipStream_t stream) {
@@ -947,31 +912,8 @@ int slab_step_launch(float* gradstate, const StepPlan& plan, long cnt_off, long 
                               ps.stop, 0, A);
     } else {
         RC(stage_program(*rule, stream));
-        SeqStreams* ss = (A.il_n > 0 && seq_two_streams()) ? seq_streams() : nullptr;
-        if (ss && plan.u_conv > 0 && plan.u_conv < plan.units) {
-            // two launches on two streams instead of one interleaved launch: the small and wide
-            // units (the linear layers: most of the program's arithmetic) beside the packed conv
-            // units (most of the slab bytes), so the interpreter's adds run under the stream.
-            // The span is timed by events around both (the probe's start / stop).
-            StepArgs B = A;
-            A.il_n = 0;
-            B.il_n = 0;
-            B.u_lo = plan.u_conv;
-            if (ps.start) FLSIM_CHECK_HIP(hipEventRecord(ps.start, stream));
-            FLSIM_CHECK_HIP(hipEventRecord(ss->fork, stream));
-            FLSIM_CHECK_HIP(hipStreamWaitEvent(ss->s, ss->fork, 0));
-            hipLaunchKernelGGL(k_slab_step_seq, dim3(plan.units - plan.u_conv), dim3(256), 0,
-                               ss->s, B);
-            FLSIM_LAUNCH_CHECK();
-            hipLaunchKernelGGL(k_slab_step_seq, dim3(plan.u_conv), dim3(256), 0, stream, A);
-            FLSIM_LAUNCH_CHECK();
-            FLSIM_CHECK_HIP(hipEventRecord(ss->join, ss->s));
-            FLSIM_CHECK_HIP(hipStreamWaitEvent(stream, ss->join, 0));
-            if (ps.stop) FLSIM_CHECK_HIP(hipEventRecord(ps.stop, stream));
-        } else {
-            hipExtLaunchKernelGGL(k_slab_step_seq, dim3(nblk), dim3(256), 0, stream, ps.start,
-                                  ps.stop, 0, A);
-        }
+        hipExtLaunchKernelGGL(k_slab_step_seq, dim3(nblk), dim3(256), 0, stream, ps.start,
+                              ps.stop, 0, A);
     }
     FLSIM_LAUNCH_CHECK();
     const int kid = !rule ? K_SLABSUM : (rule->prog == nullptr ? K_STEP : K_STEP_SEQ);
