@@ -108,6 +108,13 @@ struct IsStaged : std::false_type {};
 template <class E>
 struct IsStaged<E, std::void_t<decltype(E::STAGED)>> : std::bool_constant<E::STAGED> {};
 
+// Epilogues with PRE = true load the per-fragment inputs of a fragment row first
+// (pre4(m, n, z) -> f32x4), then store its fragments (apply4p(m, n, z, acc, pre))
+template <class E, class = void>
+struct HasPre : std::false_type {};
+template <class E>
+struct HasPre<E, std::void_t<decltype(E::PRE)>> : std::bool_constant<E::PRE> {};
+
 template <int FM, int FN, int WAVES_M, int WAVES_N, class AL, class BL, class EPI>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N)
 gemm_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, int tiles_m,
@@ -251,6 +258,19 @@ gemm_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, int t
             const int wm_hi = (pass + 1) * WM_PASS < WAVES_M ? (pass + 1) * WM_PASS : WAVES_M;
             epi.store_rows(lds, STAGE_LD, m0 + pass * WM_PASS * WROWS,
                            (wm_hi - pass * WM_PASS) * WROWS, tid, 64 * WAVES_M * WAVES_N);
+        }
+    } else if constexpr (HasPre<EPI>::value) {
+        // one fragment row at a time: its FN fragments' inputs are loaded before any is stored
+        // (FN round trips become one; FN * 4 extra registers, not FM * FN * 4)
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+            const int m = m0 + wm * 16 * FM + 16 * i + 4 * (lane >> 4);
+            const int nb = n0 + wn * 16 * FN + (lane & 15);
+            f32x4 pre[FN];
+#pragma unroll
+            for (int j = 0; j < FN; ++j) pre[j] = epi.pre4(m, nb + 16 * j, tz);
+#pragma unroll
+            for (int j = 0; j < FN; ++j) epi.apply4p(m, nb + 16 * j, tz, acc[i][j], pre[j]);
         }
     } else {
         // epilogue: lane holds rows 4*(lane>>4)+r, col lane&15 of each 16x16 tile

@@ -533,22 +533,37 @@ struct EpiMaskRows {
     const float* act;
     int M;
     __device__ float value(int, float v) const { return v; }
+    // the pass's mask operand is loaded for BATCH of a thread's units before any is used (one
+    // HBM round trip per pass; profiles/r03s: conv2's data gradient 6.15 -> 6.00 ms)
+    static constexpr int BATCH = 8;
     __device__ void store_rows(const float* tile, int ld, int m0, int bm, int tid, int nt) const {
         const int rows = M - m0 < bm ? M - m0 : bm;
         constexpr int N4 = NC / 4;
         f32x4* dst = reinterpret_cast<f32x4*>(Y + (long)m0 * NC);
         const f32x4* a4 = reinterpret_cast<const f32x4*>(act + (long)m0 * NC);
-        for (int q = tid; q < rows * N4; q += nt) {
+        const int total = rows * N4;
+        auto unit = [&](int q, f32x4 a) {
             const int r = q / N4, c = q - r * N4;
             const f32x4 t = *reinterpret_cast<const f32x4*>(tile + r * ld + 4 * c);
-            const f32x4 a = a4[q];
             f32x4 o;
             o.x = a.x > 0.f ? t.x : 0.f;
             o.y = a.y > 0.f ? t.y : 0.f;
             o.z = a.z > 0.f ? t.z : 0.f;
             o.w = a.w > 0.f ? t.w : 0.f;
             st_nt4(reinterpret_cast<float*>(dst + q), o);
+        };
+        f32x4 av[BATCH];
+#pragma unroll
+        for (int it = 0; it < BATCH; ++it) {
+            const int q = tid + it * nt;
+            if (q < total) av[it] = a4[q];
         }
+#pragma unroll
+        for (int it = 0; it < BATCH; ++it) {
+            const int q = tid + it * nt;
+            if (q < total) unit(q, av[it]);
+        }
+        for (int q = tid + BATCH * nt; q < total; q += nt) unit(q, a4[q]);
     }
 };
 
@@ -559,6 +574,21 @@ struct EpiDropMask {
     const float* act;
     float scale;
     int M, N;
+    __device__ f32x4 pre4(int m, int n, int) const {
+        f32x4 a = {0.f, 0.f, 0.f, 0.f};
+        if (n < N) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (m + r < M) a[r] = act[(long)(m + r) * N + n];
+        }
+        return a;
+    }
+    __device__ void apply4p(int m, int n, int z, f32x4 v, f32x4 a) const {
+        if (n >= N) return;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (m + r < M) Y[(long)(m + r) * N + n] = a[r] > 0.f ? v[r] * scale : 0.f;
+    }
     __device__ void apply4(int m, int n, int z, f32x4 v) const {
         if (n >= N) return;
 #pragma unroll
@@ -570,6 +600,16 @@ struct EpiDropMask {
     }
 };
 
+// EpiDropMask with PRE: the GEMM kernels load the mask values of a whole fragment row (pre4)
+// before storing any of it (apply4p) -- a store to Y may alias act for the compiler, which
+// otherwise keeps each fragment's loads behind the previous fragment's stores.  profiles/r03s:
+// linear1's data gradient 1.33 -> 1.23 ms; the same for EpiMask (conv4/conv6 data gradients) and
+// EpiSlabAcc (conv5 weight gradient) measured 2-7 % slower, their larger tiles lose occupancy to
+// the extra VGPRs, so only the linear data gradients use it
+struct EpiDropMaskPre : EpiDropMask {
+    static constexpr bool PRE = true;
+};
+
 // EpiDropMask fused with the 2x2 max-pool backward of the layer below (PerformantNet1 pool1 and
 // pool2, models.py:31-32,35-36): the masked gradient g of pooled element (m, n) goes straight to
 // the full-resolution dZ at the position the forward's argmax recorded (idx, 2 dy + dx), zeros to
@@ -579,8 +619,11 @@ struct EpiDropMask {
 // through LDS (gemm_core.h STAGED, the block covers all NC channels): a thread takes (pooled pixel,
 // 4 channels) and writes the four positions of its 2x2 window as float4 pieces of whole dZ pixel
 // rows (profiles/r02j: 16 scalar stores per lane from the accumulator layout were 10 % slower on
-// conv3's data gradient)
-template <int PH, int PW, int NC>
+// conv3's data gradient).  BATCH: how many of a thread's units have their pooled activations and
+// argmax bytes loaded before any is used (one HBM round trip per pass, not one per unit); 0 keeps
+// one unit at a time (profiles/r03s: batching is 2 % faster on conv3's data gradient, 2 % slower
+// on conv5's, whose 96-column tile has more VGPRs live at this point)
+template <int PH, int PW, int NC, int BATCH = 8>
 struct EpiDropScatterRows {
     static constexpr bool ASUM = false;
     static constexpr bool STAGED = true;
@@ -597,11 +640,33 @@ struct EpiDropScatterRows {
         constexpr int N4 = NC / 4;
         const f32x4* a4 = reinterpret_cast<const f32x4*>(act + (long)m0 * NC);
         const uint32_t* i4 = reinterpret_cast<const uint32_t*>(idx + (long)m0 * NC);
-        for (int q = tid; q < rows * N4; q += nt) {
+        const int total = rows * N4;
+        int q0 = tid;
+        if constexpr (BATCH > 0) {
+            f32x4 av[BATCH];
+            uint32_t iv[BATCH];
+#pragma unroll
+            for (int it = 0; it < BATCH; ++it) {
+                const int q = tid + it * nt;
+                if (q < total) {
+                    av[it] = a4[q];
+                    iv[it] = i4[q];
+                }
+            }
+#pragma unroll
+            for (int it = 0; it < BATCH; ++it) {
+                const int q = tid + it * nt;
+                if (q < total) unit(tile, ld, m0, q, av[it], iv[it]);
+            }
+            q0 = tid + BATCH * nt;
+        }
+        for (int q = q0; q < total; q += nt) unit(tile, ld, m0, q, a4[q], i4[q]);
+    }
+    __device__ void unit(const float* tile, int ld, int m0, int q, f32x4 a, uint32_t id) const {
+        constexpr int N4 = NC / 4;
+        {
             const int r = q / N4, c = q - r * N4;
             const f32x4 t = *reinterpret_cast<const f32x4*>(tile + r * ld + 4 * c);
-            const f32x4 a = a4[q];
-            const uint32_t id = i4[q];
             f32x4 g;
             g.x = a.x > 0.f ? t.x * scale : 0.f;
             g.y = a.y > 0.f ? t.y * scale : 0.f;

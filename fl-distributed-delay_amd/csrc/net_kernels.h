@@ -902,7 +902,7 @@ static int linear_dgrad(const float* dy, const float* W, float* dx, const float*
     dl.P = dy; dl.ld = N; dl.NR = S;
     RowsKM<16 * FN * WN, NT> wl{};
     wl.P = W; wl.ld = K; wl.NK = N; wl.NC = K;
-    EpiDropMask de{dx, act, scale, S, K};
+    EpiDropMaskPre de{{dx, act, scale, S, K}};
     return launch_gemm<FM, FN, WM, WN>(dl, wl, de, S, K, N / GK, 1, st, kid, 2.0 * S * N * K);
 }
 

@@ -494,46 +494,42 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     float* dz6 = w.a6;
     // ---- conv6: wgrad (input a5), bias, dgrad -> dz5 = . * (a5 > 0) into gx ----
     RC(fork());
-    RC((conv_wgrad_sz<13, 13, 192, 2, 6, 3, 2, 4, 3, 3, 2, 2, 14, true>(dz6, w.a5, S, 192, 1728, g.sw[5],
-                                                        g.sb[5], GEO[5].ZW, sw, K_WG6, 1728, zi(5),
-                                             &zu[5])));
+    RC((conv_wgrad_sz<13, 13, 192, 2, 6, 3, 2, 4, 3, 3, 2, 2, 14, true>(
+        dz6, w.a5, S, 192, 1728, g.sw[5], g.sb[5], GEO[5].ZW, sw, K_WG6, 1728, zi(5), &zu[5])));
     RC((conv_direct_sz<14, 14, 192, 0, 2, 1, 6, 8, 6, 2, false, 13>(dz6, S, g.wd[5], 192, 1728,
         EpiMask<true>{w.gx, w.a5, S * 13 * 13, 192}, st, K_DG6, 1728)));
     float* dz5 = w.gx;
     // ---- conv5: wgrad (input d2), bias, dgrad -> grad wrt d2 (dropout site 2), scattered through
     //      pool2 straight into dz4 (a4 buffer; EpiDropScatterRows, no gy round trip) ----
     RC(fork());
-    RC((conv_wgrad_sz<11, 11, 96, 2, 6, 3, 2, 2, 3, 3, 2, 2>(dz5, w.d2, S, 192, 864, g.sw[4], g.sb[4], GEO[4].ZW,
-                                             sw, K_WG5, 864, zi(4),
-                                             &zu[4])));
+    RC((conv_wgrad_sz<11, 11, 96, 2, 6, 3, 2, 2, 3, 3, 2, 2>(
+        dz5, w.d2, S, 192, 864, g.sw[4], g.sb[4], GEO[4].ZW, sw, K_WG5, 864, zi(4), &zu[4])));
     RC((conv_direct_sz<13, 13, 192, 0, 2, 1, 6, 8, 3, 2, false, 0>(dz5, S, g.wd[4], 96, 1728,
-        EpiDropScatterRows<11, 11, 96>{w.a4, w.d2, w.i2, s25, S * 11 * 11}, st, K_DG5, 1728)));
+        EpiDropScatterRows<11, 11, 96, 0>{w.a4, w.d2, w.i2, s25, S * 11 * 11}, st, K_DG5, 1728)));
     float* dz4 = w.a4;
     // ---- conv4: wgrad (input a3), bias, dgrad -> dz3 = . * (a3 > 0) into gx ----
     RC(join());                                   // conv5's wgrad reads gx = dz5: done first
     RC(fork());
-    RC((conv_wgrad<20, 20, 96, 2, 3, 3, 2, 2>(dz4, w.a3, S, 96, 864, g.sw[3], g.sb[3], GEO[3].ZW,
-                                             sw, K_WG4, 864, zi(3),
-                                             &zu[3])));
+    RC((conv_wgrad<20, 20, 96, 2, 3, 3, 2, 2>(
+        dz4, w.a3, S, 96, 864, g.sw[3], g.sb[3], GEO[3].ZW, sw, K_WG4, 864, zi(3), &zu[3])));
     RC((conv_direct<22, 22, 96, 0, 2, 6, 8, 3, 2, false, 0>(dz4, S, g.wd[3], 96, 864,
         EpiMask<true>{w.gx, w.a3, S * 20 * 20, 96}, st, K_DG4, 864)));
     float* dz3 = w.gx;
     // ---- conv3: wgrad (input d1), bias, dgrad -> grad wrt d1 (site 1), scattered through pool1
     //      straight into dz2 (a2 buffer) ----
     RC(fork());
-    RC((conv_wgrad_sz<18, 18, 48, 2, 3, 3, 2, 1, 3, 3, 2, 2>(dz3, w.d1, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW,
-                                             sw, K_WG3, 432, zi(2),
-                                             &zu[2])));
-    // (gemm_kernel: the direct-A form measured 3.87 vs 3.78 ms with this staged epilogue, r03b)
+    RC((conv_wgrad_sz<18, 18, 48, 2, 3, 3, 2, 1, 3, 3, 2, 2>(
+        dz3, w.d1, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW, sw, K_WG3, 432, zi(2), &zu[2])));
+    // (gemm_kernel: the direct-A form measured 3.87 vs 3.78 ms with this staged epilogue, r03b,
+    // and 3.97 vs 3.77 with the batched epilogue loads, profiles/r03t/r03q_dg3)
     RC((conv_like_sz<20, 20, 96, 0, 4, 2, 3, 4, 1>(dz3, S, g.wd[2], 48, 864,
         EpiDropScatterRows<18, 18, 48>{w.a2, w.d1, w.i1, s25, S * 18 * 18}, st, K_DG3, 864)));
     float* dz2 = w.a2;
     // ---- conv2: wgrad (input a1), bias, dgrad -> dz1 = . * (a1 > 0) into gx ----
     RC(join());                                   // conv3's wgrad reads gx = dz3: done first
     RC(fork());
-    RC((conv_wgrad_sz<34, 34, 48, 2, 3, 3, 1, 1, 3, 3, 1, 3>(dz2, w.a1, S, 48, 432, g.sw[1], g.sb[1], GEO[1].ZW,
-                                             sw, K_WG2, 432, zi(1),
-                                             &zu[1])));
+    RC((conv_wgrad_sz<34, 34, 48, 2, 3, 3, 1, 1, 3, 3, 1, 3>(
+        dz2, w.a1, S, 48, 432, g.sw[1], g.sb[1], GEO[1].ZW, sw, K_WG2, 432, zi(1), &zu[1])));
     RC((conv_direct_sz<36, 36, 48, 0, 2, 1, 3, 8, 3, 2, false, 0>(dz2, S, g.wd[1], 48, 432,
         EpiMaskRows<48>{w.gx, w.a1, S * 34 * 34}, st, K_DG2, 432)));
     float* dz1 = w.gx;

@@ -12,8 +12,8 @@ run() {
         > $OUT/$name.json 2> $OUT/$name.err || { echo "$name failed $?"; tail -5 $OUT/$name.err; return 1; }
     python3 tools/bench_summary.py $OUT/$name.json > $OUT/$name.txt; echo "== $name ($VAR=$val)"; head -2 $OUT/$name.txt
 }
-run head_A $A "$@" || exit 1
-run head_B $B "$@" || exit 1
-run head_A2 $A "$@" || exit 1
-run head_B2 $B "$@" || exit 1
+run head_A "$A" "$@" || exit 1
+run head_B "$B" "$@" || exit 1
+run head_A2 "$A" "$@" || exit 1
+run head_B2 "$B" "$@" || exit 1
 echo done
