@@ -178,6 +178,13 @@ struct Im2colKC {
         for (int j = 0; j < UNITS; ++j)
             if (TOTAL % NT == 0 || row[j] < ROWS) store_unit<true, ROWS>(lds, row[j], q, r[j]);
     }
+    // f(row, chunk, value) for each staged unit (the split-bf16 kernel's plane stores)
+    template <class F>
+    __device__ void each_unit(const f32x4 (&r)[UNITS], F&& f) const {
+#pragma unroll
+        for (int j = 0; j < UNITS; ++j)
+            if (TOTAL % NT == 0 || row[j] < ROWS) f(row[j], q, r[j]);
+    }
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -225,6 +232,13 @@ struct RowsKC {
 #pragma unroll
         for (int j = 0; j < UNITS; ++j)
             if (TOTAL % NT == 0 || row[j] < ROWS) store_unit<true, ROWS>(lds, row[j], q, r[j]);
+    }
+    // f(row, chunk, value) for each staged unit (the split-bf16 kernel's plane stores)
+    template <class F>
+    __device__ void each_unit(const f32x4 (&r)[UNITS], F&& f) const {
+#pragma unroll
+        for (int j = 0; j < UNITS; ++j)
+            if (TOTAL % NT == 0 || row[j] < ROWS) f(row[j], q, r[j]);
     }
 };
 

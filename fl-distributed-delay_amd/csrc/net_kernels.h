@@ -8,6 +8,7 @@
 // gradient), k in Im2colKC's channel-slice-major order (k_pack_fwd).
 #pragma once
 #include "gemm_direct.h"
+#include "gemm_x6.h"
 #include "loaders.h"
 #include "pn1.h"
 #include "probe.h"
@@ -609,7 +610,8 @@ static int fin_sum(const float* slab, int Z, long n, float* out, hipStream_t st,
 // =============================================================================================
 // GEMM launch helpers
 // =============================================================================================
-template <int FM, int FN, int WM, int WN, class AL, class BL, class EPI>
+// X6: the split-bf16 kernel (gemm_x6.h, k-contiguous operands only) instead of the fp32 one
+template <int FM, int FN, int WM, int WN, bool X6 = false, class AL, class BL, class EPI>
 static int launch_gemm(const AL& al, const BL& bl, const EPI& epi, int M, int N, int ksteps, int Z,
                        hipStream_t st, int kid, double alg_flops) {
     constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
@@ -617,8 +619,13 @@ static int launch_gemm(const AL& al, const BL& bl, const EPI& epi, int M, int N,
     const int tm = ceil_div(M, BM), tn = ceil_div(N, BN);
     dim3 grid(tm * tn * Z);
     const ProbeSlot ps = probe_begin();
-    hipExtLaunchKernelGGL((gemm_kernel<FM, FN, WM, WN, AL, BL, EPI>), grid, dim3(64 * WM * WN), 0,
-                          st, ps.start, ps.stop, 0, al, bl, epi, ksteps, per, tm, tn);
+    if constexpr (X6)
+        hipExtLaunchKernelGGL((gemm_x6_kernel<FM, FN, WM, WN, AL, BL, EPI, 2>), grid,
+                              dim3(64 * WM * WN), 0, st, ps.start, ps.stop, 0, al, bl, epi, ksteps,
+                              per, tm, tn);
+    else
+        hipExtLaunchKernelGGL((gemm_kernel<FM, FN, WM, WN, AL, BL, EPI>), grid, dim3(64 * WM * WN),
+                              0, st, ps.start, ps.stop, 0, al, bl, epi, ksteps, per, tm, tn);
     FLSIM_LAUNCH_CHECK();
     return probe_end(ps, kid, alg_flops);
 }
@@ -762,7 +769,8 @@ static int resident_blocks(const void* f, int nt) {
 
 // forward conv (also the data-gradient conv): out[m][n] for m < S*OH*OW, n < N
 // (OHX > 0: explicit output size, see Im2colKC)
-template <int IH, int IW, int CI, int PAD, int FM, int FN, int WM, int WN, class EPI, int OHX = 0>
+template <int IH, int IW, int CI, int PAD, int FM, int FN, int WM, int WN, class EPI, int OHX = 0,
+          bool X6 = false>
 static int conv_like(const float* X, int S, const float* Wpk, int N, int KP, const EPI& epi,
                      hipStream_t st, int kid, int kreal) {
     constexpr int NT = 64 * WM * WN;
@@ -776,8 +784,17 @@ static int conv_like(const float* X, int S, const float* Wpk, int N, int KP, con
     bl.P = Wpk;
     bl.ld = KP;
     bl.NR = N;
-    return launch_gemm<FM, FN, WM, WN>(al, bl, epi, al.M, N, KP / GK, 1, st, kid,
-                                       2.0 * al.M * N * kreal);
+    return launch_gemm<FM, FN, WM, WN, X6>(al, bl, epi, al.M, N, KP / GK, 1, st, kid,
+                                           2.0 * al.M * N * kreal);
+}
+
+// conv_like on the split-bf16 GEMM (gemm_x6.h): the forward and data-gradient convolutions at
+// fp32 accuracy on the bf16 matrix cores
+template <int IH, int IW, int CI, int PAD, int FM, int FN, int WM, int WN, int OHX = 0, class EPI>
+static int conv_x6(const float* X, int S, const float* Wpk, int N, int KP, const EPI& epi,
+                   hipStream_t st, int kid, int kreal) {
+    return conv_like<IH, IW, CI, PAD, FM, FN, WM, WN, EPI, OHX, true>(X, S, Wpk, N, KP, epi, st,
+                                                                      kid, kreal);
 }
 
 template <int IH, int IW, int CI, int PAD, int FM, int FMS, int FN, int WM, int WN, class EPI>
@@ -839,7 +856,8 @@ static int conv_wgrad_sz(const float* dz, const float* X, int S, int CO, int KP,
 
 // forward conv fused with bias + ReLU + 2x2 max-pool (+ dropout: keep iff philox >= thr, kept
 // values * scale): GEMM rows in pool-window order
-template <int IH, int IW, int CI, int CO, int PAD, int FM, int FN, int WM, int WN, bool NCHW_OUT>
+template <int IH, int IW, int CI, int CO, int PAD, int FM, int FN, int WM, int WN, bool NCHW_OUT,
+          bool X6 = false>
 static int conv_pool_fwd(const float* X, int S, const float* Wpk, int KP, float* d, uint8_t* idx,
                          const float* bias, const WorkerRec* workers, uint64_t seed, uint32_t site,
                          uint32_t thr, float scale, int dropout, hipStream_t st, int kid,
@@ -857,8 +875,8 @@ static int conv_pool_fwd(const float* X, int S, const float* Wpk, int KP, float*
     bl.NR = CO;
     EpiPoolDrop<AL::PH, AL::PW, CO, NCHW_OUT> epi{d, idx, bias, workers, seed, site, thr,
                                                   scale, dropout, al.M};
-    return launch_gemm<FM, FN, WM, WN>(al, bl, epi, al.M, CO, KP / GK, 1, st, kid,
-                                       2.0 * al.M * CO * kreal);
+    return launch_gemm<FM, FN, WM, WN, X6>(al, bl, epi, al.M, CO, KP / GK, 1, st, kid,
+                                           2.0 * al.M * CO * kreal);
 }
 
 // linear layer part[z] = x W^T over the z-th K range (x [M][K] rows, W [N][K] torch layout)

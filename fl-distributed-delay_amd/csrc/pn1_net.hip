@@ -290,18 +290,18 @@ static int forward(const GradState& g, const WS& w, const float* theta, int S,
     RC((conv_pool_fwd<34, 34, 48, 48, 2, 2, 3, 4, 1, false>(w.a1, S, g.wf[1], 432, w.d1, w.i1,
         theta + P_OFF[3], workers, seed, SITE_DROP1, THR_P25, SCALE_P25, dropout, st, K_FWD2,
         432)));
-    RC((conv_like<18, 18, 48, 2, 2, 3, 4, 2>(w.d1, S, g.wf[2], 96, 432,
+    RC((conv_x6<18, 18, 48, 2, 4, 3, 4, 2>(w.d1, S, g.wf[2], 96, 432,
         EpiBiasRelu{w.a3, theta + P_OFF[5], S * 20 * 20, 96}, st, K_FWD3, 432)));
     // conv4 + ReLU + pool2 + dropout1 (models.py:34-36)
-    RC((conv_pool_direct<20, 20, 96, 96, 2, 2, 6, 8, 6, 2, false>(w.a3, S, g.wf[3], 864, w.d2,
+    RC((conv_pool_fwd<20, 20, 96, 96, 2, 4, 3, 4, 2, false, true>(w.a3, S, g.wf[3], 864, w.d2,
         w.i2, theta + P_OFF[7], workers, seed, SITE_DROP2, THR_P25, SCALE_P25, dropout, st,
         K_FWD4, 864)));
-    RC((conv_direct_sz<11, 11, 96, 2, 2, 1, 6, 8, 3, 2, false, 0>(w.d2, S, g.wf[4], 192, 864,
+    RC((conv_x6<11, 11, 96, 2, 4, 6, 4, 2>(w.d2, S, g.wf[4], 192, 864,
         EpiBiasRelu{w.a5, theta + P_OFF[9], S * 13 * 13, 192}, st, K_FWD5, 864)));
     // conv6 + ReLU + pool3 + dropout1 (models.py:38-40), written in torch's flatten order
     // (models.py:41) so linear1 keeps the torch weight layout; the floor-mode border row/column
     // of the 15x15 output (dropped by the pool) is never computed
-    RC((conv_pool_direct<13, 13, 192, 192, 2, 2, 6, 8, 6, 2, true>(w.a5, S, g.wf[5], 1728, w.d3,
+    RC((conv_pool_fwd<13, 13, 192, 192, 2, 4, 6, 4, 2, true, true>(w.a5, S, g.wf[5], 1728, w.d3,
         w.i3, theta + P_OFF[11], workers, seed, SITE_DROP3, THR_P25, SCALE_P25, dropout, st,
         K_FWD6, 1728)));
     // linear1 + relu + dropout2 (models.py:41-43), split-K partials then finish
@@ -496,7 +496,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC(fork());
     RC((conv_wgrad_sz<13, 13, 192, 2, 6, 3, 2, 4, 3, 3, 2, 2, 14, true>(
         dz6, w.a5, S, 192, 1728, g.sw[5], g.sb[5], GEO[5].ZW, sw, K_WG6, 1728, zi(5), &zu[5])));
-    RC((conv_direct_sz<14, 14, 192, 0, 2, 1, 6, 8, 6, 2, false, 13>(dz6, S, g.wd[5], 192, 1728,
+    RC((conv_x6<14, 14, 192, 0, 4, 6, 4, 2, 13>(dz6, S, g.wd[5], 192, 1728,
         EpiMask<true>{w.gx, w.a5, S * 13 * 13, 192}, st, K_DG6, 1728)));
     float* dz5 = w.gx;
     // ---- conv5: wgrad (input d2), bias, dgrad -> grad wrt d2 (dropout site 2), scattered through
@@ -504,7 +504,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC(fork());
     RC((conv_wgrad_sz<11, 11, 96, 2, 6, 3, 2, 2, 3, 3, 2, 2>(
         dz5, w.d2, S, 192, 864, g.sw[4], g.sb[4], GEO[4].ZW, sw, K_WG5, 864, zi(4), &zu[4])));
-    RC((conv_direct_sz<13, 13, 192, 0, 2, 1, 6, 8, 3, 2, false, 0>(dz5, S, g.wd[4], 96, 1728,
+    RC((conv_x6<13, 13, 192, 0, 4, 3, 4, 2>(dz5, S, g.wd[4], 96, 1728,
         EpiDropScatterRows<11, 11, 96, 0>{w.a4, w.d2, w.i2, s25, S * 11 * 11}, st, K_DG5, 1728)));
     float* dz4 = w.a4;
     // ---- conv4: wgrad (input a3), bias, dgrad -> dz3 = . * (a3 > 0) into gx ----
@@ -512,7 +512,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC(fork());
     RC((conv_wgrad<20, 20, 96, 2, 3, 3, 2, 2>(
         dz4, w.a3, S, 96, 864, g.sw[3], g.sb[3], GEO[3].ZW, sw, K_WG4, 864, zi(3), &zu[3])));
-    RC((conv_direct<22, 22, 96, 0, 2, 6, 8, 3, 2, false, 0>(dz4, S, g.wd[3], 96, 864,
+    RC((conv_x6<22, 22, 96, 0, 4, 3, 4, 2>(dz4, S, g.wd[3], 96, 864,
         EpiMask<true>{w.gx, w.a3, S * 20 * 20, 96}, st, K_DG4, 864)));
     float* dz3 = w.gx;
     // ---- conv3: wgrad (input d1), bias, dgrad -> grad wrt d1 (site 1), scattered through pool1
@@ -522,7 +522,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
         dz3, w.d1, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW, sw, K_WG3, 432, zi(2), &zu[2])));
     // (gemm_kernel: the direct-A form measured 3.87 vs 3.78 ms with this staged epilogue, r03b,
     // and 3.97 vs 3.77 with the batched epilogue loads, profiles/r03t/r03q_dg3)
-    RC((conv_like_sz<20, 20, 96, 0, 4, 2, 3, 4, 1>(dz3, S, g.wd[2], 48, 864,
+    RC((conv_x6<20, 20, 96, 0, 4, 3, 8, 1>(dz3, S, g.wd[2], 48, 864,
         EpiDropScatterRows<18, 18, 48>{w.a2, w.d1, w.i1, s25, S * 18 * 18}, st, K_DG3, 864)));
     float* dz2 = w.a2;
     // ---- conv2: wgrad (input a1), bias, dgrad -> dz1 = . * (a1 > 0) into gx ----

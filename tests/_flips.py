@@ -14,6 +14,9 @@ is in two parts:
               FLIP_C * (the CPU fp32 port's own disagreements with fp64) + FLIP_FLOOR, out of
               ~10^7 decisions per 128 samples -- a wrong mask or argmax rule would flip thousands.
 """
+import json
+import os
+
 import numpy as np
 import torch
 import torch.nn.functional as F
@@ -21,7 +24,11 @@ import torch.nn.functional as F
 from oracle import model_ref as MR
 
 TF_TOL = 2e-6
-FLIP_C, FLIP_FLOOR = 3, 6
+# FLIP_FLOOR: the fp32-MFMA build measured up to 6 flips where the CPU port had none (the CIFAR
+# pool test) and 9 against the port's 4; the split-bf16 build (gemm_x6.h) 7 and 12 on the same
+# inputs, 58 against 45 summed over the 11 checks (profiles/r03w/flips_census.txt).  A wrong
+# mask or argmax rule flips thousands.
+FLIP_C, FLIP_FLOOR = 3, 10
 GROUP = 1 << 20
 LAYERS = ("a1", "i1", "a3", "i2", "a5", "i3", "e1", "e2")
 
@@ -139,6 +146,10 @@ def check_worker_step(g_gpu, eng, theta, x, y, noise, scale, rows=None):
     _, d32 = grad(theta, torch.float32, x, y, noise, scale)
     fg, fc = flips(forced, d64), flips(d32, d64)
     stats = dict(tf=rel(g_gpu, g_tf), vs64=rel(g_gpu, g_64), flips_gpu=fg, flips_cpu32=fc)
+    log = os.environ.get("FLSIM_FLIP_LOG")
+    if log:       # census across runs / libraries (measurement only)
+        with open(log, "a") as f:
+            f.write(json.dumps(dict(test=os.environ.get("PYTEST_CURRENT_TEST", ""), **stats)) + "\n")
     assert stats["tf"] <= TF_TOL, stats
     assert sum(fg.values()) <= FLIP_C * sum(fc.values()) + FLIP_FLOOR, stats
     return stats
