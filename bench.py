@@ -413,6 +413,11 @@ def main():
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            # fp32 in, fp32 accumulate; the k-contiguous convolution GEMMs split each fp32 operand
+            # into three bf16 parts and sum six exact partial products on the bf16 matrix cores
+            # (gemm_x6.h): fp32 accuracy, not a reduced-precision mode
+            "math": "fp32 MFMA (weight gradients, linear layers, conv1, conv2); bf16x6 split of "
+                    "the fp32 operands, fp32 accumulate (conv3-6 forward + data gradient)",
             "data": f"synthetic: seeded CIFAR-shaped u8 pool in HBM, "
                     + (f"{args.model} warm-started from {os.path.basename(args.model_file)}"
                        if args.model_file else f"models.py-init {args.model}")
@@ -431,7 +436,8 @@ def main():
                        "parallelism": f"workers sharded over {world} GPU(s), "
                                       f"{'1 RCCL all-reduce/step' if world > 1 and args.backend == 'nccl' else '1 gloo all-reduce/step (rehearsal)' if world > 1 else 'no collective'}"},
             # executed GEMM FLOPs of this rank (the probe's per-launch counts: conv6 skips its
-            # never-pooled border) / wall time / peak; the nominal SURVEY 8d count beside it
+            # never-pooled border) / wall time / the fp32 MFMA peak (the bf16x6 GEMMs count their
+            # fp32-equivalent FLOPs, so this can pass 1); the nominal SURVEY 8d count beside it
             "mfma_efficiency_whole_step": (round(roofline["all_gemms"]["executed_tflop"] /
                                                  (elapsed * MFMA_F32_PEAK_TFLOPS), 4)
                                            if roofline else None),

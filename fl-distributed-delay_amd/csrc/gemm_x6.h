@@ -16,6 +16,10 @@
 //     MFMA 3: A [h|l] x B [l|h]  = ah bl + al bh
 // so the LDS holds two 16-B combination planes of the A tile and three of the B tile, each laid
 // out and swizzled exactly like the fp32 KC tile, and every fragment is one ds_read_b128.
+// k-major operands (the weight gradients: the pixel is the reduction index of both dZ and im2col)
+// keep three plain planes h, m, l as [16 k][rows] bf16 and read each 4-k half with gfx950's
+// transposing ds_read_b64_tr_b16 (lane 4q+p of a 16-lane group addresses k row q, columns
+// 4p..4p+3; lane i receives column i's four k), the halves paired in registers.
 // Three 16-cycle bf16 MFMAs replace four 32-cycle fp32 ones per k-step (profiles/r03v:
 // bf16x6 max error 1.0-3.1 x 2^-24 of sum |a b| against the fp32 MFMA's 1.6-3.3 on the same
 // data, K = 1728 and 16384; pre-split operands run the inner loop at 312-316 fp32-equivalent
@@ -58,24 +62,99 @@ __device__ __forceinline__ f32x4 mfma_x32(f32x4 a, f32x4 b, f32x4 c) {
                                                    __builtin_bit_cast(bf16x8v, b), c, 0, 0, 0);
 }
 
+typedef short s16x4v __attribute__((ext_vector_type(4)));
+
+// 4 consecutive k of one tile row from a k-major bf16 plane [16][LD] (ds_read_b64_tr_b16)
+__device__ __forceinline__ bf16x4v read_km_half(const float* plane, int LD, int r0, int lane) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const __bf16* base = reinterpret_cast<const __bf16*>(plane) + (4 * g + q) * LD + r0 + 4 * p;
+    typedef __attribute__((address_space(3))) s16x4v lds_s16x4;
+    const s16x4v v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base));
+    return __builtin_bit_cast(bf16x4v, v);
+}
+
+// One operand tile of a stage.  AROLE: the A side ([h|m], [h|l]) or the B side ([h|m], [m|h],
+// [l|h]).  KC: combination planes laid out like the fp32 KC tile; KM: planes h, m, l as
+// [16][LD] bf16 (LD = ROWS + 8: rows of one transposed read land 4 dwords apart mod 64), one
+// spare 8-B slot after each for surplus units.
+template <bool KC, int ROWS, bool AROLE>
+struct X6Tile {
+    static constexpr int LD = ROWS + 8;
+    static constexpr int NPL = KC ? 2 : 3;
+    static constexpr int PLANE_FL = KC ? KCTile<ROWS>::FLOATS : (GK * LD + 4) / 2;
+    static constexpr int FL = NPL * PLANE_FL;
+    struct Frag {
+        f32x4 x0, x1, x2;
+    };
+    __device__ static void store(float* s, int a, int b, f32x4 v, bool valid) {
+        const SplitBf16 p = split_bf16(v);
+        if constexpr (KC) {
+            store_unit<true, ROWS>(s, a, b, cat_bf16(p.h, p.m));
+            store_unit<true, ROWS>(s + PLANE_FL, a, b, AROLE ? cat_bf16(p.h, p.l)
+                                                             : cat_bf16(p.l, p.h));
+        } else {
+            const int off = valid ? a * LD + 4 * b : GK * LD;   // bf16 units
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) {
+                const bf16x4v x = pl == 0 ? p.h : pl == 1 ? p.m : p.l;
+                *reinterpret_cast<bf16x4v*>(reinterpret_cast<__bf16*>(s + pl * PLANE_FL) + off) = x;
+            }
+        }
+    }
+    __device__ static Frag frag(const float* s, int r0, int lane) {
+        Frag f;
+        if constexpr (KC) {
+            f.x0 = read_frag<true, ROWS>(s, r0, lane);                        // [h|m]
+            if constexpr (AROLE) {
+                f.x1 = read_frag<true, ROWS>(s + PLANE_FL, r0, lane);         // [h|l]
+            } else {
+                f.x1 = f32x4{f.x0.z, f.x0.w, f.x0.x, f.x0.y};                 // [m|h]
+                f.x2 = read_frag<true, ROWS>(s + PLANE_FL, r0, lane);         // [l|h]
+            }
+        } else {
+            const bf16x4v h = read_km_half(s, LD, r0, lane);
+            const bf16x4v m = read_km_half(s + PLANE_FL, LD, r0, lane);
+            const bf16x4v l = read_km_half(s + 2 * PLANE_FL, LD, r0, lane);
+            f.x0 = cat_bf16(h, m);
+            if constexpr (AROLE) {
+                f.x1 = cat_bf16(h, l);
+            } else {
+                f.x1 = cat_bf16(m, h);
+                f.x2 = cat_bf16(l, h);
+            }
+        }
+        return f;
+    }
+    // column sum of a k-major tile's 16 k rows (the bias gradient, ASUM): h + m + l per element
+    __device__ static float colsum(const float* s, int col) {
+        const __bf16* ph = reinterpret_cast<const __bf16*>(s);
+        const __bf16* pm = reinterpret_cast<const __bf16*>(s + PLANE_FL);
+        const __bf16* pl = reinterpret_cast<const __bf16*>(s + 2 * PLANE_FL);
+        float a = 0.f;
+#pragma unroll
+        for (int k = 0; k < GK; ++k)
+            a += ((float)ph[k * LD + col] + (float)pm[k * LD + col]) + (float)pl[k * LD + col];
+        return a;
+    }
+};
+
 // Same contract as gemm_kernel (gemm_core.h: 1-D XCD-aware grid, register-staged double buffer,
-// one barrier per 16-deep k-step, STAGED / plain epilogues) for KC loaders that expose
-// each_unit(); no ASUM epilogues (those need k-major tiles).
-// BP = 3: B planes [h|h], [m|m], [l|h] (every fragment one ds_read_b128, no register moves);
-// BP = 2: B planes [h|m], [l|h] and the pairing ah bh + am bm, ah bm + am bh (B [m|h] = the
-// halves of [h|m] swapped in registers), ah bl + al bh: a third less LDS traffic for B.
-template <int FM, int FN, int WAVES_M, int WAVES_N, class AL, class BL, class EPI, int BP = 3>
+// one barrier per 16-deep k-step, STAGED / plain / PRE / ASUM epilogues); loaders expose
+// each_unit().  The B side of a KC tile keeps two planes [h|m], [l|h] and pairs
+// ah bh + am bm, ah bm + am bh (B [m|h] = [h|m] with its halves swapped in registers),
+// ah bl + al bh; a third plane ([h|h], [m|m], [l|h], no swaps) measured 3-24 % slower
+// (profiles/r03w/x6_lab2.txt, "BP3"): these kernels are bound by LDS bandwidth.
+template <int FM, int FN, int WAVES_M, int WAVES_N, class AL, class BL, class EPI>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N)
 gemm_x6_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, int tiles_m,
                int tiles_n) {
     constexpr int BM = 16 * FM * WAVES_M;
     constexpr int BN = 16 * FN * WAVES_N;
     static_assert(AL::ROWS == BM && BL::ROWS == BN, "loader rows != tile");
-    static_assert(AL::KC && BL::KC, "split-bf16 tiles are k-contiguous");
-    static_assert(!EPI::ASUM, "no fused column sums on k-contiguous tiles");
-    constexpr int A_FL = KCTile<BM>::FLOATS;      // one combination plane
-    constexpr int B_FL = KCTile<BN>::FLOATS;
-    constexpr int BUF = 2 * A_FL + BP * B_FL;     // one stage: A [h|m], [h|l]; B planes (BP)
+    using TA = X6Tile<AL::KC, BM, true>;
+    using TB = X6Tile<BL::KC, BN, false>;
+    static_assert(!EPI::ASUM || !AL::KC, "ASUM needs a k-major A tile");
+    constexpr int BUF = TA::FL + TB::FL;
     constexpr bool STAGED = IsStaged<EPI>::value;
     constexpr int STAGE_LD = BN + 4;
     constexpr int BASE_FL = 2 * BUF;
@@ -115,26 +194,12 @@ gemm_x6_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, in
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    float asum = 0.f;
     f32x4 ra[AL::UNITS];
     f32x4 rb[BL::UNITS];
     auto stage = [&](float* s) {
-        al.each_unit(ra, [&](int row, int c, f32x4 v) {
-            const SplitBf16 p = split_bf16(v);
-            store_unit<true, BM>(s, row, c, cat_bf16(p.h, p.m));
-            store_unit<true, BM>(s + A_FL, row, c, cat_bf16(p.h, p.l));
-        });
-        bl.each_unit(rb, [&](int row, int c, f32x4 v) {
-            const SplitBf16 p = split_bf16(v);
-            float* t = s + 2 * A_FL;
-            if constexpr (BP == 3) {
-                store_unit<true, BN>(t, row, c, cat_bf16(p.h, p.h));
-                store_unit<true, BN>(t + B_FL, row, c, cat_bf16(p.m, p.m));
-                store_unit<true, BN>(t + 2 * B_FL, row, c, cat_bf16(p.l, p.h));
-            } else {
-                store_unit<true, BN>(t, row, c, cat_bf16(p.h, p.m));
-                store_unit<true, BN>(t + B_FL, row, c, cat_bf16(p.l, p.h));
-            }
-        });
+        al.each_unit(ra, [&](int a, int c, f32x4 v, bool ok) { TA::store(s, a, c, v, ok); });
+        bl.each_unit(rb, [&](int a, int c, f32x4 v, bool ok) { TB::store(s + TA::FL, a, c, v, ok); });
     };
 
     if (ks0 < ks1) {
@@ -160,37 +225,22 @@ gemm_x6_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, in
             }
         }
         const float* A = lds + cur * BUF;
-        const float* B = A + 2 * A_FL;
-        f32x4 b0[FN], b1[FN], b2[FN];
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-            const int c0 = wn * 16 * FN + 16 * j;
-            if constexpr (BP == 3) {
-                b0[j] = read_frag<true, BN>(B, c0, lane);                 // [h|h]
-                b1[j] = read_frag<true, BN>(B + B_FL, c0, lane);          // [m|m]
-                b2[j] = read_frag<true, BN>(B + 2 * B_FL, c0, lane);      // [l|h]
-            } else {
-                b0[j] = read_frag<true, BN>(B, c0, lane);                 // [h|m]
-                b1[j] = f32x4{b0[j].z, b0[j].w, b0[j].x, b0[j].y};        // [m|h]
-                b2[j] = read_frag<true, BN>(B + B_FL, c0, lane);          // [l|h]
-            }
+        const float* B = A + TA::FL;
+        if constexpr (EPI::ASUM) {
+            if (tn == 0 && tid < BM) asum += TA::colsum(A, tid);
         }
+        typename TB::Frag bf[FN];
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bf[j] = TB::frag(B, wn * 16 * FN + 16 * j, lane);
 #pragma unroll
         for (int i = 0; i < FM; ++i) {
-            const int r0 = wm * 16 * FM + 16 * i;
-            const f32x4 ahm = read_frag<true, BM>(A, r0, lane);
-            const f32x4 ahl = read_frag<true, BM>(A + A_FL, r0, lane);
+            const typename TA::Frag af = TA::frag(A, wm * 16 * FM + 16 * i, lane);
 #pragma unroll
             for (int j = 0; j < FN; ++j) {
                 f32x4 c = acc[i][j];
-                c = mfma_x32(ahl, b2[j], c);       // ah bl + al bh: smallest terms first
-                if constexpr (BP == 3) {
-                    c = mfma_x32(ahm, b1[j], c);   // ah bm + am bm
-                    c = mfma_x32(ahm, b0[j], c);   // ah bh + am bh
-                } else {
-                    c = mfma_x32(ahm, b1[j], c);   // ah bm + am bh
-                    c = mfma_x32(ahm, b0[j], c);   // ah bh + am bm
-                }
+                c = mfma_x32(af.x1, bf[j].x2, c);     // ah bl + al bh: smallest terms first
+                c = mfma_x32(af.x0, bf[j].x1, c);     // ah bm + am bh
+                c = mfma_x32(af.x0, bf[j].x0, c);     // ah bh + am bm
                 acc[i][j] = c;
             }
         }
@@ -198,6 +248,9 @@ gemm_x6_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, in
         cur ^= 1;
     }
 
+    if constexpr (EPI::ASUM) {
+        if (tn == 0 && tid < BM) epi.asum(m0 + tid, tz, asum);
+    }
     if constexpr (STAGED) {
         static_assert(BN == EPI::NCOL, "staged epilogue needs the full row in one block");
         constexpr int PASSES = (WAVES_M + WM_PASS - 1) / WM_PASS;

@@ -178,12 +178,12 @@ struct Im2colKC {
         for (int j = 0; j < UNITS; ++j)
             if (TOTAL % NT == 0 || row[j] < ROWS) store_unit<true, ROWS>(lds, row[j], q, r[j]);
     }
-    // f(row, chunk, value) for each staged unit (the split-bf16 kernel's plane stores)
+    // f(row, chunk, value, valid) for each staged unit (the split-bf16 kernel's plane stores)
     template <class F>
     __device__ void each_unit(const f32x4 (&r)[UNITS], F&& f) const {
 #pragma unroll
         for (int j = 0; j < UNITS; ++j)
-            if (TOTAL % NT == 0 || row[j] < ROWS) f(row[j], q, r[j]);
+            if (TOTAL % NT == 0 || row[j] < ROWS) f(row[j], q, r[j], true);
     }
 };
 
@@ -233,12 +233,12 @@ struct RowsKC {
         for (int j = 0; j < UNITS; ++j)
             if (TOTAL % NT == 0 || row[j] < ROWS) store_unit<true, ROWS>(lds, row[j], q, r[j]);
     }
-    // f(row, chunk, value) for each staged unit (the split-bf16 kernel's plane stores)
+    // f(row, chunk, value, valid) for each staged unit (the split-bf16 kernel's plane stores)
     template <class F>
     __device__ void each_unit(const f32x4 (&r)[UNITS], F&& f) const {
 #pragma unroll
         for (int j = 0; j < UNITS; ++j)
-            if (TOTAL % NT == 0 || row[j] < ROWS) f(row[j], q, r[j]);
+            if (TOTAL % NT == 0 || row[j] < ROWS) f(row[j], q, r[j], true);
     }
 };
 
@@ -329,6 +329,13 @@ struct RowsKM {
         for (int j = 0; j < UNITS; ++j)
             store_km_or_spare<ROWS>(lds, C4 % TPR == 0 || c4[j] < C4, krow, c4[j], r[j]);
     }
+    // f(k row, column chunk, value, valid) for each staged unit (split-bf16 plane stores; a
+    // surplus unit has valid = false and goes to the plane's spare slot)
+    template <class F>
+    __device__ void each_unit(const f32x4 (&r)[UNITS], F&& f) const {
+#pragma unroll
+        for (int j = 0; j < UNITS; ++j) f(krow, c4[j], r[j], C4 % TPR == 0 || c4[j] < C4);
+    }
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -409,6 +416,13 @@ struct Im2colKM {
 #pragma unroll
         for (int j = 0; j < UNITS; ++j)
             store_km_or_spare<ROWS>(lds, C4 % TPR == 0 || c4[j] < C4, krow, c4[j], r[j]);
+    }
+    // f(k row, column chunk, value, valid) for each staged unit (split-bf16 plane stores; a
+    // surplus unit has valid = false and goes to the plane's spare slot)
+    template <class F>
+    __device__ void each_unit(const f32x4 (&r)[UNITS], F&& f) const {
+#pragma unroll
+        for (int j = 0; j < UNITS; ++j) f(krow, c4[j], r[j], C4 % TPR == 0 || c4[j] < C4);
     }
 };
 

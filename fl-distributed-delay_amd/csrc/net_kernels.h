@@ -610,7 +610,7 @@ static int fin_sum(const float* slab, int Z, long n, float* out, hipStream_t st,
 // =============================================================================================
 // GEMM launch helpers
 // =============================================================================================
-// X6: the split-bf16 kernel (gemm_x6.h, k-contiguous operands only) instead of the fp32 one
+// X6: the split-bf16 kernel (gemm_x6.h) instead of the fp32 one
 template <int FM, int FN, int WM, int WN, bool X6 = false, class AL, class BL, class EPI>
 static int launch_gemm(const AL& al, const BL& bl, const EPI& epi, int M, int N, int ksteps, int Z,
                        hipStream_t st, int kid, double alg_flops) {
@@ -620,7 +620,7 @@ static int launch_gemm(const AL& al, const BL& bl, const EPI& epi, int M, int N,
     dim3 grid(tm * tn * Z);
     const ProbeSlot ps = probe_begin();
     if constexpr (X6)
-        hipExtLaunchKernelGGL((gemm_x6_kernel<FM, FN, WM, WN, AL, BL, EPI, 2>), grid,
+        hipExtLaunchKernelGGL((gemm_x6_kernel<FM, FN, WM, WN, AL, BL, EPI>), grid,
                               dim3(64 * WM * WN), 0, st, ps.start, ps.stop, 0, al, bl, epi, ksteps,
                               per, tm, tn);
     else
@@ -810,7 +810,7 @@ static int conv_like_sz(const float* X, int S, const float* Wpk, int N, int KP, 
 // DZC: dz is already stored compact over that window ([S][VO][VO][CO]), so its rows are the
 // reduction index as they stand
 template <int IH, int IW, int CI, int PAD, int FM, int FN, int WM, int WN, int VO = 0,
-          bool DZC = false>
+          bool DZC = false, bool X6 = false>
 static int conv_wgrad(const float* dz, const float* X, int S, int CO, int KP, float* slab,
                       float* bslab, int Z, hipStream_t st, int kid, int kreal,
                       int zinit = 0x7fffffff, int* zused = nullptr) {
@@ -831,27 +831,28 @@ static int conv_wgrad(const float* dz, const float* X, int S, int CO, int KP, fl
     bl.M = M;
     EpiSlabAcc epi{slab, CO, KP, (long)CO * KP, bslab, zinit};
     const int tiles = ceil_div(CO, BM) * ceil_div(KP, BN);
-    static const int cap =
-        resident_blocks((const void*)gemm_kernel<FM, FN, WM, WN, AL, BL, EpiSlabAcc>, NT);
+    static const int cap = resident_blocks(
+        X6 ? (const void*)gemm_x6_kernel<FM, FN, WM, WN, AL, BL, EpiSlabAcc>
+           : (const void*)gemm_kernel<FM, FN, WM, WN, AL, BL, EpiSlabAcc>, NT);
     const int zu = wsplit(ceil_div(M, GK), Z, tiles, cap);
     if (zused) *zused = zu;
-    return launch_gemm<FM, FN, WM, WN>(al, bl, epi, CO, KP, ceil_div(M, GK), zu, st, kid,
-                                       2.0 * M * CO * kreal);
+    return launch_gemm<FM, FN, WM, WN, X6>(al, bl, epi, CO, KP, ceil_div(M, GK), zu, st, kid,
+                                           2.0 * M * CO * kreal);
 }
 
 // conv_wgrad with a second tile for chunks of at most small_chunk_samples() samples
 // (profiles/r03f/lab_s640_wgrad.txt: at 640 samples 96x96 4-wave tiles beat the 128-worker
 // chunk's larger ones on conv3/5/6 by 3-10 %, 48x144 beats 48x48 on conv2 by 4 %)
 template <int IH, int IW, int CI, int PAD, int FM, int FN, int WM, int WN, int FMS, int FNS,
-          int WMS, int WNS, int VO = 0, bool DZC = false>
+          int WMS, int WNS, int VO = 0, bool DZC = false, bool X6 = false>
 static int conv_wgrad_sz(const float* dz, const float* X, int S, int CO, int KP, float* slab,
                          float* bslab, int Z, hipStream_t st, int kid, int kreal, int zinit,
                          int* zused) {
     if (S <= small_chunk_samples())
-        return conv_wgrad<IH, IW, CI, PAD, FMS, FNS, WMS, WNS, VO, DZC>(
+        return conv_wgrad<IH, IW, CI, PAD, FMS, FNS, WMS, WNS, VO, DZC, X6>(
             dz, X, S, CO, KP, slab, bslab, Z, st, kid, kreal, zinit, zused);
-    return conv_wgrad<IH, IW, CI, PAD, FM, FN, WM, WN, VO, DZC>(dz, X, S, CO, KP, slab, bslab, Z,
-                                                                st, kid, kreal, zinit, zused);
+    return conv_wgrad<IH, IW, CI, PAD, FM, FN, WM, WN, VO, DZC, X6>(
+        dz, X, S, CO, KP, slab, bslab, Z, st, kid, kreal, zinit, zused);
 }
 
 // forward conv fused with bias + ReLU + 2x2 max-pool (+ dropout: keep iff philox >= thr, kept
@@ -880,7 +881,7 @@ static int conv_pool_fwd(const float* X, int S, const float* Wpk, int KP, float*
 }
 
 // linear layer part[z] = x W^T over the z-th K range (x [M][K] rows, W [N][K] torch layout)
-template <int FM, int FN, int WM, int WN>
+template <int FM, int FN, int WM, int WN, bool X6 = false>
 static int linear_fwd(const float* x, const float* W, float* part, int M, int N, int K, int Z,
                       hipStream_t st, int kid) {
     constexpr int NT = 64 * WM * WN;
@@ -889,11 +890,11 @@ static int linear_fwd(const float* x, const float* W, float* part, int M, int N,
     RowsKC<16 * FN * WN, NT> bl{};
     bl.P = W; bl.ld = K; bl.NR = N;
     EpiSlabStore epi{part, M, N, (long)M * N};
-    return launch_gemm<FM, FN, WM, WN>(al, bl, epi, M, N, K / GK, Z, st, kid, 2.0 * M * N * K);
+    return launch_gemm<FM, FN, WM, WN, X6>(al, bl, epi, M, N, K / GK, Z, st, kid, 2.0 * M * N * K);
 }
 
 // linear weight gradient: slab[z][n][k] += sum_s dy[s][n] x[s][k]; bias slab[z][n] += sum_s dy
-template <int FM, int FN, int WM, int WN>
+template <int FM, int FN, int WM, int WN, bool X6 = false>
 static int linear_wgrad(const float* dy, const float* x, float* slab, float* bslab, int S, int N,
                         int K, int Z, hipStream_t st, int kid, int zinit = 0x7fffffff,
                         int* zused = nullptr) {
@@ -906,13 +907,13 @@ static int linear_wgrad(const float* dy, const float* x, float* slab, float* bsl
     const int tiles = ceil_div(N, 16 * FM * WM) * ceil_div(K, 16 * FN * WN);
     const int zu = wsplit(ceil_div(S, GK), Z, tiles);
     if (zused) *zused = zu;
-    return launch_gemm<FM, FN, WM, WN>(al, bl, epi, N, K, ceil_div(S, GK), zu, st, kid,
-                                       2.0 * S * N * K);
+    return launch_gemm<FM, FN, WM, WN, X6>(al, bl, epi, N, K, ceil_div(S, GK), zu, st, kid,
+                                           2.0 * S * N * K);
 }
 
 // linear data gradient through the producer's dropout / ReLU:
 // dx[s][k] = (sum_n dy[s][n] W[n][k]) * scale * (act[s][k] > 0)
-template <int FM, int FN, int WM, int WN>
+template <int FM, int FN, int WM, int WN, bool X6 = false>
 static int linear_dgrad(const float* dy, const float* W, float* dx, const float* act, float scale,
                         int S, int N, int K, hipStream_t st, int kid) {
     constexpr int NT = 64 * WM * WN;
@@ -921,7 +922,8 @@ static int linear_dgrad(const float* dy, const float* W, float* dx, const float*
     RowsKM<16 * FN * WN, NT> wl{};
     wl.P = W; wl.ld = K; wl.NK = N; wl.NC = K;
     EpiDropMaskPre de{{dx, act, scale, S, K}};
-    return launch_gemm<FM, FN, WM, WN>(dl, wl, de, S, K, N / GK, 1, st, kid, 2.0 * S * N * K);
+    return launch_gemm<FM, FN, WM, WN, X6>(dl, wl, de, S, K, N / GK, 1, st, kid,
+                                           2.0 * S * N * K);
 }
 
 }  // namespace flsim

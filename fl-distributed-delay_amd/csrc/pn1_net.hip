@@ -287,7 +287,7 @@ static int forward(const GradState& g, const WS& w, const float* theta, int S,
     RC(conv1_fwd(w.x0, theta + P_OFF[0], theta + P_OFF[1], w.a1, S, st));
     // conv2 + ReLU + pool1 + dropout1 (models.py:30-32), one fused launch
     // (gemm_kernel: the direct-A form measured 7.51 vs 7.30 ms with this epilogue, r03b)
-    RC((conv_pool_fwd<34, 34, 48, 48, 2, 2, 3, 4, 1, false>(w.a1, S, g.wf[1], 432, w.d1, w.i1,
+    RC((conv_pool_fwd<34, 34, 48, 48, 2, 4, 3, 8, 1, false, true>(w.a1, S, g.wf[1], 432, w.d1, w.i1,
         theta + P_OFF[3], workers, seed, SITE_DROP1, THR_P25, SCALE_P25, dropout, st, K_FWD2,
         432)));
     RC((conv_x6<18, 18, 48, 2, 4, 3, 4, 2>(w.d1, S, g.wf[2], 96, 432,
@@ -307,12 +307,17 @@ static int forward(const GradState& g, const WS& w, const float* theta, int S,
     // linear1 + relu + dropout2 (models.py:41-43), split-K partials then finish
     // small chunks (configs[1]: 640 samples = 5 x 4 tiles of 128 x 128, 80 blocks with the split)
     // take 64 x 64 tiles: the same split, hence the same sums, with 4x the blocks
+    // (every tile on the split-bf16 kernel: a chunk's losses must not depend on its size, and
+    // the two kernels round differently)
     if (S <= 2048)          // 32 x 64 tiles: 640 blocks at configs[1]'s 640 samples
-        RC((linear_fwd<1, 2, 2, 2>(w.d3, theta + P_OFF[12], w.part, S, 512, 9408, ZL1F, st, K_L1F)));
+        RC((linear_fwd<1, 2, 2, 2, true>(w.d3, theta + P_OFF[12], w.part, S, 512, 9408, ZL1F, st,
+                                         K_L1F)));
     else if (S <= 4096)
-        RC((linear_fwd<2, 2, 2, 2>(w.d3, theta + P_OFF[12], w.part, S, 512, 9408, ZL1F, st, K_L1F)));
+        RC((linear_fwd<2, 2, 2, 2, true>(w.d3, theta + P_OFF[12], w.part, S, 512, 9408, ZL1F, st,
+                                         K_L1F)));
     else
-        RC((linear_fwd<4, 4, 2, 2>(w.d3, theta + P_OFF[12], w.part, S, 512, 9408, ZL1F, st, K_L1F)));
+        RC((linear_fwd<4, 4, 2, 2, true>(w.d3, theta + P_OFF[12], w.part, S, 512, 9408, ZL1F, st,
+                                         K_L1F)));
     RC(linear_finish(w.part, ZL1F, theta + P_OFF[13], w.e1, S, 512, workers, seed, SITE_DROP4,
                      THR_P50, SCALE_P50, dropout, st));
     // linear2 + relu + dropout2 (models.py:44-45)
@@ -478,14 +483,14 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
                                  K_L2D)));
     // ---- linear1: wgrad, bias, dgrad (-> gradient wrt d3 through dropout1 site 3) ----
     RC(fork());
-    RC((linear_wgrad<4, 4, 2, 2>(w.dh1, w.d3, g.l1w, g.l1b, S, 512, 9408, ZL1W, sw, K_L1W, zi(6),
-                                 &zu[6])));
+    RC((linear_wgrad<4, 4, 2, 2, true>(w.dh1, w.d3, g.l1w, g.l1b, S, 512, 9408, ZL1W, sw, K_L1W,
+                                       zi(6), &zu[6])));
     if (S <= 2048)          // 64 x 128 tiles: twice the blocks of 128 x 128 on a small chunk
-        RC((linear_dgrad<2, 4, 2, 2>(w.dh1, theta + P_OFF[12], w.gy, w.d3, s25, S, 512, 9408, st,
-                                     K_L1D)));
+        RC((linear_dgrad<2, 4, 2, 2, true>(w.dh1, theta + P_OFF[12], w.gy, w.d3, s25, S, 512,
+                                           9408, st, K_L1D)));
     else
-        RC((linear_dgrad<4, 4, 2, 2>(w.dh1, theta + P_OFF[12], w.gy, w.d3, s25, S, 512, 9408, st,
-                                     K_L1D)));
+        RC((linear_dgrad<4, 4, 2, 2, true>(w.dh1, theta + P_OFF[12], w.gy, w.d3, s25, S, 512,
+                                           9408, st, K_L1D)));
     // ---- pool3 backward -> dz6 (a6 buffer: conv6 fwd no longer writes it) ----
     // Row/column 14 of conv6's 15x15 output is never pooled (floor mode), so its dz is zero: dz6
     // is stored compact as [S][14][14][192].  The weight gradient then runs over those rows as
@@ -494,7 +499,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     float* dz6 = w.a6;
     // ---- conv6: wgrad (input a5), bias, dgrad -> dz5 = . * (a5 > 0) into gx ----
     RC(fork());
-    RC((conv_wgrad_sz<13, 13, 192, 2, 6, 3, 2, 4, 3, 3, 2, 2, 14, true>(
+    RC((conv_wgrad_sz<13, 13, 192, 2, 6, 3, 2, 2, 3, 3, 2, 2, 14, true, true>(
         dz6, w.a5, S, 192, 1728, g.sw[5], g.sb[5], GEO[5].ZW, sw, K_WG6, 1728, zi(5), &zu[5])));
     RC((conv_x6<14, 14, 192, 0, 4, 6, 4, 2, 13>(dz6, S, g.wd[5], 192, 1728,
         EpiMask<true>{w.gx, w.a5, S * 13 * 13, 192}, st, K_DG6, 1728)));
@@ -502,7 +507,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     // ---- conv5: wgrad (input d2), bias, dgrad -> grad wrt d2 (dropout site 2), scattered through
     //      pool2 straight into dz4 (a4 buffer; EpiDropScatterRows, no gy round trip) ----
     RC(fork());
-    RC((conv_wgrad_sz<11, 11, 96, 2, 6, 3, 2, 2, 3, 3, 2, 2>(
+    RC((conv_wgrad_sz<11, 11, 96, 2, 6, 3, 2, 2, 3, 3, 2, 2, 0, false, true>(
         dz5, w.d2, S, 192, 864, g.sw[4], g.sb[4], GEO[4].ZW, sw, K_WG5, 864, zi(4), &zu[4])));
     RC((conv_x6<13, 13, 192, 0, 4, 3, 4, 2>(dz5, S, g.wd[4], 96, 1728,
         EpiDropScatterRows<11, 11, 96, 0>{w.a4, w.d2, w.i2, s25, S * 11 * 11}, st, K_DG5, 1728)));
@@ -510,7 +515,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     // ---- conv4: wgrad (input a3), bias, dgrad -> dz3 = . * (a3 > 0) into gx ----
     RC(join());                                   // conv5's wgrad reads gx = dz5: done first
     RC(fork());
-    RC((conv_wgrad<20, 20, 96, 2, 3, 3, 2, 2>(
+    RC((conv_wgrad<20, 20, 96, 2, 3, 3, 2, 2, 0, false, true>(
         dz4, w.a3, S, 96, 864, g.sw[3], g.sb[3], GEO[3].ZW, sw, K_WG4, 864, zi(3), &zu[3])));
     RC((conv_x6<22, 22, 96, 0, 4, 3, 4, 2>(dz4, S, g.wd[3], 96, 864,
         EpiMask<true>{w.gx, w.a3, S * 20 * 20, 96}, st, K_DG4, 864)));
@@ -518,7 +523,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     // ---- conv3: wgrad (input d1), bias, dgrad -> grad wrt d1 (site 1), scattered through pool1
     //      straight into dz2 (a2 buffer) ----
     RC(fork());
-    RC((conv_wgrad_sz<18, 18, 48, 2, 3, 3, 2, 1, 3, 3, 2, 2>(
+    RC((conv_wgrad_sz<18, 18, 48, 2, 3, 3, 2, 1, 3, 3, 2, 2, 0, false, true>(
         dz3, w.d1, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW, sw, K_WG3, 432, zi(2), &zu[2])));
     // (gemm_kernel: the direct-A form measured 3.87 vs 3.78 ms with this staged epilogue, r03b,
     // and 3.97 vs 3.77 with the batched epilogue loads, profiles/r03t/r03q_dg3)
@@ -528,7 +533,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     // ---- conv2: wgrad (input a1), bias, dgrad -> dz1 = . * (a1 > 0) into gx ----
     RC(join());                                   // conv3's wgrad reads gx = dz3: done first
     RC(fork());
-    RC((conv_wgrad_sz<34, 34, 48, 2, 3, 3, 1, 1, 3, 3, 1, 3>(
+    RC((conv_wgrad_sz<34, 34, 48, 2, 3, 3, 1, 3, 3, 3, 1, 3, 0, false, true>(
         dz2, w.a1, S, 48, 432, g.sw[1], g.sb[1], GEO[1].ZW, sw, K_WG2, 432, zi(1), &zu[1])));
     RC((conv_direct_sz<36, 36, 48, 0, 2, 1, 3, 8, 3, 2, false, 0>(dz2, S, g.wd[1], 48, 432,
         EpiMaskRows<48>{w.gx, w.a1, S * 34 * 34}, st, K_DG2, 432)));

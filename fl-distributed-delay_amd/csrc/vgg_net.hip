@@ -244,7 +244,7 @@ static int vbn_conv(const VBN& bn, int l, const float* X, int S, const VGrad& g,
                     uint64_t seed, uint32_t site, int dropout, hipStream_t st, int kid,
                     int kreal) {
     const VWS& w = *bn.w;
-    RC((conv_like<H, H, CIP, 1, FM, FN, WM, WN>(X, S, g.wf[l], CO, VG[l].KP,
+    RC((conv_x6<H, H, CIP, 1, FM, FN, WM, WN>(X, S, g.wf[l], CO, VG[l].KP,
         EpiBias{w.z[l], th + o.b[l], S * H * H, CO}, st, kid, kreal)));
     if (bn.train)
         RC((bn_forward_stats<H, CO>(w.z[l], S, w.bmean[l], w.binv[l], w.pa, w.pb, bn.stats,
@@ -297,38 +297,38 @@ static int vforward(const VGrad& g, const VWS& w, const float* th, const VOff& o
                                                     K_VF8, 4608)));
     } else {
         // conv1 + ReLU + pool (features.0-2)
-        RC((conv_pool_fwd<32, 32, 4, 64, 1, 2, 4, 4, 1, false>(w.x0, S, g.wf[0], 48, w.d1, w.i1,
+        RC((conv_pool_fwd<32, 32, 4, 64, 1, 2, 4, 4, 1, false, true>(w.x0, S, g.wf[0], 48, w.d1, w.i1,
             th + o.b[0], workers, seed, 0, 0, 1.f, 0, st, K_VF1, 27)));
         // conv2 + ReLU + pool (features.3-5)
-        RC((conv_pool_fwd<16, 16, 64, 128, 1, 4, 4, 4, 2, false>(w.d1, S, g.wf[1], 576, w.d2,
+        RC((conv_pool_fwd<16, 16, 64, 128, 1, 4, 4, 4, 2, false, true>(w.d1, S, g.wf[1], 576, w.d2,
             w.i2, th + o.b[1], workers, seed, 0, 0, 1.f, 0, st, K_VF2, 576)));
         // conv3 + ReLU (features.6-7)
-        RC((conv_like<8, 8, 128, 1, 4, 4, 4, 2>(w.d2, S, g.wf[2], 256, 1152,
+        RC((conv_x6<8, 8, 128, 1, 4, 4, 4, 2>(w.d2, S, g.wf[2], 256, 1152,
             EpiBiasRelu{w.a3, th + o.b[2], S * 64, 256}, st, K_VF3, 1152)));
         // conv4 + ReLU + pool (features.8-10)
-        RC((conv_pool_fwd<8, 8, 256, 256, 1, 4, 4, 4, 2, false>(w.a3, S, g.wf[3], 2304, w.d4,
+        RC((conv_pool_fwd<8, 8, 256, 256, 1, 4, 4, 4, 2, false, true>(w.a3, S, g.wf[3], 2304, w.d4,
             w.i4, th + o.b[3], workers, seed, 0, 0, 1.f, 0, st, K_VF4, 2304)));
         // conv5 + ReLU (features.11-12)
-        RC((conv_like<4, 4, 256, 1, 4, 4, 4, 2>(w.d4, S, g.wf[4], 512, 2304,
+        RC((conv_x6<4, 4, 256, 1, 4, 4, 4, 2>(w.d4, S, g.wf[4], 512, 2304,
             EpiBiasRelu{w.a5, th + o.b[4], S * 16, 512}, st, K_VF5, 2304)));
         // conv6 + ReLU + pool (features.13-15)
-        RC((conv_pool_fwd<4, 4, 512, 512, 1, 4, 4, 4, 2, false>(w.a5, S, g.wf[5], 4608, w.d6,
+        RC((conv_pool_fwd<4, 4, 512, 512, 1, 4, 4, 4, 2, false, true>(w.a5, S, g.wf[5], 4608, w.d6,
             w.i6, th + o.b[5], workers, seed, 0, 0, 1.f, 0, st, K_VF6, 4608)));
         // conv7 + ReLU (features.16-17)
-        RC((conv_like<2, 2, 512, 1, 4, 4, 4, 2>(w.d6, S, g.wf[6], 512, 4608,
+        RC((conv_x6<2, 2, 512, 1, 4, 4, 4, 2>(w.d6, S, g.wf[6], 512, 4608,
             EpiBiasRelu{w.a7, th + o.b[6], S * 4, 512}, st, K_VF7, 4608)));
         // conv8 + ReLU + pool (features.18-20) + classifier Dropout (models.py:58): the 1x1
         // pooled map is the flattened feature vector
-        RC((conv_pool_fwd<2, 2, 512, 512, 1, 4, 4, 4, 2, false>(w.a7, S, g.wf[7], 4608, w.f0,
+        RC((conv_pool_fwd<2, 2, 512, 512, 1, 4, 4, 4, 2, false, true>(w.a7, S, g.wf[7], 4608, w.f0,
             w.i8, th + o.b[7], workers, seed, SITE_VDROP1, THR_P50, SCALE_P50, dropout, st,
             K_VF8, 4608)));
     }
     // Linear + ReLU + Dropout (models.py:59-61)
-    RC((linear_fwd<4, 4, 2, 2>(w.f0, th + o.l1w, w.part, S, VFEAT, VFEAT, 1, st, K_VL1F)));
+    RC((linear_fwd<4, 4, 2, 2, true>(w.f0, th + o.l1w, w.part, S, VFEAT, VFEAT, 1, st, K_VL1F)));
     RC(linear_finish(w.part, 1, th + o.l1b, w.e1, S, VFEAT, workers, seed, SITE_VDROP2, THR_P50,
                      SCALE_P50, dropout, st));
     // Linear + ReLU (models.py:62-63)
-    RC((linear_fwd<4, 4, 2, 2>(w.e1, th + o.l2w, w.part, S, VFEAT, VFEAT, 1, st, K_VL2F)));
+    RC((linear_fwd<4, 4, 2, 2, true>(w.e1, th + o.l2w, w.part, S, VFEAT, VFEAT, 1, st, K_VL2F)));
     RC(linear_finish(w.part, 1, th + o.l2b, w.e2, S, VFEAT, workers, seed, 0, 0, 1.f, 0, st));
     return 0;
 }
@@ -351,64 +351,64 @@ static int vbackward(const VGrad& g, const VWS& w, const float* th, const VOff& 
     // Linear(512,10) weight / bias
     RC(head_wgrad<VFEAT>(w.dlog, w.e2, g.l3w, g.l3b, S, VZH, st));
     // Linear2: wgrad (input e1), dgrad through Dropout + ReLU of Linear1 (e1 is the dropped output)
-    RC((linear_wgrad<4, 4, 2, 2>(w.dh2, w.e1, g.l2w, g.l2b, S, VFEAT, VFEAT, VZL, st, K_VL2W)));
-    RC((linear_dgrad<4, 4, 2, 2>(w.dh2, th + o.l2w, w.dh1, w.e1, s50, S, VFEAT, VFEAT, st,
+    RC((linear_wgrad<4, 4, 2, 2, true>(w.dh2, w.e1, g.l2w, g.l2b, S, VFEAT, VFEAT, VZL, st, K_VL2W)));
+    RC((linear_dgrad<4, 4, 2, 2, true>(w.dh2, th + o.l2w, w.dh1, w.e1, s50, S, VFEAT, VFEAT, st,
                                  K_VL2D)));
     // Linear1: wgrad (input f0 = dropped features), dgrad through the first Dropout and conv8's
     // pooled ReLU (f0 > 0), then the pool scatter -> dz8
-    RC((linear_wgrad<4, 4, 2, 2>(w.dh1, w.f0, g.l1w, g.l1b, S, VFEAT, VFEAT, VZL, st, K_VL1W)));
-    RC((linear_dgrad<4, 4, 2, 2>(w.dh1, th + o.l1w, w.gy, w.f0, s50, S, VFEAT, VFEAT, st,
+    RC((linear_wgrad<4, 4, 2, 2, true>(w.dh1, w.f0, g.l1w, g.l1b, S, VFEAT, VFEAT, VZL, st, K_VL1W)));
+    RC((linear_dgrad<4, 4, 2, 2, true>(w.dh1, th + o.l1w, w.gy, w.f0, s50, S, VFEAT, VFEAT, st,
                                  K_VL1D)));
     RC((pool_scatter<2, 2, 512, false>(w.gy, w.i8, w.ga, S, st)));
     RC((vbn_back<BN, 2, 512>(g, w, th, o, 7, w.ga, S, st)));
     // conv8: wgrad (input a7), dgrad -> dz7 = . * (a7 > 0)
-    RC((conv_wgrad<2, 2, 512, 1, 4, 4, 4, 2>(w.ga, w.a7, S, 512, 4608, g.sw[7], g.sb[7], VG[7].ZW,
+    RC((conv_wgrad<2, 2, 512, 1, 4, 4, 4, 2, 0, false, true>(w.ga, w.a7, S, 512, 4608, g.sw[7], g.sb[7], VG[7].ZW,
                                             st, K_VWG8, 4608)));
-    RC((conv_like<2, 2, 512, 1, 4, 4, 4, 2>(w.ga, S, g.wd[7], 512, 4608,
+    RC((conv_x6<2, 2, 512, 1, 4, 4, 4, 2>(w.ga, S, g.wd[7], 512, 4608,
         EpiMask<true>{w.gb, w.a7, S * 4, 512}, st, K_VDG8, 4608)));
     RC((vbn_back<BN, 2, 512>(g, w, th, o, 6, w.gb, S, st)));
     // conv7: wgrad (input d6), dgrad -> gradient wrt d6 (d6 > 0), pool scatter -> dz6
-    RC((conv_wgrad<2, 2, 512, 1, 4, 4, 4, 2>(w.gb, w.d6, S, 512, 4608, g.sw[6], g.sb[6], VG[6].ZW,
+    RC((conv_wgrad<2, 2, 512, 1, 4, 4, 4, 2, 0, false, true>(w.gb, w.d6, S, 512, 4608, g.sw[6], g.sb[6], VG[6].ZW,
                                             st, K_VWG7, 4608)));
-    RC((conv_like<2, 2, 512, 1, 4, 4, 4, 2>(w.gb, S, g.wd[6], 512, 4608,
+    RC((conv_x6<2, 2, 512, 1, 4, 4, 4, 2>(w.gb, S, g.wd[6], 512, 4608,
         EpiDropMask{w.gy, w.d6, 1.f, S * 4, 512}, st, K_VDG7, 4608)));
     RC((pool_scatter<4, 4, 512, false>(w.gy, w.i6, w.ga, S, st)));
     RC((vbn_back<BN, 4, 512>(g, w, th, o, 5, w.ga, S, st)));
     // conv6: wgrad (input a5), dgrad -> dz5 = . * (a5 > 0)
-    RC((conv_wgrad<4, 4, 512, 1, 4, 4, 4, 2>(w.ga, w.a5, S, 512, 4608, g.sw[5], g.sb[5], VG[5].ZW,
+    RC((conv_wgrad<4, 4, 512, 1, 4, 4, 4, 2, 0, false, true>(w.ga, w.a5, S, 512, 4608, g.sw[5], g.sb[5], VG[5].ZW,
                                             st, K_VWG6, 4608)));
-    RC((conv_like<4, 4, 512, 1, 4, 4, 4, 2>(w.ga, S, g.wd[5], 512, 4608,
+    RC((conv_x6<4, 4, 512, 1, 4, 4, 4, 2>(w.ga, S, g.wd[5], 512, 4608,
         EpiMask<true>{w.gb, w.a5, S * 16, 512}, st, K_VDG6, 4608)));
     RC((vbn_back<BN, 4, 512>(g, w, th, o, 4, w.gb, S, st)));
     // conv5: wgrad (input d4), dgrad -> gradient wrt d4, pool scatter -> dz4
-    RC((conv_wgrad<4, 4, 256, 1, 4, 4, 2, 2>(w.gb, w.d4, S, 512, 2304, g.sw[4], g.sb[4], VG[4].ZW,
+    RC((conv_wgrad<4, 4, 256, 1, 4, 4, 2, 2, 0, false, true>(w.gb, w.d4, S, 512, 2304, g.sw[4], g.sb[4], VG[4].ZW,
                                             st, K_VWG5, 2304)));
-    RC((conv_like<4, 4, 512, 1, 4, 4, 4, 2>(w.gb, S, g.wd[4], 256, 4608,
+    RC((conv_x6<4, 4, 512, 1, 4, 4, 4, 2>(w.gb, S, g.wd[4], 256, 4608,
         EpiDropMask{w.gy, w.d4, 1.f, S * 16, 256}, st, K_VDG5, 4608)));
     RC((pool_scatter<8, 8, 256, false>(w.gy, w.i4, w.ga, S, st)));
     RC((vbn_back<BN, 8, 256>(g, w, th, o, 3, w.ga, S, st)));
     // conv4: wgrad (input a3), dgrad -> dz3 = . * (a3 > 0)
-    RC((conv_wgrad<8, 8, 256, 1, 4, 4, 2, 2>(w.ga, w.a3, S, 256, 2304, g.sw[3], g.sb[3], VG[3].ZW,
+    RC((conv_wgrad<8, 8, 256, 1, 4, 4, 2, 2, 0, false, true>(w.ga, w.a3, S, 256, 2304, g.sw[3], g.sb[3], VG[3].ZW,
                                             st, K_VWG4, 2304)));
-    RC((conv_like<8, 8, 256, 1, 4, 4, 4, 2>(w.ga, S, g.wd[3], 256, 2304,
+    RC((conv_x6<8, 8, 256, 1, 4, 4, 4, 2>(w.ga, S, g.wd[3], 256, 2304,
         EpiMask<true>{w.gb, w.a3, S * 64, 256}, st, K_VDG4, 2304)));
     RC((vbn_back<BN, 8, 256>(g, w, th, o, 2, w.gb, S, st)));
     // conv3: wgrad (input d2), dgrad -> gradient wrt d2, pool scatter -> dz2
-    RC((conv_wgrad<8, 8, 128, 1, 4, 4, 2, 2>(w.gb, w.d2, S, 256, 1152, g.sw[2], g.sb[2], VG[2].ZW,
+    RC((conv_wgrad<8, 8, 128, 1, 4, 4, 2, 2, 0, false, true>(w.gb, w.d2, S, 256, 1152, g.sw[2], g.sb[2], VG[2].ZW,
                                             st, K_VWG3, 1152)));
-    RC((conv_like<8, 8, 256, 1, 4, 4, 4, 2>(w.gb, S, g.wd[2], 128, 2304,
+    RC((conv_x6<8, 8, 256, 1, 4, 4, 4, 2>(w.gb, S, g.wd[2], 128, 2304,
         EpiDropMask{w.gy, w.d2, 1.f, S * 64, 128}, st, K_VDG3, 2304)));
     RC((pool_scatter<16, 16, 128, false>(w.gy, w.i2, w.ga, S, st)));
     RC((vbn_back<BN, 16, 128>(g, w, th, o, 1, w.ga, S, st)));
     // conv2: wgrad (input d1), dgrad -> gradient wrt d1, pool scatter -> dz1
-    RC((conv_wgrad<16, 16, 64, 1, 2, 4, 4, 2>(w.ga, w.d1, S, 128, 576, g.sw[1], g.sb[1], VG[1].ZW,
+    RC((conv_wgrad<16, 16, 64, 1, 2, 4, 4, 2, 0, false, true>(w.ga, w.d1, S, 128, 576, g.sw[1], g.sb[1], VG[1].ZW,
                                              st, K_VWG2, 576)));
-    RC((conv_like<16, 16, 128, 1, 2, 4, 4, 1>(w.ga, S, g.wd[1], 64, 1152,
+    RC((conv_x6<16, 16, 128, 1, 2, 4, 4, 1>(w.ga, S, g.wd[1], 64, 1152,
         EpiDropMask{w.gy, w.d1, 1.f, S * 256, 64}, st, K_VDG2, 1152)));
     RC((pool_scatter<32, 32, 64, false>(w.gy, w.i1, w.ga, S, st)));
     RC((vbn_back<BN, 32, 64>(g, w, th, o, 0, w.ga, S, st)));
     // conv1: wgrad (input x0)
-    RC((conv_wgrad<32, 32, 4, 1, 4, 3, 1, 1>(w.ga, w.x0, S, 64, 48, g.sw[0], g.sb[0], VG[0].ZW, st,
+    RC((conv_wgrad<32, 32, 4, 1, 4, 3, 1, 1, 0, false, true>(w.ga, w.x0, S, 64, 48, g.sw[0], g.sb[0], VG[0].ZW, st,
                                             K_VWG1, 27)));
     return 0;
 }
