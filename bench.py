@@ -32,6 +32,12 @@ import torch  # noqa: E402
 
 METRIC = "simulated worker-steps/sec (node) @1024 workers, delay 50; aggregation HBM GB/s"
 MFMA_F32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: fp32 matrix (v_mfma_f32_16x16x4_f32)
+# the split-bf16 GEMMs (gemm_x6.h) issue six bf16 products per fp32 product on the bf16 matrix
+# cores (~2.5 PF/s dense, MI355X_MICROARCH.md): their fp32-equivalent peak
+MFMA_X6_PEAK_TFLOPS = 2500.0 / 6
+# probe names of the GEMMs that run on gemm_x6_kernel (pn1_net.hip, vgg_net.hip)
+X6_KERNELS = {f"conv{i}_{p}" for i in range(2, 7) for p in ("fwd", "wgrad")} | \
+    {f"conv{i}_dgrad" for i in range(3, 7)} | {"linear1_fwd", "linear1_dgrad", "linear1_wgrad"}
 HBM_PEAK_GBPS = 8000.0           # MI355X_MICROARCH.md: HBM3E spec
 
 
@@ -318,9 +324,13 @@ def main():
         gemm_ms = sum(v[1] for v in kern.values())
         gemm_fl = sum(v[2] for v in kern.values())
         traffic = TRAFFIC.get(name) if args.model == "PerformantNet1" else None
+        x6 = name in X6_KERNELS or name.startswith("vgg")
+        peak = MFMA_X6_PEAK_TFLOPS if x6 else MFMA_F32_PEAK_TFLOPS
         roofline = dict(bound="mfma", kernel=name, achieved=round(achieved, 2),
-                        peak=MFMA_F32_PEAK_TFLOPS, unit="TFLOP/s",
-                        frac=round(achieved / MFMA_F32_PEAK_TFLOPS, 4),
+                        peak=round(peak, 1), unit="TFLOP/s",
+                        frac=round(achieved / peak, 4),
+                        math=("bf16x6 split on the bf16 MFMA (fp32-equivalent FLOP/s against "
+                              "2.5 PF/s / 6)" if x6 else "fp32 MFMA"),
                         traffic=traffic["bytes_per_launch"] if traffic else None,
                         traffic_source=traffic["source"] if traffic else None,
                         launches=cnt, avg_launch_ms=round(ms / cnt, 4),
