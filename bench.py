@@ -37,7 +37,7 @@ MFMA_F32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: fp32 matrix (v_mfma_f32_
 MFMA_X6_PEAK_TFLOPS = 2500.0 / 6
 # probe names of the GEMMs that run on gemm_x6_kernel (pn1_net.hip, vgg_net.hip)
 X6_KERNELS = {f"conv{i}_{p}" for i in range(2, 7) for p in ("fwd", "wgrad")} | \
-    {f"conv{i}_dgrad" for i in range(3, 7)} | {"linear1_fwd", "linear1_dgrad", "linear1_wgrad"}
+    {"conv5_dgrad", "conv6_dgrad", "linear1_fwd", "linear1_wgrad"}
 HBM_PEAK_GBPS = 8000.0           # MI355X_MICROARCH.md: HBM3E spec
 
 
@@ -426,8 +426,9 @@ def main():
             # fp32 in, fp32 accumulate; the k-contiguous convolution GEMMs split each fp32 operand
             # into three bf16 parts and sum six exact partial products on the bf16 matrix cores
             # (gemm_x6.h): fp32 accuracy, not a reduced-precision mode
-            "math": "fp32 MFMA (weight gradients, linear layers, conv1, conv2); bf16x6 split of "
-                    "the fp32 operands, fp32 accumulate (conv3-6 forward + data gradient)",
+            "math": "bf16x6 split of the fp32 operands, fp32 accumulate (conv2-6 forward and "
+                    "weight gradients, conv5/6 data gradients, linear1 forward and weight "
+                    "gradient; all of VGG); fp32 MFMA for the rest",
             "data": f"synthetic: seeded CIFAR-shaped u8 pool in HBM, "
                     + (f"{args.model} warm-started from {os.path.basename(args.model_file)}"
                        if args.model_file else f"models.py-init {args.model}")

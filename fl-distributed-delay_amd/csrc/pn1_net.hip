@@ -485,12 +485,13 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC(fork());
     RC((linear_wgrad<4, 4, 2, 2, true>(w.dh1, w.d3, g.l1w, g.l1b, S, 512, 9408, ZL1W, sw, K_L1W,
                                        zi(6), &zu[6])));
+    // (fp32: on the split-bf16 kernel 1.32 vs 1.24 ms, profiles/r03z)
     if (S <= 2048)          // 64 x 128 tiles: twice the blocks of 128 x 128 on a small chunk
-        RC((linear_dgrad<2, 4, 2, 2, true>(w.dh1, theta + P_OFF[12], w.gy, w.d3, s25, S, 512,
-                                           9408, st, K_L1D)));
+        RC((linear_dgrad<2, 4, 2, 2>(w.dh1, theta + P_OFF[12], w.gy, w.d3, s25, S, 512, 9408, st,
+                                     K_L1D)));
     else
-        RC((linear_dgrad<4, 4, 2, 2, true>(w.dh1, theta + P_OFF[12], w.gy, w.d3, s25, S, 512,
-                                           9408, st, K_L1D)));
+        RC((linear_dgrad<4, 4, 2, 2>(w.dh1, theta + P_OFF[12], w.gy, w.d3, s25, S, 512, 9408, st,
+                                     K_L1D)));
     // ---- pool3 backward -> dz6 (a6 buffer: conv6 fwd no longer writes it) ----
     // Row/column 14 of conv6's 15x15 output is never pooled (floor mode), so its dz is zero: dz6
     // is stored compact as [S][14][14][192].  The weight gradient then runs over those rows as
@@ -517,7 +518,8 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC(fork());
     RC((conv_wgrad<20, 20, 96, 2, 3, 3, 2, 2, 0, false, true>(
         dz4, w.a3, S, 96, 864, g.sw[3], g.sb[3], GEO[3].ZW, sw, K_WG4, 864, zi(3), &zu[3])));
-    RC((conv_x6<22, 22, 96, 0, 4, 3, 4, 2>(dz4, S, g.wd[3], 96, 864,
+    // (fp32 direct kernel: the split-bf16 256x96 tile measured 8.21 vs 7.99 ms, profiles/r03z)
+    RC((conv_direct<22, 22, 96, 0, 2, 6, 8, 3, 2, false, 0>(dz4, S, g.wd[3], 96, 864,
         EpiMask<true>{w.gx, w.a3, S * 20 * 20, 96}, st, K_DG4, 864)));
     float* dz3 = w.gx;
     // ---- conv3: wgrad (input d1), bias, dgrad -> grad wrt d1 (site 1), scattered through pool1
@@ -526,8 +528,9 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC((conv_wgrad_sz<18, 18, 48, 2, 3, 3, 2, 1, 3, 3, 2, 2, 0, false, true>(
         dz3, w.d1, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW, sw, K_WG3, 432, zi(2), &zu[2])));
     // (gemm_kernel: the direct-A form measured 3.87 vs 3.78 ms with this staged epilogue, r03b,
-    // and 3.97 vs 3.77 with the batched epilogue loads, profiles/r03t/r03q_dg3)
-    RC((conv_x6<20, 20, 96, 0, 4, 3, 8, 1>(dz3, S, g.wd[2], 48, 864,
+    // 3.97 vs 3.77 with the batched epilogue loads, profiles/r03t/r03q_dg3; the split-bf16 512x48
+    // tile 3.82 vs 3.74, profiles/r03z)
+    RC((conv_like_sz<20, 20, 96, 0, 4, 2, 3, 4, 1>(dz3, S, g.wd[2], 48, 864,
         EpiDropScatterRows<18, 18, 48>{w.a2, w.d1, w.i1, s25, S * 18 * 18}, st, K_DG3, 864)));
     float* dz2 = w.a2;
     // ---- conv2: wgrad (input a1), bias, dgrad -> dz1 = . * (a1 > 0) into gx ----

@@ -114,6 +114,19 @@ __global__ void acc_kernel(const float* A, const float* B, float* C, int K) {
     } else if constexpr (MODE <= 3) {
         constexpr int T = MODE == 1 ? 3 : MODE == 2 ? 6 : 9;
         for (int ks = 0; ks < KS; ++ks) c = split_mac16<T>(split3(fa(ks)), split3(fb(ks)), c);
+    } else if constexpr (MODE >= 7) {
+        // the product's pairing (gemm_x6.h): per 16-deep k-step A [h|m], [h|l] x B [h|m], [m|h],
+        // [l|h]; MODE 8: the three MFMAs into a zero accumulator, added to c by a VALU add
+        for (int ks = 0; ks < KS; ++ks) {
+            const Parts a = split3(fa(ks)), b = split3(fb(ks));
+            const bf16x8 ahm = cat(a.h, a.m), ahl = cat(a.h, a.l);
+            const bf16x8 bhm = cat(b.h, b.m), bmh = cat(b.m, b.h), blh = cat(b.l, b.h);
+            f32x4 t = MODE == 8 ? f32x4{0.f, 0.f, 0.f, 0.f} : c;
+            t = mfma_bf16x32(ahl, blh, t);
+            t = mfma_bf16x32(ahm, bmh, t);
+            t = mfma_bf16x32(ahm, bhm, t);
+            c = MODE == 8 ? c + t : t;
+        }
     } else {
         constexpr int T = MODE == 4 ? 3 : MODE == 5 ? 6 : 9;
         for (int ks = 0; ks + 1 < KS; ks += 2)
@@ -233,7 +246,7 @@ static void run_acc(const char* name, const float* dA, const float* dB, float* d
     CK(hipDeviceSynchronize());
     std::vector<float> C(256);
     CK(hipMemcpy(C.data(), dC, 1024, hipMemcpyDeviceToHost));
-    double emax = 0, esum = 0;
+    double emax = 0, esum = 0, bias = 0, cabs = 0, rel2 = 0, ref2 = 0;
     for (int r = 0; r < 16; ++r)
         for (int c = 0; c < 16; ++c) {
             double ref = 0, mag = 0;
@@ -242,12 +255,18 @@ static void run_acc(const char* name, const float* dA, const float* dB, float* d
                 ref += p;
                 mag += fabs(p);
             }
-            const double e = fabs((double)C[r * 16 + c] - ref) / (mag > 0 ? mag : 1);
+            const double d = (double)C[r * 16 + c] - ref;
+            const double e = fabs(d) / (mag > 0 ? mag : 1);
             emax = e > emax ? e : emax;
             esum += e;
+            bias += d * (ref > 0 ? 1.0 : -1.0);   // < 0: errors lean toward zero (truncation)
+            cabs += fabs(ref);
+            rel2 += d * d;
+            ref2 += ref * ref;
         }
-    printf("acc %-12s K=%6d  max %.3e  mean %.3e  (x 2^-24: max %.2f mean %.2f)\n", name, K, emax,
-           esum / 256, emax * 16777216.0, esum / 256 * 16777216.0);
+    printf("acc %-12s K=%6d  max %.3e  mean %.3e  (x 2^-24: max %.2f mean %.2f)  rel-L2 %.3e  "
+           "signed bias / mean|C| %+.3e\n", name, K, emax, esum / 256, emax * 16777216.0,
+           esum / 256 * 16777216.0, sqrt(rel2 / ref2), bias / cabs);
 }
 
 template <int MODE, int FM, int FN>
@@ -303,11 +322,14 @@ int main() {
             run_acc<4>("bf16x3/x32", dA, dB, dC, K, A, B);
             run_acc<5>("bf16x6/x32", dA, dB, dC, K, A, B);
             run_acc<6>("bf16x9/x32", dA, dB, dC, K, A, B);
+            run_acc<7>("x6 product", dA, dB, dC, K, A, B);
+            run_acc<8>("x6 prod+add", dA, dB, dC, K, A, B);
             CK(hipFree(dA));
             CK(hipFree(dB));
             CK(hipFree(dC));
         }
     }
+    if (getenv("ACC_ONLY")) return 0;
     run_rate<0, 4, 4>("fp32");
     run_rate<7, 4, 4>("fp32 2 k-steps/stage");
     run_rate<2, 4, 4>("bf16x6 x16 split@read");
