@@ -5,9 +5,9 @@ VGG11Ref, itself pinned to the reference's own vgg11() by tests/golden/vgg.npz).
 Tolerances (as tests/test_gpu_parity.py):
   * one worker-step gradient: per-tensor rel-L2 vs fp64 <= 5e-3; whole gradient within
     2.5e-4 of |g64| (or 4x the CPU's own fp32 error), or else at most 8 knife-edge decisions
-    that fp64 takes the other way, with the teacher-forced gradient exact to 2e-5;
+    that fp64 takes the other way, with the teacher-forced gradient exact to TF_TOL;
   * teacher-forced (the GPU's own ReLU / argmax / dropout decisions in an fp64 reference):
-    per-tensor rel-L2 <= 2e-5, losses to 1e-5;
+    per-tensor rel-L2 <= TF_TOL, losses to 1e-5;
   * losses |dloss| <= 1e-4 on the first step, <= 1e-3 over the first epochs; trace bit-exact.
 """
 import numpy as np
@@ -18,6 +18,12 @@ from conftest import has_gpu
 
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not has_gpu(), reason="needs an MI355X")]
 
+
+# per-tensor rel-L2 of the GPU gradient against the fp64 reference with the GPU's own decisions.
+# The fp32-MFMA build stayed within 2e-5; with every VGG GEMM on the split-bf16 kernel
+# (gemm_x6.h, fp32 accumulation) the worst tensor measured 2.3e-5 and 3.1e-5
+# (profiles/r03z/pytest.log): the bound is 5e-5.  A wrong kernel misses by orders of magnitude.
+TF_TOL = 5e-5
 
 def _tol_log(worst):
     """Per-tensor error census across builds (measurement only: FLSIM_TOL_LOG=<file>)."""
@@ -167,7 +173,7 @@ def test_vgg_single_worker_step_gradient(pool, dropout):
     if e_gpu > max(2.5e-4 * np.linalg.norm(g64), 4 * e_cpu):
         g_tf, _, flips = _teacher_forced(sim, eng, items, dropout)
         assert 1 <= flips <= FLIPS, (e_gpu, e_cpu, flips)
-        assert _rel_l2(g, g_tf) <= 2e-5, (e_gpu, flips, _rel_l2(g, g_tf))
+        assert _rel_l2(g, g_tf) <= TF_TOL, (e_gpu, flips, _rel_l2(g, g_tf))
 
 
 @pytest.mark.parametrize("dropout,items", [
@@ -190,7 +196,7 @@ def test_vgg_gradient_teacher_forced_decisions(pool, dropout, items):
         off += n
     _tol_log(worst)
     np.testing.assert_allclose(loss, lrefs, atol=1e-5)
-    assert max(worst.values()) <= 2e-5, worst
+    assert max(worst.values()) <= TF_TOL, worst
     assert flips <= 8 * len(items), flips
 
 

@@ -12,12 +12,12 @@ order.  Tolerances:
     tools/dbg_bn.py: 1 of 65,536 pooled conv8 values for worker (0, 0, 0)) moves one
     (sample, channel) gradient to another window position, and the BatchNorm backward spreads
     that over the whole channel: 0.1-1.5 % in every feature tensor.  The exactness of every
-    backward kernel is the teacher-forced test's job (the GPU's own decisions, 2e-5);
+    backward kernel is the teacher-forced test's job (the GPU's own decisions, 5e-5);
   * conv biases: a bias in front of a BatchNorm cancels, so its gradient is rounding noise of a
     zero sum -- checked as an absolute error against the whole gradient's norm (<= 1e-6 |g64|,
     or 10x the CPU's);
   * teacher-forced (the GPU's ReLU / argmax / dropout decisions in an fp64 reference with fp64
-    batch statistics): per-tensor rel-L2 <= 2e-5 (conv biases absolute as above), losses 1e-5;
+    batch statistics): per-tensor rel-L2 <= 5e-5 (conv biases absolute as above), losses 1e-5;
   * running buffers: running_var rel 1e-5, running_mean abs 1e-6 after one call (the trajectory
     test: abs 2e-4, see tests/test_oracle_golden._check_running);
   * losses |dloss| <= 1e-4 / 2e-3 / 5e-3 / 1e-2 over epochs 0-3: the near-tie flips above, then
@@ -193,7 +193,9 @@ def test_vgg_bn_gradient_teacher_forced_decisions(pool, dropout, items):
         lrefs.append(lref.item())
     np.testing.assert_allclose(loss, lrefs, atol=1e-5)
     ref = torch.cat([p.grad.reshape(-1) for p in P]).numpy()
-    _check_grad(g, ref, rtol=2e-5)
+    # 2e-5 on the fp32-MFMA build; the split-bf16 GEMMs measured up to 1.16x that
+    # (profiles/r03z/pytest.log), as in test_gpu_vgg.py's TF_TOL
+    _check_grad(g, ref, rtol=5e-5)
     # per-worker statistics of the chunk vs each worker's own BatchNorm batch (oracle, fp64)
     st = stats.double().cpu().numpy()
     for wi, it in enumerate(items):
