@@ -323,8 +323,10 @@ def main():
         achieved = fl / cnt / avg_s / 1e12
         gemm_ms = sum(v[1] for v in kern.values())
         gemm_fl = sum(v[2] for v in kern.values())
-        traffic = TRAFFIC.get(name) if args.model == "PerformantNet1" else None
         x6 = name in X6_KERNELS or name.startswith("vgg")
+        traffic = TRAFFIC.get(name) if args.model == "PerformantNet1" else None
+        if traffic and x6 and traffic.get("math") != "bf16x6":
+            traffic = None      # profiles/traffic.json was counted on the fp32 kernel
         peak = MFMA_X6_PEAK_TFLOPS if x6 else MFMA_F32_PEAK_TFLOPS
         roofline = dict(bound="mfma", kernel=name, achieved=round(achieved, 2),
                         peak=round(peak, 1), unit="TFLOP/s",
