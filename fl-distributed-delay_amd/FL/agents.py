@@ -61,10 +61,15 @@ for _n in ("untyped_storage", "data_ptr", "size", "dim", "numel", "stride", "sto
     if hasattr(torch.Tensor, _n):
         _META.add(getattr(torch.Tensor, _n))
 for _n in ("shape", "dtype", "device", "is_cuda", "requires_grad", "grad_fn", "is_leaf", "layout",
-           "ndim", "is_sparse", "is_quantized", "is_meta", "names", "_base", "grad", "data"):
+           "ndim", "is_sparse", "is_quantized", "is_meta", "names", "grad"):
     _pr = getattr(torch.Tensor, _n, None)
     if _pr is not None and hasattr(_pr, "__get__"):
         _META.add(_pr.__get__)
+# .data and ._base hand out another tensor over the same storage: they reduce the slabs first and
+# the tensor they return is itself lazy, so a later read through it (p.grad.data.sum() after more
+# fwd_bkwd calls) reduces again instead of reading a stale partial sum
+_ALIASING = {getattr(torch.Tensor, _n).__get__ for _n in ("data", "_base")
+             if hasattr(getattr(torch.Tensor, _n, None), "__get__")}
 del _n, _pr
 
 
@@ -91,7 +96,14 @@ class _LazyGrad(torch.Tensor):
                             seen.append(ctx)
                             ctx.flush(touched=True)
         with torch._C.DisableTorchFunctionSubclass():
-            return func(*args, **kwargs)
+            out = func(*args, **kwargs)
+        if func in _ALIASING and isinstance(out, torch.Tensor) and args and \
+                isinstance(args[0], _LazyGrad):
+            if not isinstance(out, _LazyGrad):
+                out = torch.Tensor._make_subclass(_LazyGrad, out, False)
+            if "_flsim_ctx" not in out.__dict__:
+                out.__dict__["_flsim_ctx"] = args[0].__dict__.get("_flsim_ctx")
+        return out
 
     def __repr__(self, *, tensor_contents=None):
         return repr(self.as_subclass(torch.Tensor))
@@ -172,13 +184,15 @@ class _ModelContext:
         cw = -(-n_samples // 128)
         if cw > self.engine.chunk_workers:
             old = self.engine
+            if self.G is not None:
+                # the old engine's slabs, reduced by the old engine before it goes away (flush
+                # runs end_epoch on self.engine, so this comes before the replacement)
+                self.flush()
+                self.carry = self.G.clone()
             self.engine = self.engine_cls(self.device, chunk_workers=cw)
             if old.STATS_PER_WORKER:        # the running buffers stay where the module sees them
                 self.engine.running = old.running
                 self.engine.num_batches_tracked = old.num_batches_tracked
-            if self.G is not None:
-                self.flush()                # the old engine's slabs, before they go away
-                self.carry = self.G.clone()
             self.packed = False
         if cw > self.loss_buf.numel():
             self.loss_buf = torch.zeros(cw, device=self.device)

@@ -10,12 +10,13 @@
 // go into ONE instruction over the same 16-deep k-step: its 32 slots are (term, k) pairs.  A lane
 // of the 16x16x32 MFMA supplies slots 8g .. 8g+7 (g = lane >> 4) of its row / column; with the
 // k-contiguous LDS unit of 4 k values per lane (k = 4g .. 4g+3, gemm_core.h) the A operand is
-// the 16-B unit [ah | am] (slots 8g..8g+3 = ah, 8g+4..8g+7 = am) and B is [bh | bh], etc.:
-//     MFMA 1: A [h|m] x B [h|h]  = ah bh + am bh
-//     MFMA 2: A [h|m] x B [m|m]  = ah bm + am bm
+// the 16-B unit [ah | am] (slots 8g..8g+3 = ah, 8g+4..8g+7 = am) and B is [bh | bm], etc.:
+//     MFMA 1: A [h|m] x B [h|m]  = ah bh + am bm
+//     MFMA 2: A [h|m] x B [m|h]  = ah bm + am bh
 //     MFMA 3: A [h|l] x B [l|h]  = ah bl + al bh
-// so the LDS holds two 16-B combination planes of the A tile and three of the B tile, each laid
-// out and swizzled exactly like the fp32 KC tile, and every fragment is one ds_read_b128.
+// so the LDS holds two 16-B combination planes of each tile (A: [h|m], [h|l]; B: [h|m], [l|h]),
+// each laid out and swizzled exactly like the fp32 KC tile; every fragment is one ds_read_b128,
+// and B's [m|h] is its [h|m] fragment with the two halves swapped in registers.
 // k-major operands (the weight gradients: the pixel is the reduction index of both dZ and im2col)
 // keep three plain planes h, m, l as [16 k][rows] bf16 and read each 4-k half with gfx950's
 // transposing ds_read_b64_tr_b16 (lane 4q+p of a 16-lane group addresses k row q, columns

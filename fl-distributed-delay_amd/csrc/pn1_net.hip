@@ -421,9 +421,13 @@ static StepPlan plan_in_use(const GradState& g, const void* gradstate) {
 // round.  The side stream joins back before a data gradient overwrites a buffer a queued weight
 // gradient still reads (gx holds dz5, dz3, dz1 in turn) and at the end of the backward pass.
 // One non-blocking side stream and two events per device, created on first use.
+// The two events are shared by every backward pass on the device, so a pass holds `mu` from its
+// first fork to its last join: two host threads' passes would otherwise record and wait on each
+// other's events (a weight gradient could start before its own dZ is written).
 struct SideStream {
     hipStream_t s = nullptr;
     hipEvent_t to_side = nullptr, to_main = nullptr;
+    std::mutex* mu = nullptr;
 };
 static SideStream* side_stream() {
     static std::mutex mu;
@@ -439,6 +443,7 @@ static SideStream* side_stream() {
             ss = SideStream{};
             return nullptr;
         }
+        ss.mu = new std::mutex();          // lives as long as the process, like the stream
     }
     return &ss;
 }
@@ -460,6 +465,8 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     const float s25 = dropout ? SCALE_P25 : 1.f;
     const float s50 = dropout ? SCALE_P50 : 1.f;
     SideStream* ss = concurrent_backward(S) ? side_stream() : nullptr;
+    std::unique_lock<std::mutex> ss_lock;
+    if (ss) ss_lock = std::unique_lock<std::mutex>(*ss->mu);   // fork .. last join (SideStream)
     hipStream_t sw = ss ? ss->s : st;              // the weight gradients' stream
     auto fork = [&]() -> int {                     // sw sees everything queued on st so far
         if (!ss) return 0;

@@ -54,3 +54,18 @@ def test_views_alias_the_buffer_and_assign_as_grad():
     assert p.grad is w
     G[0] = 42.0
     assert float(p.grad[0, 0]) == 42.0
+
+
+def test_data_and_base_reduce_and_stay_lazy():
+    """p.grad.data / p.grad._base hand out another tensor over G: they reduce first, and what they
+    return reduces again on its own later reads (they used to be metadata, so the
+    common .grad.data idiom read a stale partial sum)."""
+    ctx, G, (w, b) = _views()
+    d = w.data
+    assert ctx.flushes == 1 and ctx.touched
+    assert float(d.sum()) == 15.0 and ctx.flushes == 2      # a later read through .data reduces
+    base = b._base                       # None for these views (made by _make_subclass)
+    assert ctx.flushes == 3
+    if base is not None:
+        assert base.untyped_storage().data_ptr() == G.untyped_storage().data_ptr()
+        assert float(base.sum()) == 45.0 and ctx.flushes == 4

@@ -118,6 +118,31 @@ def test_mixed_batch_sizes_in_one_epoch(pool):
     assert all(p.grad.data_ptr() == t.data_ptr() for p, t in zip(model.parameters(), grads))
 
 
+def test_mixed_batch_sizes_untouched_grads(pool):
+    """The same two calls with no .grad read in between: the engine grows while the
+    128-sample gradient still sits in the old engine's slabs.  The epoch's gradient read after the
+    second call equals the one read with a flush between the calls, bit for bit."""
+    from FL.agents import Worker
+
+    def run(read_between):
+        model, central = _fresh_central()
+        ws = [Worker(nn.CrossEntropyLoss()) for _ in range(2)]
+        model.train()
+        xa, ya = _batch(pool, 128, 1)
+        xb, yb = _batch(pool, 256, 2)
+        ws[0].model = model
+        grads, _ = ws[0].fwd_bkwd(xa.to(DEV), ya.to(DEV))
+        if read_between:
+            float(grads[0].sum())
+        ws[1].model = model
+        grads, _ = ws[1].fwd_bkwd(xb.to(DEV), yb.to(DEV))
+        return torch.cat([t.reshape(-1) for t in grads]).cpu().numpy()
+
+    g_read, g_untouched = run(True), run(False)
+    assert np.abs(g_read).max() > 0
+    assert np.array_equal(g_read.view(np.uint32), g_untouched.view(np.uint32))
+
+
 def test_interleaved_stale_entries_update_model(pool):
     """weight_ups = [fresh, stale(t=0), fresh, stale(t=0), fresh] in worker order (two slow
     workers popping the same epoch): Central.update_model == the oracle's cascade + Adam, bit

@@ -37,6 +37,16 @@ def probe_name(kname):
     m = re.search(r"k_agg_stream<(true|false)>", kname)
     if m:
         return "aggregate_adam" if m.group(1) == "true" else "aggregate_adam_seq"
+    # linear layers (net_kernels.h linear_fwd / linear_wgrad / linear_dgrad): linear1 runs the
+    # 128x128 tiles (fp32 dgrad) or the split-bf16 kernel, linear2 the 64x64 fp32 tiles
+    if "RowsKC" in kname or "RowsKM" in kname:
+        big = "gemm_x6_kernel" in kname or "gemm_kernel<4, 4, 2, 2" in kname
+        if "EpiSlabStore" in kname and "Im2col" not in kname:
+            return "linear1_fwd" if big else "linear2_fwd"
+        if re.search(r"RowsKM<\d+, \d+, 0, 0>, flsim::RowsKM", kname):
+            return "linear1_wgrad" if big else "linear2_wgrad"
+        if "EpiDropMask" in kname and "Im2col" not in kname:
+            return "linear1_dgrad" if big else "linear2_dgrad"
     m = re.search(r"Im2colKM<(\d+), (\d+), (\d+),", kname)
     if m:
         return f"conv{FWD[tuple(map(int, m.groups()))]}_wgrad"
@@ -49,6 +59,12 @@ def probe_name(kname):
     return None
 
 
+# probe name -> the arithmetic of the kernel that ran it: "bf16x6" for gemm_x6_kernel (gemm_x6.h,
+# fp32 operands split into three bf16 parts on the bf16 matrix cores), "fp32" otherwise;
+# bench.py only borrows a split kernel's traffic from a table tagged bf16x6
+maths = {}
+
+
 def read(path, counter):
     out = {}
     with open(path) as f:
@@ -58,6 +74,7 @@ def read(path, counter):
             name = probe_name(r["Kernel_Name"])
             if name is None:
                 continue
+            maths[name] = "bf16x6" if "gemm_x6_kernel" in r["Kernel_Name"] else "fp32"
             out.setdefault(name, []).append(float(r["Counter_Value"]))
     return out
 
@@ -72,7 +89,7 @@ def main():
         f = 2 * 1024 * sum(fetch[k]) / len(fetch[k])
         w = 1024 * sum(write[k]) / len(write[k])
         res[k] = dict(bytes_per_launch=int(f + w), fetch=int(f), write=int(w),
-                      launches=len(fetch[k]),
+                      launches=len(fetch[k]), math=maths.get(k, "fp32"),
                       source=f"rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE, "
                              f"{os.path.basename(os.path.normpath(d))}")
     stats = os.path.join(d, "trace", "run_kernel_stats.csv")
