@@ -108,6 +108,23 @@ struct IsStaged : std::false_type {};
 template <class E>
 struct IsStaged<E, std::void_t<decltype(E::STAGED)>> : std::bool_constant<E::STAGED> {};
 
+// Staged epilogues with PARTIAL = true take a tile narrower than the output row: the kernels call
+// store_rows(tile, ld, m0, bm, n0, bn, tid, nt) with the tile's columns [n0, n0 + bn)
+template <class E, class = void>
+struct IsPartial : std::false_type {};
+template <class E>
+struct IsPartial<E, std::void_t<decltype(E::PARTIAL)>> : std::bool_constant<E::PARTIAL> {};
+
+// store the staged tile's rows through the epilogue (full rows, or the PARTIAL column range)
+template <class EPI>
+__device__ __forceinline__ void staged_store(const EPI& epi, const float* tile, int ld, int m0,
+                                             int bm, int n0, int bn, int tid, int nt) {
+    if constexpr (IsPartial<EPI>::value)
+        epi.store_rows(tile, ld, m0, bm, n0, bn, tid, nt);
+    else
+        epi.store_rows(tile, ld, m0, bm, tid, nt);
+}
+
 // Epilogues with PRE = true load the per-fragment inputs of a fragment row first
 // (pre4(m, n, z) -> f32x4), then store its fragments (apply4p(m, n, z, acc, pre))
 template <class E, class = void>

@@ -21,8 +21,10 @@ namespace flsim {
 // dZ with the flipped weights) loaded per wave into MFMA fragments.  Same K order and the same
 // geometry options (WIN: pool-window row order; OHX: explicit output size) as Im2colKC with
 // CI % 16 == 0: k-step ks = 9 * (ci0 / 16) + tap.
-template <int IH, int IW, int CI, int PAD, int FM, bool WIN = false, int OHX = 0>
+template <int IH, int IW, int CI, int PAD, int FM, bool WIN = false, int OHX = 0,
+          class SRC = BufSrc>
 struct Im2colDirect {
+    using Unit = typename SRC::Unit;
     static constexpr int OH = OHX > 0 ? OHX : IH + 2 * PAD - 2;
     static constexpr int OW = OHX > 0 ? OHX : IW + 2 * PAD - 2;
     static constexpr int PH = OH / 2, PW = OW / 2;
@@ -30,15 +32,16 @@ struct Im2colDirect {
     static_assert(CI % 16 == 0, "direct A needs whole 16-channel slices");
 
     const float* X;
+    const float* XL = nullptr;   // SRC = XsSrc: X is the HM part, XL the L part (split.h)
     int M;
     unsigned vb[FM];          // byte offset of input pixel (oh - PAD, ow - PAD), channel 4 (lane >> 4)
     unsigned short tapmask[FM];
-    BufSrc buf;
+    SRC buf;
 
     // r0: the wave's first row; fragment f covers rows r0 + 16 f + (lane & 15)
     __device__ void setup(int r0, int lane) {
         const int q = lane >> 4;
-        buf.init(X, (unsigned long)((M + ROWS_PER_IMG - 1) / ROWS_PER_IMG) * IH * IW * CI * 4);
+        buf.init(X, XL, (unsigned long)((M + ROWS_PER_IMG - 1) / ROWS_PER_IMG) * IH * IW * CI * 4);
 #pragma unroll
         for (int f = 0; f < FM; ++f) {
             const int m = r0 + 16 * f + (lane & 15);
@@ -68,7 +71,7 @@ struct Im2colDirect {
             tapmask[f] = (unsigned short)msk;
         }
     }
-    __device__ void load(int ks, f32x4 (&r)[FM]) const {
+    __device__ void load(int ks, Unit (&r)[FM]) const {
         const int cs = ks / 9;                  // uniform
         const int khkw = ks - 9 * cs;
         const int kh = khkw / 3;

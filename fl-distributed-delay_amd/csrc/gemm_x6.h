@@ -27,40 +27,37 @@
 // TF/s against 148).
 #pragma once
 #include "gemm_core.h"
+#include "split.h"
 
 namespace flsim {
-
-typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
-typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
-
-struct SplitBf16 {
-    bf16x4v h, m, l;
-};
-
-__device__ __forceinline__ SplitBf16 split_bf16(f32x4 x) {
-    SplitBf16 p;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        const __bf16 h = (__bf16)x[e];
-        const float r1 = x[e] - (float)h;
-        const __bf16 m = (__bf16)r1;
-        const float r2 = r1 - (float)m;
-        p.h[e] = h;
-        p.m[e] = m;
-        p.l[e] = (__bf16)r2;
-    }
-    return p;
-}
-
-// two bf16x4 halves as one 16-B LDS unit (f32x4 bits)
-__device__ __forceinline__ f32x4 cat_bf16(bf16x4v a, bf16x4v b) {
-    const bf16x8v v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-    return __builtin_bit_cast(f32x4, v);
-}
 
 __device__ __forceinline__ f32x4 mfma_x32(f32x4 a, f32x4 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8v, a),
                                                    __builtin_bit_cast(bf16x8v, b), c, 0, 0, 0);
+}
+
+// One k-step of a 16x16 output tile: the six partial products of its 16 k, A = ([h|m] a0,
+// [h|l] a1), B = ([h|m] b0, [m|h] b1, [l|h] b2), smallest terms first.  FLSIM_X6_FRESH (default):
+// the three MFMAs accumulate into a fresh register from zero and the k-step's sum is added to the
+// running accumulator with one IEEE fp32 add (round to nearest even) per element; otherwise they
+// accumulate straight into the running sum.  The bf16 MFMA's own accumulation is not a chain of
+// correctly rounded fp32 adds: over long reductions (weight gradients, data gradients through
+// several layers) the fresh form measured closer to fp64.
+#ifndef FLSIM_X6_FRESH
+#define FLSIM_X6_FRESH 1
+#endif
+__device__ __forceinline__ f32x4 x6_step(f32x4 acc, f32x4 a0, f32x4 a1, f32x4 b0, f32x4 b1,
+                                         f32x4 b2) {
+    if constexpr (FLSIM_X6_FRESH) {
+        f32x4 t = mfma_x32(a1, b2, f32x4{0.f, 0.f, 0.f, 0.f});   // ah bl + al bh
+        t = mfma_x32(a0, b1, t);                                   // ah bm + am bh
+        t = mfma_x32(a0, b0, t);                                   // ah bh + am bm
+        return acc + t;
+    } else {
+        acc = mfma_x32(a1, b2, acc);
+        acc = mfma_x32(a0, b1, acc);
+        return mfma_x32(a0, b0, acc);
+    }
 }
 
 typedef short s16x4v __attribute__((ext_vector_type(4)));
@@ -87,20 +84,22 @@ struct X6Tile {
     struct Frag {
         f32x4 x0, x1, x2;
     };
-    __device__ static void store(float* s, int a, int b, f32x4 v, bool valid) {
-        const SplitBf16 p = split_bf16(v);
+    // a unit already in the split form (split.h: loaders over HM / L tensors): plane stores only
+    __device__ static void store(float* s, int a, int b, const XsUnit& v, bool valid) {
         if constexpr (KC) {
-            store_unit<true, ROWS>(s, a, b, cat_bf16(p.h, p.m));
-            store_unit<true, ROWS>(s + PLANE_FL, a, b, AROLE ? cat_bf16(p.h, p.l)
-                                                             : cat_bf16(p.l, p.h));
+            store_unit<true, ROWS>(s, a, b, v.hm);
+            store_unit<true, ROWS>(s + PLANE_FL, a, b, AROLE ? xs_hl(v) : xs_lh(v));
         } else {
             const int off = valid ? a * LD + 4 * b : GK * LD;   // bf16 units
-#pragma unroll
-            for (int pl = 0; pl < 3; ++pl) {
-                const bf16x4v x = pl == 0 ? p.h : pl == 1 ? p.m : p.l;
-                *reinterpret_cast<bf16x4v*>(reinterpret_cast<__bf16*>(s + pl * PLANE_FL) + off) = x;
-            }
+            __bf16* base = reinterpret_cast<__bf16*>(s) + off;
+            *reinterpret_cast<f32x2*>(base) = f32x2{v.hm.x, v.hm.y};
+            *reinterpret_cast<f32x2*>(base + 2 * PLANE_FL) = f32x2{v.hm.z, v.hm.w};
+            *reinterpret_cast<f32x2*>(base + 4 * PLANE_FL) = v.l;
         }
+    }
+    // an fp32 unit: split here, when it is staged
+    __device__ static void store(float* s, int a, int b, f32x4 v, bool valid) {
+        store(s, a, b, xs_of(v), valid);
     }
     __device__ static Frag frag(const float* s, int r0, int lane) {
         Frag f;
@@ -196,11 +195,13 @@ gemm_x6_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, in
         for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     float asum = 0.f;
-    f32x4 ra[AL::UNITS];
-    f32x4 rb[BL::UNITS];
+    typename AL::Unit ra[AL::UNITS];
+    typename BL::Unit rb[BL::UNITS];
     auto stage = [&](float* s) {
-        al.each_unit(ra, [&](int a, int c, f32x4 v, bool ok) { TA::store(s, a, c, v, ok); });
-        bl.each_unit(rb, [&](int a, int c, f32x4 v, bool ok) { TB::store(s + TA::FL, a, c, v, ok); });
+        al.each_unit(ra, [&](int a, int c, const auto& v, bool ok) { TA::store(s, a, c, v, ok); });
+        bl.each_unit(rb, [&](int a, int c, const auto& v, bool ok) {
+            TB::store(s + TA::FL, a, c, v, ok);
+        });
     };
 
     if (ks0 < ks1) {
@@ -238,11 +239,7 @@ gemm_x6_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, in
             const typename TA::Frag af = TA::frag(A, wm * 16 * FM + 16 * i, lane);
 #pragma unroll
             for (int j = 0; j < FN; ++j) {
-                f32x4 c = acc[i][j];
-                c = mfma_x32(af.x1, bf[j].x2, c);     // ah bl + al bh: smallest terms first
-                c = mfma_x32(af.x0, bf[j].x1, c);     // ah bm + am bh
-                c = mfma_x32(af.x0, bf[j].x0, c);     // ah bh + am bm
-                acc[i][j] = c;
+                acc[i][j] = x6_step(acc[i][j], af.x0, af.x1, bf[j].x0, bf[j].x1, bf[j].x2);
             }
         }
         __syncthreads();
@@ -253,7 +250,8 @@ gemm_x6_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, in
         if (tn == 0 && tid < BM) epi.asum(m0 + tid, tz, asum);
     }
     if constexpr (STAGED) {
-        static_assert(BN == EPI::NCOL, "staged epilogue needs the full row in one block");
+        static_assert(BN == EPI::NCOL || (IsPartial<EPI>::value && EPI::NCOL % BN == 0),
+                      "staged epilogue needs the full row in one block");
         constexpr int PASSES = (WAVES_M + WM_PASS - 1) / WM_PASS;
 #pragma unroll 1
         for (int pass = 0; pass < PASSES; ++pass) {
@@ -272,8 +270,8 @@ gemm_x6_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, in
             }
             __syncthreads();
             const int wm_hi = (pass + 1) * WM_PASS < WAVES_M ? (pass + 1) * WM_PASS : WAVES_M;
-            epi.store_rows(lds, STAGE_LD, m0 + pass * WM_PASS * WROWS,
-                           (wm_hi - pass * WM_PASS) * WROWS, tid, 64 * WAVES_M * WAVES_N);
+            staged_store(epi, lds, STAGE_LD, m0 + pass * WM_PASS * WROWS,
+                         (wm_hi - pass * WM_PASS) * WROWS, n0, BN, tid, 64 * WAVES_M * WAVES_N);
         }
     } else if constexpr (HasPre<EPI>::value) {
 #pragma unroll

@@ -2,6 +2,7 @@
 #pragma once
 #include "gemm_core.h"
 #include "pn1.h"
+#include "split.h"
 
 namespace flsim {
 
@@ -29,18 +30,47 @@ __device__ __forceinline__ f32x4 ldg4_or0(const float* p, const float* /*safe*/,
 #define FLSIM_BUFLOAD 1
 #endif
 constexpr unsigned BUF_OOB = 0xfffffff0u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t raw_rsrc(const void* base, unsigned long bytes) {
+    // raw buffer (stride 0): num_records in bytes; dword 3 = the gfx9 raw-buffer format word
+    const unsigned n = bytes < (unsigned long)BUF_OOB ? (unsigned)bytes : BUF_OOB;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)n, 0x00020000);
+}
 struct BufSrc {
+    using Unit = f32x4;
+    static constexpr bool SPLIT = false;
     __amdgpu_buffer_rsrc_t r;
     __device__ __forceinline__ void init(const float* base, unsigned long bytes) {
-        // raw buffer (stride 0): num_records in bytes; dword 3 = the gfx9 raw-buffer format word
-        const unsigned n = bytes < (unsigned long)BUF_OOB ? (unsigned)bytes : BUF_OOB;
-        r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, (int)n,
-                                              0x00020000);
+        r = raw_rsrc(base, bytes);
+    }
+    __device__ __forceinline__ void init(const float* base, const float*, unsigned long bytes) {
+        init(base, bytes);
     }
     __device__ __forceinline__ f32x4 ld(unsigned byte_off) const {
         return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
     }
     __device__ __forceinline__ f32x4 ld_or0(unsigned byte_off, bool ok) const {
+        return ld(ok ? byte_off : BUF_OOB);
+    }
+};
+// The same over a tensor in the split-bf16 form (split.h): byte offsets are the fp32 tensor's; the
+// HM unit is read at that offset and the L unit at half of it.  A masked unit's BUF_OOB halves to
+// 0x7ffffff8, still past the end of the L buffer (< 2 GB: every split tensor here is; the fp32
+// equivalent is < 4 GB), so both reads return zeros.
+struct XsSrc {
+    using Unit = XsUnit;
+    static constexpr bool SPLIT = true;
+    __amdgpu_buffer_rsrc_t rhm, rl;
+    __device__ __forceinline__ void init(const float* hm, const float* l, unsigned long bytes) {
+        rhm = raw_rsrc(hm, bytes);
+        rl = raw_rsrc(l, bytes / 2);
+    }
+    __device__ __forceinline__ XsUnit ld(unsigned byte_off) const {
+        XsUnit u;
+        u.hm = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rhm, byte_off, 0, 0));
+        u.l = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rl, byte_off >> 1, 0, 0));
+        return u;
+    }
+    __device__ __forceinline__ XsUnit ld_or0(unsigned byte_off, bool ok) const {
         return ld(ok ? byte_off : BUF_OOB);
     }
 };
@@ -77,8 +107,10 @@ struct SmallDiv {
 // OHX > 0: output OHX x OHX instead of IH + 2 PAD - 2, i.e. taps past the bottom/right edge of X
 // read as zero (conv6's data gradient over the compact 14x14 dZ, whose 15th row/column would be
 // zero: the floor-mode pool never reads conv6's row/column 14).
-template <int IH, int IW, int CI, int PAD, int TR, int NT, bool WIN = false, int OHX = 0>
+template <int IH, int IW, int CI, int PAD, int TR, int NT, bool WIN = false, int OHX = 0,
+          class SRC = BufSrc>
 struct Im2colKC {
+    using Unit = typename SRC::Unit;
     static constexpr int ROWS = TR;
     static constexpr bool KC = true;
     static constexpr int OH = OHX > 0 ? OHX : IH + 2 * PAD - 2;
@@ -94,18 +126,20 @@ struct Im2colKC {
     static_assert(CI == 4 || CI % 16 == 0, "");
 
     const float* X;
+    const float* XL = nullptr;   // SRC = XsSrc: X is the HM part, XL the L part (split.h)
     int M;
     long base[UNITS];       // element offset of input pixel (oh - PAD, ow - PAD), channel 4q
     unsigned vb[UNITS];     // the same in bytes, mod 2^32 (buffer loads)
     short tapmask[UNITS];   // bit kh*3+kw set iff that tap of this output pixel is inside X
     short row[UNITS];
     int q;
-    BufSrc buf;
+    SRC buf;
+    static_assert(FLSIM_BUFLOAD || !SRC::SPLIT, "split operands use buffer loads");
 
     __device__ void setup(int m0, int tid) {
         q = tid & 3;
         if constexpr (FLSIM_BUFLOAD)
-            buf.init(X, (unsigned long)((M + ROWS_PER_IMG - 1) / ROWS_PER_IMG) * IH * IW * CI * 4);
+            buf.init(X, XL, (unsigned long)((M + ROWS_PER_IMG - 1) / ROWS_PER_IMG) * IH * IW * CI * 4);
 #pragma unroll
         for (int j = 0; j < UNITS; ++j) {
             const int u = tid + j * NT;
@@ -139,7 +173,7 @@ struct Im2colKC {
             vb[j] = (unsigned)base[j] * 4u;
         }
     }
-    __device__ void load(int ks, f32x4 (&r)[UNITS]) const {
+    __device__ void load(int ks, Unit (&r)[UNITS]) const {
         if constexpr (TAP_UNIFORM) {
             // channel-slice-major K order: k-step ks = 9 * (ci0 / 16) + tap, so the nine taps of
             // one 16-channel slice of the input window are read in nine consecutive k-steps and
@@ -180,7 +214,7 @@ struct Im2colKC {
     }
     // f(row, chunk, value, valid) for each staged unit (the split-bf16 kernel's plane stores)
     template <class F>
-    __device__ void each_unit(const f32x4 (&r)[UNITS], F&& f) const {
+    __device__ void each_unit(const Unit (&r)[UNITS], F&& f) const {
 #pragma unroll
         for (int j = 0; j < UNITS; ++j)
             if (TOTAL % NT == 0 || row[j] < ROWS) f(row[j], q, r[j], true);
@@ -191,24 +225,27 @@ struct Im2colKC {
 // Row-major matrix whose rows are the tile rows and whose reduction index is contiguous (KC):
 // element (row, k) at P[row * ld + k].  Rows >= NR read as zero.  K must be a multiple of 16.
 // ---------------------------------------------------------------------------------------------
-template <int TR, int NT>
+template <int TR, int NT, class SRC = BufSrc>
 struct RowsKC {
+    using Unit = typename SRC::Unit;
     static constexpr int ROWS = TR;
     static constexpr bool KC = true;
     static constexpr int TOTAL = ROWS * 4;
     static constexpr int UNITS = (TOTAL + NT - 1) / NT;
     static_assert(NT % 4 == 0, "");
+    static_assert(FLSIM_BUFLOAD || !SRC::SPLIT, "split operands use buffer loads");
     const float* P;
+    const float* PL = nullptr;   // SRC = XsSrc: P is the HM part, PL the L part (split.h)
     long ld;
     int NR;
     const float* rowp[UNITS];
     unsigned rowb[UNITS];   // byte offset of the unit's row chunk, BUF_OOB past the matrix
     short row[UNITS];
     int q;
-    BufSrc buf;
+    SRC buf;
     __device__ void setup(int r0, int tid) {
         q = tid & 3;
-        if constexpr (FLSIM_BUFLOAD) buf.init(P, (unsigned long)NR * ld * 4);
+        if constexpr (FLSIM_BUFLOAD) buf.init(P, PL, (unsigned long)NR * ld * 4);
 #pragma unroll
         for (int j = 0; j < UNITS; ++j) {
             const int u = tid + j * NT;
@@ -219,7 +256,7 @@ struct RowsKC {
             rowb[j] = ok ? (unsigned)(((long)(r0 + r) * ld + 4 * q) * 4) : BUF_OOB;
         }
     }
-    __device__ void load(int ks, f32x4 (&r)[UNITS]) const {
+    __device__ void load(int ks, Unit (&r)[UNITS]) const {
 #pragma unroll
         for (int j = 0; j < UNITS; ++j) {
             if constexpr (FLSIM_BUFLOAD)
@@ -235,7 +272,7 @@ struct RowsKC {
     }
     // f(row, chunk, value, valid) for each staged unit (the split-bf16 kernel's plane stores)
     template <class F>
-    __device__ void each_unit(const f32x4 (&r)[UNITS], F&& f) const {
+    __device__ void each_unit(const Unit (&r)[UNITS], F&& f) const {
 #pragma unroll
         for (int j = 0; j < UNITS; ++j)
             if (TOTAL % NT == 0 || row[j] < ROWS) f(row[j], q, r[j], true);
@@ -267,8 +304,9 @@ __device__ __forceinline__ int km_row(int tid) {
 // window of each (k -> row img*PO*PO + oh*PO + ow): conv6's weight gradient skips the pixels
 // the floor-mode pool never reads (their dZ is zero).
 // ---------------------------------------------------------------------------------------------
-template <int TR, int NT, int PO = 0, int PV = 0>
+template <int TR, int NT, int PO = 0, int PV = 0, class SRC = BufSrc>
 struct RowsKM {
+    using Unit = typename SRC::Unit;
     static constexpr int ROWS = TR;
     static constexpr bool KC = false;
     static constexpr int C4 = ROWS / 4;
@@ -277,19 +315,22 @@ struct RowsKM {
     static constexpr int TPR = NT / GK;
     static_assert(NT % GK == 0, "");
     static constexpr int UNITS = (C4 + TPR - 1) / TPR;
+    static_assert(FLSIM_BUFLOAD || !SRC::SPLIT, "split operands use buffer loads");
     const float* P;
+    const float* PL = nullptr;   // SRC = XsSrc: P is the HM part, PL the L part (split.h)
     long ld;
     int NK;
     int NC;
     int krow;
     int c_off[UNITS];
     short c4[UNITS];
-    BufSrc buf;
+    SRC buf;
     __device__ void setup(int c0, int tid) {
         krow = km_row<TPR>(tid);
         if constexpr (FLSIM_BUFLOAD) {
-            const long rows = PO > 0 ? (long)((NK + PV * PV - 1) / (PV * PV)) * PO * PO : NK;
-            buf.init(P, (unsigned long)rows * ld * 4);
+            long rows = NK;
+            if constexpr (PO > 0) rows = (long)((NK + PV * PV - 1) / (PV * PV)) * PO * PO;
+            buf.init(P, PL, (unsigned long)rows * ld * 4);
         }
 #pragma unroll
         for (int j = 0; j < UNITS; ++j) {
@@ -299,7 +340,7 @@ struct RowsKM {
             c_off[j] = (c < C4 && col < NC) ? col : -1;
         }
     }
-    __device__ void load(int ks, f32x4 (&r)[UNITS]) const {
+    __device__ void load(int ks, Unit (&r)[UNITS]) const {
         const int k = ks * GK + krow;
         long row = k;
         if constexpr (PO > 0) {
@@ -332,7 +373,7 @@ struct RowsKM {
     // f(k row, column chunk, value, valid) for each staged unit (split-bf16 plane stores; a
     // surplus unit has valid = false and goes to the plane's spare slot)
     template <class F>
-    __device__ void each_unit(const f32x4 (&r)[UNITS], F&& f) const {
+    __device__ void each_unit(const Unit (&r)[UNITS], F&& f) const {
 #pragma unroll
         for (int j = 0; j < UNITS; ++j) f(krow, c4[j], r[j], C4 % TPR == 0 || c4[j] < C4);
     }
@@ -344,8 +385,9 @@ struct RowsKM {
 // VO > 0: p walks only the top-left VO x VO output window of each image (pairs with RowsKM's
 // PV window).
 // ---------------------------------------------------------------------------------------------
-template <int IH, int IW, int CI, int PAD, int TR, int NT, int VO = 0>
+template <int IH, int IW, int CI, int PAD, int TR, int NT, int VO = 0, class SRC = BufSrc>
 struct Im2colKM {
+    using Unit = typename SRC::Unit;
     static constexpr int ROWS = TR;
     static constexpr bool KC = false;
     static constexpr int OH = VO > 0 ? VO : IH + 2 * PAD - 2;
@@ -356,17 +398,19 @@ struct Im2colKM {
     static constexpr int TPR = NT / GK;
     static_assert(NT % GK == 0, "");
     static constexpr int UNITS = (C4 + TPR - 1) / TPR;
+    static_assert(FLSIM_BUFLOAD || !SRC::SPLIT, "split operands use buffer loads");
     const float* X;
+    const float* XL = nullptr;   // SRC = XsSrc: X is the HM part, XL the L part (split.h)
     int M;  // total pixels
     int krow;
     int coff[UNITS];   // ((kh - PAD) * IW + kw - PAD) * CI + ci: the column's offset from pixel (oh, ow)
     short kh[UNITS], kw[UNITS];   // tap of the column; kh = -64 when it is padding
     short c4[UNITS];
-    BufSrc buf;
+    SRC buf;
     __device__ void setup(int c0, int tid) {
         krow = km_row<TPR>(tid);
         if constexpr (FLSIM_BUFLOAD)
-            buf.init(X, (unsigned long)((M + OH * OW - 1) / (OH * OW)) * IH * IW * CI * 4);
+            buf.init(X, XL, (unsigned long)((M + OH * OW - 1) / (OH * OW)) * IH * IW * CI * 4);
 #pragma unroll
         for (int j = 0; j < UNITS; ++j) {
             const int c = tid % TPR + TPR * j;
@@ -380,7 +424,7 @@ struct Im2colKM {
             coff[j] = real ? ((khkw / 3 - PAD) * IW + (khkw % 3 - PAD)) * CI + ci : 0;
         }
     }
-    __device__ void load(int ks, f32x4 (&r)[UNITS]) const {
+    __device__ void load(int ks, Unit (&r)[UNITS]) const {
         const int p = ks * GK + krow;
         const unsigned img0 = (unsigned)(ks * GK) / (unsigned)(OH * OW);   // block-uniform
         unsigned rem = (unsigned)(ks * GK) - img0 * (OH * OW) + krow, img = img0;
@@ -420,7 +464,7 @@ struct Im2colKM {
     // f(k row, column chunk, value, valid) for each staged unit (split-bf16 plane stores; a
     // surplus unit has valid = false and goes to the plane's spare slot)
     template <class F>
-    __device__ void each_unit(const f32x4 (&r)[UNITS], F&& f) const {
+    __device__ void each_unit(const Unit (&r)[UNITS], F&& f) const {
 #pragma unroll
         for (int j = 0; j < UNITS; ++j) f(krow, c4[j], r[j], C4 % TPR == 0 || c4[j] < C4);
     }

@@ -7,7 +7,9 @@
 // Wf[co][k(khkw, ci)] (forward) and Wd[ci][k(khkw', co)] = W[co][ci][2-kh'][2-kw'] (data
 // gradient), k in Im2colKC's channel-slice-major order (k_pack_fwd).
 #pragma once
+#include "epi_xs.h"
 #include "gemm_direct.h"
+#include "gemm_dx6.h"
 #include "gemm_x6.h"
 #include "loaders.h"
 #include "pn1.h"
@@ -151,10 +153,10 @@ k_pool_scatter(const float* __restrict__ gy, const uint8_t* __restrict__ idx,
 // sample's gy plane set (C * PH * PW floats, contiguous) is read into LDS with coalesced float4
 // loads, then the (window, 4 channels) threads pick their four channels from LDS, so neither
 // side of the transpose makes strided global accesses.
-template <int H, int W, int C>
+template <int H, int W, int C, bool XS = false>
 __global__ void __launch_bounds__(256)
 k_pool_scatter_nchw(const float* __restrict__ gy, const uint8_t* __restrict__ idx,
-                    float* __restrict__ dz) {
+                    float* __restrict__ dz, float* __restrict__ dzl = nullptr) {
     constexpr int PH = H / 2, PW = W / 2, PP = PH * PW;
     constexpr int CH = (H + 1) / 2, CW = (W + 1) / 2;
     constexpr int C4 = C / 4;
@@ -188,15 +190,30 @@ k_pool_scatter_nchw(const float* __restrict__ gy, const uint8_t* __restrict__ id
             v.y = (((id >> 8) & 0xff) == (uint32_t)pos) ? g.y : 0.f;
             v.z = (((id >> 16) & 0xff) == (uint32_t)pos) ? g.z : 0.f;
             v.w = ((id >> 24) == (uint32_t)pos) ? g.w : 0.f;
-            st_nt4(dz + (((long)n * H + h) * W + w) * C + c, v);
+            const long o = (((long)n * H + h) * W + w) * C + c;
+            if constexpr (XS)
+                xs_store(dz, dzl, o / 4, v);     // dZ in the split form (split.h)
+            else
+                st_nt4(dz + o, v);
         }
     }
+}
+
+// pool3's backward into a split dZ (PerformantNet1's dz6, read by conv6's split-bf16 GEMMs)
+template <int H, int W, int C>
+static int pool_scatter_nchw_xs(const float* gy, const uint8_t* idx, float* dzhm, float* dzl, int S,
+                                hipStream_t st) {
+    hipLaunchKernelGGL((k_pool_scatter_nchw<H, W, C, true>), dim3(S), dim3(256), 0, st, gy, idx,
+                       dzhm, dzl);
+    FLSIM_LAUNCH_CHECK();
+    return 0;
 }
 
 template <int H, int W, int C, bool NCHW_G>
 static int pool_scatter(const float* gy, const uint8_t* idx, float* dz, int S, hipStream_t st) {
     if constexpr (NCHW_G) {
-        hipLaunchKernelGGL((k_pool_scatter_nchw<H, W, C>), dim3(S), dim3(256), 0, st, gy, idx, dz);
+        hipLaunchKernelGGL((k_pool_scatter_nchw<H, W, C, false>), dim3(S), dim3(256), 0, st, gy,
+                           idx, dz, nullptr);
     } else {
         const long total = (long)S * ((H + 1) / 2) * ((W + 1) / 2) * (C / 4);
         hipLaunchKernelGGL((k_pool_scatter<H, W, C, false>), dim3(ceil_div(total, 256)), dim3(256),
@@ -445,6 +462,78 @@ static __global__ void k_pack_dgrad(const float* __restrict__ W, float* __restri
     const int khkw = r >> 4;
     const int co = 16 * cs + (r & 15);
     Wd[e] = W[(co * CI + ci) * 9 + (8 - khkw)];
+}
+
+// The same two packings in the split-bf16 form (split.h), one thread per 4-k unit: the forward
+// packing of a layer with CIP % 16 == 0 and the data-gradient packing (PerformantNet1 conv2-6,
+// whose GEMMs read split operands)
+static __global__ void k_pack_fwd_xs(const float* __restrict__ W, float* __restrict__ hm,
+                                     float* __restrict__ l, int CO, int CI, int KP) {
+    const int u = blockIdx.x * 256 + threadIdx.x;
+    if (u >= CO * KP / 4) return;
+    const int e0 = 4 * u;
+    const int co = e0 / KP;
+    const int k0 = e0 - co * KP;
+    f32x4 v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int k = k0 + j;
+        const int cs = k / 144, r = k - 144 * cs;
+        const int khkw = r >> 4;
+        const int ci = 16 * cs + (r & 15);
+        v[j] = (khkw < 9 && ci < CI) ? W[(co * CI + ci) * 9 + khkw] : 0.f;
+    }
+    xs_store<false>(hm, l, u, v);
+}
+static __global__ void k_pack_dgrad_xs(const float* __restrict__ W, float* __restrict__ hm,
+                                       float* __restrict__ l, int CO, int CI) {
+    const int u = blockIdx.x * 256 + threadIdx.x;
+    const int KD = 9 * CO;
+    if (u >= CI * KD / 4) return;
+    const int e0 = 4 * u;
+    const int ci = e0 / KD;
+    const int k0 = e0 - ci * KD;
+    f32x4 v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int k = k0 + j;
+        const int cs = k / 144, r = k - 144 * cs;
+        const int khkw = r >> 4;
+        const int co = 16 * cs + (r & 15);
+        v[j] = W[(co * CI + ci) * 9 + (8 - khkw)];
+    }
+    xs_store<false>(hm, l, u, v);
+}
+// a row-major matrix (linear1's W [512][9408], torch layout) in the split form
+static __global__ void k_split_rows(const float* __restrict__ W, float* __restrict__ hm,
+                                    float* __restrict__ l, long units) {
+    const long u = (long)blockIdx.x * 256 + threadIdx.x;
+    if (u < units) xs_store<false>(hm, l, u, reinterpret_cast<const f32x4*>(W)[u]);
+}
+
+// split tensor: HM part and L part (split.h)
+struct XsT {
+    float* hm;
+    float* l;
+};
+
+static int pack_conv_xs(const float* W, XsT wf, XsT wd, int CO, int CI, int KP, hipStream_t st) {
+    if (CI % 16 != 0 || CO % 16 != 0 || KP != 9 * CI) return 1;
+    hipLaunchKernelGGL(k_pack_fwd_xs, dim3(ceil_div((long)CO * KP / 4, 256)), dim3(256), 0, st, W,
+                       wf.hm, wf.l, CO, CI, KP);
+    FLSIM_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_pack_dgrad_xs, dim3(ceil_div((long)CI * 9 * CO / 4, 256)), dim3(256), 0,
+                       st, W, wd.hm, wd.l, CO, CI);
+    FLSIM_LAUNCH_CHECK();
+    return 0;
+}
+
+static int split_rows(const float* W, XsT out, long n, hipStream_t st) {
+    if (n % 4) return 1;
+    hipLaunchKernelGGL(k_split_rows, dim3(ceil_div(n / 4, 256)), dim3(256), 0, st, W, out.hm, out.l,
+                       n / 4);
+    FLSIM_LAUNCH_CHECK();
+    return 0;
 }
 
 // both packings of one conv layer (wd == nullptr: no data gradient needed, first layer)
@@ -809,31 +898,39 @@ static int conv_like_sz(const float* X, int S, const float* Wpk, int N, int KP, 
 // VO > 0: only the top-left VO x VO window of the output pixels (dz is zero outside it)
 // DZC: dz is already stored compact over that window ([S][VO][VO][CO]), so its rows are the
 // reduction index as they stand
+// SRC = XsSrc: dz and X in the split form (dzl, Xl their L parts; X6 only)
 template <int IH, int IW, int CI, int PAD, int FM, int FN, int WM, int WN, int VO = 0,
-          bool DZC = false, bool X6 = false>
+          bool DZC = false, bool X6 = false, class SRC = BufSrc>
 static int conv_wgrad(const float* dz, const float* X, int S, int CO, int KP, float* slab,
                       float* bslab, int Z, hipStream_t st, int kid, int kreal,
-                      int zinit = 0x7fffffff, int* zused = nullptr) {
+                      int zinit = 0x7fffffff, int* zused = nullptr, const float* dzl = nullptr,
+                      const float* Xl = nullptr) {
     constexpr int NT = 64 * WM * WN;
     constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
     constexpr int OFULL = IH + 2 * PAD - 2;
     static_assert(IH == IW && VO <= OFULL, "square maps only");
-    using AL = RowsKM<BM, NT, (VO > 0 && !DZC ? OFULL : 0), (DZC ? 0 : VO)>;
-    using BL = Im2colKM<IH, IW, CI, PAD, BN, NT, VO>;
+    static_assert(X6 || !SRC::SPLIT, "split operands run on the split-bf16 GEMM");
+    using AL = RowsKM<BM, NT, (VO > 0 && !DZC ? OFULL : 0), (DZC ? 0 : VO), SRC>;
+    using BL = Im2colKM<IH, IW, CI, PAD, BN, NT, VO, SRC>;
     const int M = S * BL::OH * BL::OW;
     AL al;
     al.P = dz;
+    al.PL = dzl;
     al.ld = CO;
     al.NK = M;
     al.NC = CO;
     BL bl;
     bl.X = X;
+    bl.XL = Xl;
     bl.M = M;
     EpiSlabAcc epi{slab, CO, KP, (long)CO * KP, bslab, zinit};
     const int tiles = ceil_div(CO, BM) * ceil_div(KP, BN);
-    static const int cap = resident_blocks(
-        X6 ? (const void*)gemm_x6_kernel<FM, FN, WM, WN, AL, BL, EpiSlabAcc>
-           : (const void*)gemm_kernel<FM, FN, WM, WN, AL, BL, EpiSlabAcc>, NT);
+    const void* kfn;
+    if constexpr (X6)
+        kfn = (const void*)gemm_x6_kernel<FM, FN, WM, WN, AL, BL, EpiSlabAcc>;
+    else
+        kfn = (const void*)gemm_kernel<FM, FN, WM, WN, AL, BL, EpiSlabAcc>;
+    static const int cap = resident_blocks(kfn, NT);
     const int zu = wsplit(ceil_div(M, GK), Z, tiles, cap);
     if (zused) *zused = zu;
     return launch_gemm<FM, FN, WM, WN, X6>(al, bl, epi, CO, KP, ceil_div(M, GK), zu, st, kid,
@@ -844,15 +941,68 @@ static int conv_wgrad(const float* dz, const float* X, int S, int CO, int KP, fl
 // (profiles/r03f/lab_s640_wgrad.txt: at 640 samples 96x96 4-wave tiles beat the 128-worker
 // chunk's larger ones on conv3/5/6 by 3-10 %, 48x144 beats 48x48 on conv2 by 4 %)
 template <int IH, int IW, int CI, int PAD, int FM, int FN, int WM, int WN, int FMS, int FNS,
-          int WMS, int WNS, int VO = 0, bool DZC = false, bool X6 = false>
+          int WMS, int WNS, int VO = 0, bool DZC = false, bool X6 = false, class SRC = BufSrc>
 static int conv_wgrad_sz(const float* dz, const float* X, int S, int CO, int KP, float* slab,
                          float* bslab, int Z, hipStream_t st, int kid, int kreal, int zinit,
-                         int* zused) {
+                         int* zused, const float* dzl = nullptr, const float* Xl = nullptr) {
     if (S <= small_chunk_samples())
-        return conv_wgrad<IH, IW, CI, PAD, FMS, FNS, WMS, WNS, VO, DZC, X6>(
-            dz, X, S, CO, KP, slab, bslab, Z, st, kid, kreal, zinit, zused);
-    return conv_wgrad<IH, IW, CI, PAD, FM, FN, WM, WN, VO, DZC, X6>(
-        dz, X, S, CO, KP, slab, bslab, Z, st, kid, kreal, zinit, zused);
+        return conv_wgrad<IH, IW, CI, PAD, FMS, FNS, WMS, WNS, VO, DZC, X6, SRC>(
+            dz, X, S, CO, KP, slab, bslab, Z, st, kid, kreal, zinit, zused, dzl, Xl);
+    return conv_wgrad<IH, IW, CI, PAD, FM, FN, WM, WN, VO, DZC, X6, SRC>(
+        dz, X, S, CO, KP, slab, bslab, Z, st, kid, kreal, zinit, zused, dzl, Xl);
+}
+
+// ---- split-form operands (split.h): the PerformantNet1 conv2-6 forward / data-gradient GEMMs --
+// conv (forward, or data gradient as a valid convolution) over a split input X and split packed
+// weights W [N][KP] on the direct-A kernel (gemm_dx6.h): WAVES waves of 16*FM rows, 16*FN columns
+// per n-tile, B staged KB k-steps a time (NPL planes), A loaded DEPTH k-steps ahead
+template <int IH, int IW, int CI, int PAD, int FM, int FN, int WAVES, int KB, int DEPTH, int NPL,
+          bool WIN, int OHX, class EPI>
+static int conv_dx6(XsT X, int S, XsT W, int N, int KP, const EPI& epi, hipStream_t st, int kid,
+                    int kreal) {
+    using AD = Im2colDirect<IH, IW, CI, PAD, FM, WIN, OHX, XsSrc>;
+    using BL = RowsKCStageXs<16 * FN, 64 * WAVES, NPL>;
+    constexpr int BM = 16 * FM * WAVES, BN = 16 * FN;
+    FLSIM_REQUIRE((KP / GK) % KB == 0, "direct GEMM: %d k-steps not a multiple of %d", KP / GK, KB);
+    AD ad;
+    ad.X = X.hm;
+    ad.XL = X.l;
+    ad.M = S * AD::ROWS_PER_IMG;
+    BL bl;
+    bl.P = W.hm;
+    bl.PL = W.l;
+    bl.ld = KP;
+    bl.NR = N;
+    const int tm = ceil_div(ad.M, BM), tn = ceil_div(N, BN);
+    const ProbeSlot ps = probe_begin();
+    hipExtLaunchKernelGGL((gemm_dx6_kernel<FM, FN, WAVES, KB, DEPTH, AD, BL, EPI>),
+                          dim3(tm * tn), dim3(64 * WAVES), 0, st, ps.start, ps.stop, 0, ad, bl,
+                          epi, KP / GK, tm, tn);
+    FLSIM_LAUNCH_CHECK();
+    return probe_end(ps, kid, 2.0 * ad.M * N * kreal);
+}
+
+// the same GEMM on gemm_x6_kernel with both operands staged through LDS (bit-identical to
+// conv_dx6: same split, same MFMA order per output): the tiles for small chunks
+template <int IH, int IW, int CI, int PAD, int FM, int FN, int WM, int WN, bool WIN, int OHX,
+          class EPI>
+static int conv_xs(XsT X, int S, XsT W, int N, int KP, const EPI& epi, hipStream_t st, int kid,
+                   int kreal) {
+    constexpr int NT = 64 * WM * WN;
+    constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
+    using AL = Im2colKC<IH, IW, CI, PAD, BM, NT, WIN, OHX, XsSrc>;
+    using BL = RowsKC<BN, NT, XsSrc>;
+    AL al;
+    al.X = X.hm;
+    al.XL = X.l;
+    al.M = S * AL::ROWS_PER_IMG;
+    BL bl;
+    bl.P = W.hm;
+    bl.PL = W.l;
+    bl.ld = KP;
+    bl.NR = N;
+    return launch_gemm<FM, FN, WM, WN, true>(al, bl, epi, al.M, N, KP / GK, 1, st, kid,
+                                             2.0 * al.M * N * kreal);
 }
 
 // forward conv fused with bias + ReLU + 2x2 max-pool (+ dropout: keep iff philox >= thr, kept

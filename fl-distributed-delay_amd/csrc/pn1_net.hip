@@ -4,8 +4,12 @@
 // their gradients are summed (agents.py:35 accumulates into the shared .grad), which the weight
 // gradient GEMMs do along their reduction (pixel / sample) dimension.
 //
-// Layout in HBM: activations NHWC fp32 (channels innermost); the flatten before linear1 is
-// written in torch's NCHW order so linear1 uses the torch weight layout unchanged.
+// Layout in HBM: activations NHWC (channels innermost); the flatten before linear1 is written in
+// torch's NCHW order so linear1 uses the torch weight layout unchanged.  The tensors that feed the
+// conv2-6 GEMMs (a1, d1, a3, d2, a5 and the data gradients dz6 .. dz2) and the packed conv2-6
+// weights are stored in the split-bf16 form (split.h: HM + L parts, written once by their
+// producer), so those GEMMs never split an operand in their inner loops; d3, e1, e2,
+// dz1 and the linear layers stay fp32.
 // Conv weights are re-packed once per epoch (net_kernels.h, shared with the VGG-11 engine
 // vgg_net.hip together with the batch assembly, pool scatter, head, slab reduction and GEMM
 // launchers).
@@ -61,8 +65,10 @@ constexpr int ZH = 32;      // head wgrad split
 
 // gradient-state layout (floats): packed weights + slabs
 struct GradState {
-    float* wf[6];
-    float* wd[6];  // wd[0] unused
+    float* wf[6];  // conv1's fp32 packing (wf[1..5] unused)
+    float* wd[6];  // unused
+    XsT wfx[6];    // conv2-6 forward packings, split (wfx[0] unused)
+    XsT wdx[6];    // conv2-6 data-gradient packings, split (wdx[0] unused)
     float* sw[6];  // conv weight slabs [ZW][CO][KP]
     float* sb[6];  // conv bias slabs [ZW][CO] (fused into the weight-gradient GEMM)
     float* l1w;    // [ZL1W][512][9408]
@@ -108,8 +114,16 @@ static GradState gs_layout(float* base_in) {
         return p;
     };
     for (int l = 0; l < 6; ++l) {
-        g.wf[l] = take((long)GEO[l].CO * GEO[l].KP);
-        g.wd[l] = l ? take((long)GEO[l].CI * 9 * GEO[l].CO) : nullptr;
+        g.wf[l] = l ? nullptr : take((long)GEO[l].CO * GEO[l].KP);
+        g.wd[l] = nullptr;
+        g.wfx[l] = g.wdx[l] = XsT{nullptr, nullptr};
+        if (l) {
+            const long nf = (long)GEO[l].CO * GEO[l].KP, nd = (long)GEO[l].CI * 9 * GEO[l].CO;
+            g.wfx[l].hm = take(nf);
+            g.wfx[l].l = take(nf / 2);
+            g.wdx[l].hm = take(nd);
+            g.wdx[l].l = take(nd / 2);
+        }
     }
     const long slab0 = o;
     g.slab_begin = base + o;
@@ -135,12 +149,16 @@ static GradState gs_layout(float* base_in) {
 }
 
 // workspace (per chunk) layout
+// (a1 .. gx below are the HM parts of split tensors; a1l .. gxl their L parts, half the size)
 struct WS {
     float* x0; float* a1; float* a2; float* d1; float* a3; float* a4; float* d2; float* a5;
     float* a6; float* d3; float* e1; float* e2; float* part; float* dh1; float* dh2;
     float* gx; float* gy; float* loss_s; float* dlog; int32_t* y;
     uint8_t* i1; uint8_t* i2; uint8_t* i3;
+    float* a1l; float* d1l; float* a3l; float* d2l; float* a5l;     // forward split tensors
+    float* a6l; float* a4l; float* a2l; float* gxl;                  // dz6, dz4, dz2, dz5 / dz3
     long bytes;
+    XsT x(float* hm, float* l) const { return XsT{hm, l}; }
 };
 
 static WS ws_layout(char* base, int S) {
@@ -160,15 +178,19 @@ static WS ws_layout(char* base, int S) {
     w.y = (int32_t*)take(4L * S);
     w.i1 = (uint8_t*)take(15552L * S); w.i2 = (uint8_t*)take(11616L * S);
     w.i3 = (uint8_t*)take(9408L * S);
+    w.a1l = tf(55488 / 2); w.d1l = tf(15552 / 2); w.a3l = tf(38400 / 2); w.d2l = tf(11616 / 2);
+    w.a5l = tf(32448 / 2); w.a6l = tf(43200 / 2); w.a4l = tf(46464 / 2); w.a2l = tf(62208 / 2);
+    w.gxl = tf(38400 / 2);
     w.bytes = o;
     return w;
 }
 
 static int pack_weights(const GradState& g, const float* theta, hipStream_t st) {
-    for (int l = 0; l < 6; ++l) {
+    RC(pack_conv(theta + P_OFF[0], g.wf[0], nullptr, GEO[0].CO, GEO[0].CI, GEO[0].CIP, GEO[0].KP,
+                 st));
+    for (int l = 1; l < 6; ++l) {
         const ConvGeo& c = GEO[l];
-        RC(pack_conv(theta + P_OFF[2 * l], g.wf[l], l ? g.wd[l] : nullptr, c.CO, c.CI, c.CIP, c.KP,
-                     st));
+        RC(pack_conv_xs(theta + P_OFF[2 * l], g.wfx[l], g.wdx[l], c.CO, c.CI, c.KP, st));
     }
     return 0;
 }
@@ -188,7 +210,7 @@ constexpr int C1_ROWS = 32;     // output pixels per wave iteration (two 16-row 
 constexpr int C1_LD = 52;       // staging row stride (floats): 16-B aligned, rows on different banks
 __global__ void __launch_bounds__(256)
 k_conv1_fwd(const float* __restrict__ x0, const float* __restrict__ W, const float* __restrict__ bias,
-            float* __restrict__ a1, long units) {
+            float* __restrict__ a1, float* __restrict__ a1l, long units) {
     __shared__ __attribute__((aligned(16))) float stage[4][C1_ROWS * C1_LD];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int i = lane & 15, g = lane >> 4;
@@ -256,17 +278,18 @@ k_conv1_fwd(const float* __restrict__ x0, const float* __restrict__ W, const flo
                 for (int r = 0; r < 4; ++r)
                     st[(16 * t + 4 * g + r) * C1_LD + 16 * j + i] = fmaxf(acc[t][j][r] + bj[j], 0.f);
         __builtin_amdgcn_wave_barrier();
-        f32x4* dst = reinterpret_cast<f32x4*>(a1 + u * C1_ROWS * 48);
+        // a1 in the split form (split.h): each lane splits whole 4-channel units of its rows
 #pragma unroll
         for (int q0 = 0; q0 < C1_ROWS * 12; q0 += 64) {
             const int q = q0 + lane, row = q / 12, c4 = q - (q / 12) * 12;
-            st_nt4(reinterpret_cast<float*>(dst + q), *reinterpret_cast<const f32x4*>(st + row * C1_LD + 4 * c4));
+            xs_store(a1, a1l, u * C1_ROWS * 12 + q,
+                     *reinterpret_cast<const f32x4*>(st + row * C1_LD + 4 * c4));
         }
         __builtin_amdgcn_wave_barrier();
     }
 }
 
-static int conv1_fwd(const float* x0, const float* W, const float* bias, float* a1, int S,
+static int conv1_fwd(const float* x0, const float* W, const float* bias, XsT a1, int S,
                      hipStream_t st) {
     const long M = (long)S * 34 * 34;
     if (M % C1_ROWS) return 1;             // S is a multiple of 128 (whole sample groups)
@@ -276,34 +299,54 @@ static int conv1_fwd(const float* x0, const float* W, const float* bias, float* 
     const int grid = (int)(units / 4 < 2048 ? (units + 3) / 4 : 2048);
     const ProbeSlot ps = probe_begin();
     hipExtLaunchKernelGGL(k_conv1_fwd, dim3(grid), dim3(256), 0, st, ps.start, ps.stop, 0, x0, W,
-                          bias, a1, units);
+                          bias, a1.hm, a1.l, units);
     FLSIM_LAUNCH_CHECK();
     return probe_end(ps, K_FWD1, 2.0 * M * 48 * 27);
 }
 
+// The conv2-6 forward and data-gradient GEMMs: split operands on the direct-A kernel
+// (gemm_dx6.h); DX_FM rows per wave and 8 waves per block, B staged DX_KB k-steps at a time.
+// Chunks of at most small_chunk_samples() samples take 128-row blocks (DX_FMS): the same
+// arithmetic per output (bit-identical), twice the blocks.
+constexpr int DX_FM = 2, DX_FMS = 1, DX_KB = 3, DX_DEPTH = 2, DX_NPL = 2;
+
+template <int IH, int IW, int CI, int PAD, int FN, bool WIN, int OHX, class EPI>
+static int dx6(XsT X, int S, XsT W, int N, int KP, const EPI& epi, hipStream_t st, int kid,
+               int kreal) {
+    if (S <= small_chunk_samples())
+        return conv_dx6<IH, IW, CI, PAD, DX_FMS, FN, 8, DX_KB, DX_DEPTH, DX_NPL, WIN, OHX>(
+            X, S, W, N, KP, epi, st, kid, kreal);
+    return conv_dx6<IH, IW, CI, PAD, DX_FM, FN, 8, DX_KB, DX_DEPTH, DX_NPL, WIN, OHX>(
+        X, S, W, N, KP, epi, st, kid, kreal);
+}
+
 static int forward(const GradState& g, const WS& w, const float* theta, int S,
                    const WorkerRec* workers, uint64_t seed, int dropout, hipStream_t st) {
-    // conv1, conv2 (+ReLU)  models.py:29-30
-    RC(conv1_fwd(w.x0, theta + P_OFF[0], theta + P_OFF[1], w.a1, S, st));
-    // conv2 + ReLU + pool1 + dropout1 (models.py:30-32), one fused launch
-    // (gemm_kernel: the direct-A form measured 7.51 vs 7.30 ms with this epilogue, r03b)
-    RC((conv_pool_fwd<34, 34, 48, 48, 2, 4, 3, 8, 1, false, true>(w.a1, S, g.wf[1], 432, w.d1, w.i1,
-        theta + P_OFF[3], workers, seed, SITE_DROP1, THR_P25, SCALE_P25, dropout, st, K_FWD2,
-        432)));
-    RC((conv_x6<18, 18, 48, 2, 4, 3, 4, 2>(w.d1, S, g.wf[2], 96, 432,
-        EpiBiasRelu{w.a3, theta + P_OFF[5], S * 20 * 20, 96}, st, K_FWD3, 432)));
-    // conv4 + ReLU + pool2 + dropout1 (models.py:34-36)
-    RC((conv_pool_fwd<20, 20, 96, 96, 2, 4, 3, 4, 2, false, true>(w.a3, S, g.wf[3], 864, w.d2,
-        w.i2, theta + P_OFF[7], workers, seed, SITE_DROP2, THR_P25, SCALE_P25, dropout, st,
-        K_FWD4, 864)));
-    RC((conv_x6<11, 11, 96, 2, 4, 6, 4, 2>(w.d2, S, g.wf[4], 192, 864,
-        EpiBiasRelu{w.a5, theta + P_OFF[9], S * 13 * 13, 192}, st, K_FWD5, 864)));
-    // conv6 + ReLU + pool3 + dropout1 (models.py:38-40), written in torch's flatten order
+    const XsT a1 = w.x(w.a1, w.a1l), d1 = w.x(w.d1, w.d1l), a3 = w.x(w.a3, w.a3l);
+    const XsT d2 = w.x(w.d2, w.d2l), a5 = w.x(w.a5, w.a5l);
+    // conv1 + ReLU (models.py:29), a1 written split
+    RC(conv1_fwd(w.x0, theta + P_OFF[0], theta + P_OFF[1], a1, S, st));
+    // conv2 + ReLU + pool1 + dropout1 (models.py:30-32), one fused launch -> d1 (split)
+    RC((dx6<34, 34, 48, 2, 3, true, 0>(a1, S, g.wfx[1], 48, 432,
+        EpiPoolDropXs<18, 18, 48>{d1.hm, d1.l, w.i1, theta + P_OFF[3], workers, seed, SITE_DROP1,
+                                  THR_P25, SCALE_P25, dropout, S * 18 * 18 * 4}, st, K_FWD2, 432)));
+    // conv3 + ReLU (models.py:33) -> a3 (split)
+    RC((dx6<18, 18, 48, 2, 6, false, 0>(d1, S, g.wfx[2], 96, 432,
+        EpiBiasReluXs<96>{a3.hm, a3.l, theta + P_OFF[5], S * 20 * 20}, st, K_FWD3, 432)));
+    // conv4 + ReLU + pool2 + dropout1 (models.py:34-36) -> d2 (split)
+    RC((dx6<20, 20, 96, 2, 6, true, 0>(a3, S, g.wfx[3], 96, 864,
+        EpiPoolDropXs<11, 11, 96>{d2.hm, d2.l, w.i2, theta + P_OFF[7], workers, seed, SITE_DROP2,
+                                  THR_P25, SCALE_P25, dropout, S * 11 * 11 * 4}, st, K_FWD4, 864)));
+    // conv5 + ReLU (models.py:37) -> a5 (split; two 96-column n-tiles)
+    RC((dx6<11, 11, 96, 2, 6, false, 0>(d2, S, g.wfx[4], 192, 864,
+        EpiBiasReluXs<192>{a5.hm, a5.l, theta + P_OFF[9], S * 13 * 13}, st, K_FWD5, 864)));
+    // conv6 + ReLU + pool3 + dropout1 (models.py:38-40), written fp32 in torch's flatten order
     // (models.py:41) so linear1 keeps the torch weight layout; the floor-mode border row/column
     // of the 15x15 output (dropped by the pool) is never computed
-    RC((conv_pool_fwd<13, 13, 192, 192, 2, 4, 6, 4, 2, true, true>(w.a5, S, g.wf[5], 1728, w.d3,
-        w.i3, theta + P_OFF[11], workers, seed, SITE_DROP3, THR_P25, SCALE_P25, dropout, st,
-        K_FWD6, 1728)));
+    RC((dx6<13, 13, 192, 2, 6, true, 0>(a5, S, g.wfx[5], 192, 1728,
+        EpiPoolDrop<7, 7, 192, true>{w.d3, w.i3, theta + P_OFF[11], workers, seed, SITE_DROP3,
+                                     THR_P25, SCALE_P25, dropout, S * 7 * 7 * 4}, st, K_FWD6,
+        1728)));
     // linear1 + relu + dropout2 (models.py:41-43), split-K partials then finish
     // small chunks (configs[1]: 640 samples = 5 x 4 tiles of 128 x 128, 80 blocks with the split)
     // take 64 x 64 tiles: the same split, hence the same sums, with 4x the blocks
@@ -457,6 +500,16 @@ static bool concurrent_backward(int S) {
     return S <= smax;
 }
 
+// debug / measurement: FLSIM_DEBUG_BWD_STOP=6 ends the backward pass after conv6's data gradient
+static int debug_stop() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("FLSIM_DEBUG_BWD_STOP");
+        v = e ? atoi(e) : 0;
+    }
+    return v;
+}
+
 static int backward(const GradState& g, const WS& w, const float* theta, int S, int dropout,
                     hipStream_t st, EpochRows* er) {
     constexpr int ALL = 0x7fffffff;
@@ -499,54 +552,56 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     else
         RC((linear_dgrad<4, 4, 2, 2>(w.dh1, theta + P_OFF[12], w.gy, w.d3, s25, S, 512, 9408, st,
                                      K_L1D)));
-    // ---- pool3 backward -> dz6 (a6 buffer: conv6 fwd no longer writes it) ----
+    // ---- pool3 backward -> dz6 (a6 buffer: conv6 fwd no longer writes it), split ----
     // Row/column 14 of conv6's 15x15 output is never pooled (floor mode), so its dz is zero: dz6
     // is stored compact as [S][14][14][192].  The weight gradient then runs over those rows as
     // they stand, and the data gradient reads the missing 15th row/column as zero padding.
-    RC((pool_scatter<14, 14, 192, true>(w.gy, w.i3, w.a6, S, st)));
-    float* dz6 = w.a6;
-    // ---- conv6: wgrad (input a5), bias, dgrad -> dz5 = . * (a5 > 0) into gx ----
+    RC((pool_scatter_nchw_xs<14, 14, 192>(w.gy, w.i3, w.a6, w.a6l, S, st)));
+    const XsT dz6 = w.x(w.a6, w.a6l), dz5 = w.x(w.gx, w.gxl), dz4 = w.x(w.a4, w.a4l);
+    const XsT dz3 = w.x(w.gx, w.gxl), dz2 = w.x(w.a2, w.a2l);
+    // ---- conv6: wgrad (input a5), bias, dgrad -> dz5 = . * (a5 > 0) into gx (split) ----
     RC(fork());
-    RC((conv_wgrad_sz<13, 13, 192, 2, 6, 3, 2, 2, 3, 3, 2, 2, 14, true, true>(
-        dz6, w.a5, S, 192, 1728, g.sw[5], g.sb[5], GEO[5].ZW, sw, K_WG6, 1728, zi(5), &zu[5])));
-    RC((conv_x6<14, 14, 192, 0, 4, 6, 4, 2, 13>(dz6, S, g.wd[5], 192, 1728,
-        EpiMask<true>{w.gx, w.a5, S * 13 * 13, 192}, st, K_DG6, 1728)));
-    float* dz5 = w.gx;
+    RC((conv_wgrad_sz<13, 13, 192, 2, 6, 3, 2, 2, 3, 3, 2, 2, 14, true, true, XsSrc>(
+        dz6.hm, w.a5, S, 192, 1728, g.sw[5], g.sb[5], GEO[5].ZW, sw, K_WG6, 1728, zi(5), &zu[5],
+        dz6.l, w.a5l)));
+    RC((dx6<14, 14, 192, 0, 6, false, 13>(dz6, S, g.wdx[5], 192, 1728,
+        EpiMaskXs<192, true>{dz5.hm, dz5.l, w.a5, S * 13 * 13}, st, K_DG6, 1728)));
+    if (debug_stop() == 6) return join();         // (debug: dz5 stays in gx / gxl)
     // ---- conv5: wgrad (input d2), bias, dgrad -> grad wrt d2 (dropout site 2), scattered through
-    //      pool2 straight into dz4 (a4 buffer; EpiDropScatterRows, no gy round trip) ----
+    //      pool2 straight into dz4 (a4 buffer, split; no gy round trip) ----
     RC(fork());
-    RC((conv_wgrad_sz<11, 11, 96, 2, 6, 3, 2, 2, 3, 3, 2, 2, 0, false, true>(
-        dz5, w.d2, S, 192, 864, g.sw[4], g.sb[4], GEO[4].ZW, sw, K_WG5, 864, zi(4), &zu[4])));
-    RC((conv_x6<13, 13, 192, 0, 4, 3, 4, 2>(dz5, S, g.wd[4], 96, 1728,
-        EpiDropScatterRows<11, 11, 96, 0>{w.a4, w.d2, w.i2, s25, S * 11 * 11}, st, K_DG5, 1728)));
-    float* dz4 = w.a4;
-    // ---- conv4: wgrad (input a3), bias, dgrad -> dz3 = . * (a3 > 0) into gx ----
+    RC((conv_wgrad_sz<11, 11, 96, 2, 6, 3, 2, 2, 3, 3, 2, 2, 0, false, true, XsSrc>(
+        dz5.hm, w.d2, S, 192, 864, g.sw[4], g.sb[4], GEO[4].ZW, sw, K_WG5, 864, zi(4), &zu[4],
+        dz5.l, w.d2l)));
+    RC((dx6<13, 13, 192, 0, 6, false, 0>(dz5, S, g.wdx[4], 96, 1728,
+        EpiDropScatterXs<11, 11, 96>{dz4.hm, dz4.l, w.d2, w.i2, s25, S * 11 * 11}, st, K_DG5,
+        1728)));
+    // ---- conv4: wgrad (input a3), bias, dgrad -> dz3 = . * (a3 > 0) into gx (split) ----
     RC(join());                                   // conv5's wgrad reads gx = dz5: done first
     RC(fork());
-    RC((conv_wgrad<20, 20, 96, 2, 3, 3, 2, 2, 0, false, true>(
-        dz4, w.a3, S, 96, 864, g.sw[3], g.sb[3], GEO[3].ZW, sw, K_WG4, 864, zi(3), &zu[3])));
-    // (fp32 direct kernel: the split-bf16 256x96 tile measured 8.21 vs 7.99 ms, profiles/r03z)
-    RC((conv_direct<22, 22, 96, 0, 2, 6, 8, 3, 2, false, 0>(dz4, S, g.wd[3], 96, 864,
-        EpiMask<true>{w.gx, w.a3, S * 20 * 20, 96}, st, K_DG4, 864)));
-    float* dz3 = w.gx;
+    RC((conv_wgrad<20, 20, 96, 2, 3, 3, 2, 2, 0, false, true, XsSrc>(
+        dz4.hm, w.a3, S, 96, 864, g.sw[3], g.sb[3], GEO[3].ZW, sw, K_WG4, 864, zi(3), &zu[3],
+        dz4.l, w.a3l)));
+    RC((dx6<22, 22, 96, 0, 6, false, 0>(dz4, S, g.wdx[3], 96, 864,
+        EpiMaskXs<96, true>{dz3.hm, dz3.l, w.a3, S * 20 * 20}, st, K_DG4, 864)));
     // ---- conv3: wgrad (input d1), bias, dgrad -> grad wrt d1 (site 1), scattered through pool1
-    //      straight into dz2 (a2 buffer) ----
+    //      straight into dz2 (a2 buffer, split) ----
     RC(fork());
-    RC((conv_wgrad_sz<18, 18, 48, 2, 3, 3, 2, 1, 3, 3, 2, 2, 0, false, true>(
-        dz3, w.d1, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW, sw, K_WG3, 432, zi(2), &zu[2])));
-    // (gemm_kernel: the direct-A form measured 3.87 vs 3.78 ms with this staged epilogue, r03b,
-    // 3.97 vs 3.77 with the batched epilogue loads, profiles/r03t/r03q_dg3; the split-bf16 512x48
-    // tile 3.82 vs 3.74, profiles/r03z)
-    RC((conv_like_sz<20, 20, 96, 0, 4, 2, 3, 4, 1>(dz3, S, g.wd[2], 48, 864,
-        EpiDropScatterRows<18, 18, 48>{w.a2, w.d1, w.i1, s25, S * 18 * 18}, st, K_DG3, 864)));
-    float* dz2 = w.a2;
-    // ---- conv2: wgrad (input a1), bias, dgrad -> dz1 = . * (a1 > 0) into gx ----
+    RC((conv_wgrad_sz<18, 18, 48, 2, 3, 3, 2, 1, 3, 3, 2, 2, 0, false, true, XsSrc>(
+        dz3.hm, w.d1, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW, sw, K_WG3, 432, zi(2), &zu[2],
+        dz3.l, w.d1l)));
+    RC((dx6<20, 20, 96, 0, 3, false, 0>(dz3, S, g.wdx[2], 48, 864,
+        EpiDropScatterXs<18, 18, 48>{dz2.hm, dz2.l, w.d1, w.i1, s25, S * 18 * 18}, st, K_DG3,
+        864)));
+    // ---- conv2: wgrad (input a1), bias, dgrad -> dz1 = . * (a1 > 0) into gx (fp32: conv1's
+    //      weight gradient is an fp32 GEMM) ----
     RC(join());                                   // conv3's wgrad reads gx = dz3: done first
     RC(fork());
-    RC((conv_wgrad_sz<34, 34, 48, 2, 3, 3, 1, 3, 3, 3, 1, 3, 0, false, true>(
-        dz2, w.a1, S, 48, 432, g.sw[1], g.sb[1], GEO[1].ZW, sw, K_WG2, 432, zi(1), &zu[1])));
-    RC((conv_direct_sz<36, 36, 48, 0, 2, 1, 3, 8, 3, 2, false, 0>(dz2, S, g.wd[1], 48, 432,
-        EpiMaskRows<48>{w.gx, w.a1, S * 34 * 34}, st, K_DG2, 432)));
+    RC((conv_wgrad_sz<34, 34, 48, 2, 3, 3, 1, 3, 3, 3, 1, 3, 0, false, true, XsSrc>(
+        dz2.hm, w.a1, S, 48, 432, g.sw[1], g.sb[1], GEO[1].ZW, sw, K_WG2, 432, zi(1), &zu[1],
+        dz2.l, w.a1l)));
+    RC((dx6<36, 36, 48, 0, 3, false, 0>(dz2, S, g.wdx[1], 48, 432,
+        EpiMaskXs<48, false>{w.gx, nullptr, w.a1, S * 34 * 34}, st, K_DG2, 432)));
     float* dz1 = w.gx;
     // ---- conv1: wgrad (input x0), bias ----
     // (3 waves of 16 rows each: 0.272 vs 0.325 ms for one 48x48 wave, profiles/r01c/lab_conv1.txt)
@@ -581,10 +636,27 @@ int flsim_pn1_workspace_offset(int which, int samples, long* offset_bytes) {
     WS w = ws_layout(fake, samples);
     const void* p[] = {w.x0, w.a1, w.a2, w.d1, w.a3, w.a4, w.d2, w.a5, w.a6, w.d3,
                        w.e1, w.e2, w.dh1, w.dh2, w.gx, w.gy, w.loss_s, w.dlog, w.y,
-                       w.i1, w.i2, w.i3};
+                       w.i1, w.i2, w.i3,
+                       w.a1l, w.d1l, w.a3l, w.d2l, w.a5l, w.a6l, w.a4l, w.a2l, w.gxl};
     FLSIM_REQUIRE(which >= 0 && which < (int)(sizeof(p) / sizeof(p[0])), "bad workspace id %d", which);
     *offset_bytes = (long)((const char*)p[which] - fake);
     return 0;
+}
+
+// a workspace tensor held in the split-bf16 form (split.h): the id of its L part (its HM part is
+// `which` itself), or -1 for an fp32 tensor.  gx is fp32 after a backward pass (dz1).
+int flsim_pn1_workspace_split_part(int which) {
+    switch (which) {
+        case 1: return 22;     // a1
+        case 3: return 23;     // d1
+        case 4: return 24;     // a3
+        case 6: return 25;     // d2
+        case 7: return 26;     // a5
+        case 8: return 27;     // dz6 (a6 buffer)
+        case 5: return 28;     // dz4 (a4 buffer)
+        case 2: return 29;     // dz2 (a2 buffer)
+        default: return -1;
+    }
 }
 
 int flsim_pn1_begin_epoch(void* gradstate, const float* theta, hipStream_t stream) {

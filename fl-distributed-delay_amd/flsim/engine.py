@@ -220,14 +220,39 @@ class NetEngine:
             ptr(self.gradstate), ptr(S_out), ctypes.byref(rule.c_rule), ptr(theta), ptr(m), ptr(v),
             int(step), float(lr), float(betas[0]), float(betas[1]), float(eps), stream_ptr()))
 
-    def workspace_view(self, which, shape, dtype=torch.float32, samples=None):
-        """Debug view of a workspace tensor by id (PN1Engine.WORKSPACE / VGG11Engine.WORKSPACE)."""
+    def _workspace_bytes_at(self, which, n):
         off = ctypes.c_long()
         check(self._fn("workspace_offset")(which, self.max_samples, ctypes.byref(off)))
-        n = int(np.prod(shape)) * torch.tensor([], dtype=dtype).element_size()
         ws = getattr(self, "last_workspace", None)      # the last pass's (pipelined: alternating)
         ws = self.workspace if ws is None else ws
-        return ws[off.value:off.value + n].view(dtype).view(shape)
+        return ws[off.value:off.value + n]
+
+    def workspace_view(self, which, shape, dtype=torch.float32, samples=None):
+        """Debug view of a workspace tensor by id (PN1Engine.WORKSPACE / VGG11Engine.WORKSPACE).
+        A tensor the engine stores in the split-bf16 form (HM + L parts, csrc/split.h) comes back
+        as its fp32 values, (h + m) + l, which is exact: a copy, not a view."""
+        n = int(np.prod(shape)) * torch.tensor([], dtype=dtype).element_size()
+        lpart = self.split_part(which)
+        if lpart < 0 or dtype != torch.float32:
+            return self._workspace_bytes_at(which, n).view(dtype).view(shape)
+        units = int(np.prod(shape)) // 4
+        hm = self._workspace_bytes_at(which, n).view(torch.int16).view(units, 2, 4)
+        lo = self._workspace_bytes_at(lpart, n // 2).view(torch.int16).view(units, 4)
+
+        def f32(b):         # bf16 bits -> fp32 (exact)
+            return (b.to(torch.int32) << 16).view(torch.float32)
+        return ((f32(hm[:, 0]) + f32(hm[:, 1])) + f32(lo)).view(shape)
+
+    def split_part(self, which):
+        """Workspace id of tensor `which`'s L part when it is stored split, else -1."""
+        fn = getattr(self, "_split_fn", None)
+        if fn is None:
+            try:
+                fn = self._fn("workspace_split_part")
+            except AttributeError:
+                fn = lambda w: -1      # noqa: E731  (networks whose tensors are all fp32)
+            self._split_fn = fn
+        return int(fn(which))
 
     # -- server step ------------------------------------------------------------------------------
     def aggregate_adam(self, S, c, stale, theta, m, v, step, lr=1e-3, betas=(0.9, 0.999),

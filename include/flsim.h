@@ -68,6 +68,9 @@ long flsim_pn1_param_count(void);
 long flsim_pn1_gradstate_bytes(void);
 long flsim_pn1_workspace_bytes(int max_samples);
 int flsim_pn1_workspace_offset(int which, int samples, long* offset_bytes);
+/* (debug / tests) the tensors that feed the split-bf16 GEMMs are stored split (HM + L parts,
+ * DESIGN 6g): the workspace id of tensor `which`'s L part, or -1 when it is stored fp32 */
+int flsim_pn1_workspace_split_part(int which);
 /* packs theta_t into the kernel layouts and zeroes the slabs (start of main.py:126 epoch) */
 int flsim_pn1_begin_epoch(void* gradstate, const float* theta, flsim_stream_t stream);
 /* workers: device array of n_chunk_workers WorkerRec; worker_loss: device float per worker

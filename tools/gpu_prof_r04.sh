@@ -22,7 +22,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/t
     -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-stream > $OUT/trace.log 2>&1 \
     || { echo "trace failed $?"; tail -5 $OUT/trace.log; exit 1; }
 echo "trace ok"
-KREGEX="gemm_kernel|gemm_x6_kernel|gemm_direct_kernel|k_conv1_fwd|k_slab_step|k_pool_scatter"
+KREGEX="gemm_kernel|gemm_x6_kernel|gemm_dx6_kernel|gemm_direct_kernel|k_conv1_fwd|k_slab_step|k_pool_scatter"
 PASSES=(
   "FETCH_SIZE"
   "WRITE_SIZE"

@@ -74,7 +74,8 @@ def read(path, counter):
             name = probe_name(r["Kernel_Name"])
             if name is None:
                 continue
-            maths[name] = "bf16x6" if "gemm_x6_kernel" in r["Kernel_Name"] else "fp32"
+            maths[name] = ("bf16x6" if "gemm_x6_kernel" in r["Kernel_Name"] or
+                           "gemm_dx6_kernel" in r["Kernel_Name"] else "fp32")
             out.setdefault(name, []).append(float(r["Counter_Value"]))
     return out
 
