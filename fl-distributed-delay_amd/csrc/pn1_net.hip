@@ -320,6 +320,20 @@ static int dx6(XsT X, int S, XsT W, int N, int KP, const EPI& epi, hipStream_t s
         X, S, W, N, KP, epi, st, kid, kreal);
 }
 
+// The same GEMMs on gemm_x6_kernel with both operands staged through LDS (conv_xs; bit-identical
+// to conv_dx6): WM x WN waves of 16*FM x 16*FN, FM halved for small chunks.  The wide layers
+// (N = 192: conv5/6 forward, conv6 data gradient; N = 96 data gradients of conv4/5) run faster
+// this way (profiles/r04b/lab_xs.txt: conv6 data gradient 8.8 vs 10.7 ms, forward 11.1 vs 12.0)
+template <int IH, int IW, int CI, int PAD, int FM, int FN, int WM, int WN, bool WIN, int OHX,
+          class EPI>
+static int xs(XsT X, int S, XsT W, int N, int KP, const EPI& epi, hipStream_t st, int kid,
+              int kreal) {
+    if (S <= small_chunk_samples())
+        return conv_xs<IH, IW, CI, PAD, FM / 2, FN, WM, WN, WIN, OHX>(X, S, W, N, KP, epi, st, kid,
+                                                                     kreal);
+    return conv_xs<IH, IW, CI, PAD, FM, FN, WM, WN, WIN, OHX>(X, S, W, N, KP, epi, st, kid, kreal);
+}
+
 static int forward(const GradState& g, const WS& w, const float* theta, int S,
                    const WorkerRec* workers, uint64_t seed, int dropout, hipStream_t st) {
     const XsT a1 = w.x(w.a1, w.a1l), d1 = w.x(w.d1, w.d1l), a3 = w.x(w.a3, w.a3l);
@@ -337,13 +351,13 @@ static int forward(const GradState& g, const WS& w, const float* theta, int S,
     RC((dx6<20, 20, 96, 2, 6, true, 0>(a3, S, g.wfx[3], 96, 864,
         EpiPoolDropXs<11, 11, 96>{d2.hm, d2.l, w.i2, theta + P_OFF[7], workers, seed, SITE_DROP2,
                                   THR_P25, SCALE_P25, dropout, S * 11 * 11 * 4}, st, K_FWD4, 864)));
-    // conv5 + ReLU (models.py:37) -> a5 (split; two 96-column n-tiles)
-    RC((dx6<11, 11, 96, 2, 6, false, 0>(d2, S, g.wfx[4], 192, 864,
+    // conv5 + ReLU (models.py:37) -> a5 (split)
+    RC((xs<11, 11, 96, 2, 4, 6, 4, 2, false, 0>(d2, S, g.wfx[4], 192, 864,
         EpiBiasReluXs<192>{a5.hm, a5.l, theta + P_OFF[9], S * 13 * 13}, st, K_FWD5, 864)));
     // conv6 + ReLU + pool3 + dropout1 (models.py:38-40), written fp32 in torch's flatten order
     // (models.py:41) so linear1 keeps the torch weight layout; the floor-mode border row/column
     // of the 15x15 output (dropped by the pool) is never computed
-    RC((dx6<13, 13, 192, 2, 6, true, 0>(a5, S, g.wfx[5], 192, 1728,
+    RC((xs<13, 13, 192, 2, 4, 6, 4, 2, true, 0>(a5, S, g.wfx[5], 192, 1728,
         EpiPoolDrop<7, 7, 192, true>{w.d3, w.i3, theta + P_OFF[11], workers, seed, SITE_DROP3,
                                      THR_P25, SCALE_P25, dropout, S * 7 * 7 * 4}, st, K_FWD6,
         1728)));
@@ -564,7 +578,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC((conv_wgrad_sz<13, 13, 192, 2, 6, 3, 2, 2, 3, 3, 2, 2, 14, true, true, XsSrc>(
         dz6.hm, w.a5, S, 192, 1728, g.sw[5], g.sb[5], GEO[5].ZW, sw, K_WG6, 1728, zi(5), &zu[5],
         dz6.l, w.a5l)));
-    RC((dx6<14, 14, 192, 0, 6, false, 13>(dz6, S, g.wdx[5], 192, 1728,
+    RC((xs<14, 14, 192, 0, 4, 6, 4, 2, false, 13>(dz6, S, g.wdx[5], 192, 1728,
         EpiMaskXs<192, true>{dz5.hm, dz5.l, w.a5, S * 13 * 13}, st, K_DG6, 1728)));
     if (debug_stop() == 6) return join();         // (debug: dz5 stays in gx / gxl)
     // ---- conv5: wgrad (input d2), bias, dgrad -> grad wrt d2 (dropout site 2), scattered through
@@ -573,7 +587,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC((conv_wgrad_sz<11, 11, 96, 2, 6, 3, 2, 2, 3, 3, 2, 2, 0, false, true, XsSrc>(
         dz5.hm, w.d2, S, 192, 864, g.sw[4], g.sb[4], GEO[4].ZW, sw, K_WG5, 864, zi(4), &zu[4],
         dz5.l, w.d2l)));
-    RC((dx6<13, 13, 192, 0, 6, false, 0>(dz5, S, g.wdx[4], 96, 1728,
+    RC((xs<13, 13, 192, 0, 4, 3, 4, 2, false, 0>(dz5, S, g.wdx[4], 96, 1728,
         EpiDropScatterXs<11, 11, 96>{dz4.hm, dz4.l, w.d2, w.i2, s25, S * 11 * 11}, st, K_DG5,
         1728)));
     // ---- conv4: wgrad (input a3), bias, dgrad -> dz3 = . * (a3 > 0) into gx (split) ----
@@ -582,7 +596,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC((conv_wgrad<20, 20, 96, 2, 3, 3, 2, 2, 0, false, true, XsSrc>(
         dz4.hm, w.a3, S, 96, 864, g.sw[3], g.sb[3], GEO[3].ZW, sw, K_WG4, 864, zi(3), &zu[3],
         dz4.l, w.a3l)));
-    RC((dx6<22, 22, 96, 0, 6, false, 0>(dz4, S, g.wdx[3], 96, 864,
+    RC((xs<22, 22, 96, 0, 4, 3, 4, 2, false, 0>(dz4, S, g.wdx[3], 96, 864,
         EpiMaskXs<96, true>{dz3.hm, dz3.l, w.a3, S * 20 * 20}, st, K_DG4, 864)));
     // ---- conv3: wgrad (input d1), bias, dgrad -> grad wrt d1 (site 1), scattered through pool1
     //      straight into dz2 (a2 buffer, split) ----

@@ -9,7 +9,7 @@
     O(lr) parameter moves, so the GPU's distance from fp64 is bounded by a stated
     multiple of the CPU fp32 port's own distance from fp64, in loss and in parameters (JL sketch);
   * configs[4]'s launch size for vgg11: a 128-worker chunk (16,384 samples) against 32-worker
-    chunks.
+    chunks, and configs[4] at its own size (n = 4096, delay 1000) across the first tick.
 """
 import numpy as np
 import pytest
@@ -221,6 +221,62 @@ def test_n1024_d500_crosses_first_tick(pool, golden):
         assert pl.c_t == ref_c[t], t
         assert [s for (_, s) in pl.stale] == ([int(ref_stale[t])] if ref_stale[t] >= 0 else []), t
     assert np.isfinite(l500) and np.isfinite(l501)
+
+
+def test_vgg11_n4096_d1000_crosses_first_tick(pool):
+    """configs[4] at its own size (vgg11, n = 4096, delay 1000, --throttle): a synthetic
+    checkpoint at t = 999 (main.py:119's FIFO holding S_0, refcount 1) is restored and epochs
+    999-1001 run: the staleness trace equals the oracle's schedule scan (O.schedule, pinned to the
+    reference's own loop by tests/golden/schedule.npz) bit for bit, the tick's rule() + Adam over
+    [S_1000] * c + [S_0] at P = 9,750,922 equals the oracle's cascade + Adam bit for bit
+    (main.py:23-25, agents.py:9-21), the slot of t = 0 is released and t = 1000 holds S_1000, and
+    the 4,095-worker epoch after it runs (every fast worker computes, models.py:101-103 vgg11)."""
+    from flsim.engine import VGG11_SIZES
+    from flsim.sim import CKPT_FORMAT, FLSimulation, default_theta
+    from oracle import oracle as O
+    n, d = 4096, 1000
+    ref = O.schedule(n, O.reference_delays(n, d), True, d + 2)
+    kw = dict(delay=d, throttle=True, device=DEV, pool=pool, model="vgg11", keep_S=True)
+    sim = FLSimulation(n, **kw)
+    P = sim.P
+    assert P == 9_750_922
+    g = torch.Generator().manual_seed(11)
+    S0 = torch.randn(P, generator=g) * 1e-3
+    ck = dict(sim.checkpoint(), epoch=d - 1, step=d - 1, theta=default_theta(0, "vgg11"),
+              m=torch.randn(P, generator=g) * 1e-4, v=torch.rand(P, generator=g) * 1e-6,
+              stale={0: (S0, 1)}, loss_log=[float("nan")] * (d - 1), buffers={})
+    assert ck["format"] == CKPT_FORMAT
+    sim = FLSimulation(n, **kw)
+    sim.restore(ck)
+    sim.epoch()                                            # t = 999
+    p = sim.theta[:P].cpu().numpy().copy()
+    m = sim.m[:P].cpu().numpy().copy()
+    v = sim.v[:P].cpu().numpy().copy()
+    l_tick = sim.epoch()                                   # t = 1000: the tick
+    S = sim.comm[:P].cpu().numpy()
+    plan = sim.trace[d]
+    assert plan.stale == [(n - 1, 0)] and plan.pushed and plan.c_t == int(ref.c_t[d])
+    assert sorted(sim.stale_store) == [d] and sim.stale_store[d][1] == 1
+    assert torch.equal(sim.stale_store[d][0][:P].cpu(), torch.from_numpy(S))
+    gm = np.empty_like(S)
+    off = 0
+    for size in VGG11_SIZES:
+        gm[off:off + size] = O.cascade_mean([S[off:off + size]] * plan.c_t +
+                                            [S0.numpy()[off:off + size]])
+        off += size
+    assert sim.step == d + 1                               # Adam steps: 999 restored + 2
+    O.adam_step(p, m, v, gm, sim.step)
+    for name, x, y in (("p", sim.theta, p), ("m", sim.m, m), ("v", sim.v, v)):
+        assert np.array_equal(x[:P].cpu().numpy().view(np.uint32), y.view(np.uint32)), name
+    l_after = sim.epoch()                                  # t = 1001: every fast worker
+    assert int(sim.trace[d + 1].computes.sum()) == n - 1
+    for t in (d - 1, d, d + 1):
+        pl = sim.trace[t]
+        assert np.array_equal(pl.computes, ref.computes[t]), t
+        assert pl.c_t == int(ref.c_t[t]), t
+        assert [s for (_, s) in pl.stale] == \
+            [int(x) for x in ref.stale_src[t][ref.stale_src[t] >= 0]], t
+    assert np.isfinite(l_tick) and np.isfinite(l_after)
 
 
 def test_configs3_heterogeneous_full_size(pool):
