@@ -95,15 +95,16 @@ struct EpiMaskXs {
 
 // EpiDropScatterRows (loaders.h) over split tensors: the masked, scaled gradient of pooled element
 // (m, n) goes to its argmax position of the 2x2 window in the full-resolution dZ, zeros elsewhere;
-// act (the pooled, dropped activation) is split, dZ is written split.  Full rows (BN == NC).
-template <int PH, int PW, int NC>
+// act (the pooled, dropped activation) is split, dZ is written split (OUT_XS) or fp32.  Full rows
+// (BN == NC).
+template <int PH, int PW, int NC, bool OUT_XS = true>
 struct EpiDropScatterXs {
     static constexpr bool ASUM = false;
     static constexpr bool STAGED = true;
     static constexpr int NCOL = NC;
     static_assert(NC % 4 == 0, "float4 rows");
-    float* dZhm;
-    float* dZl;
+    float* dZhm;          // HM part (OUT_XS) or the fp32 dZ
+    float* dZl;           // L part (OUT_XS)
     const float* act;     // HM part
     const uint8_t* idx;
     float scale;
@@ -151,7 +152,11 @@ struct EpiDropScatterXs {
             o.y = ((id >> 8) & 0xffu) == (uint32_t)pos ? g.y : 0.f;
             o.z = ((id >> 16) & 0xffu) == (uint32_t)pos ? g.z : 0.f;
             o.w = (id >> 24) == (uint32_t)pos ? g.w : 0.f;
-            xs_store(dZhm, dZl, u0 + ((pos >> 1) * (2 * PW) + (pos & 1)) * (long)N4, o);
+            const long u = u0 + ((pos >> 1) * (2 * PW) + (pos & 1)) * (long)N4;
+            if constexpr (OUT_XS)
+                xs_store(dZhm, dZl, u, o);
+            else
+                st_nt4(dZhm + 4 * u, o);
         }
     }
 };

@@ -254,7 +254,8 @@ gemm_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, int t
         if (tn == 0 && tid < BM) epi.asum(m0 + tid, tz, asum);
     }
     if constexpr (STAGED) {
-        static_assert(BN == EPI::NCOL, "staged epilogue needs the full row in one block");
+        static_assert(BN == EPI::NCOL || (IsPartial<EPI>::value && EPI::NCOL % BN == 0),
+                      "staged epilogue needs the full row in one block");
         constexpr int PASSES = (WAVES_M + WM_PASS - 1) / WM_PASS;
 #pragma unroll 1
         for (int pass = 0; pass < PASSES; ++pass) {
@@ -273,8 +274,8 @@ gemm_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, int t
             }
             __syncthreads();
             const int wm_hi = (pass + 1) * WM_PASS < WAVES_M ? (pass + 1) * WM_PASS : WAVES_M;
-            epi.store_rows(lds, STAGE_LD, m0 + pass * WM_PASS * WROWS,
-                           (wm_hi - pass * WM_PASS) * WROWS, tid, 64 * WAVES_M * WAVES_N);
+            staged_store(epi, lds, STAGE_LD, m0 + pass * WM_PASS * WROWS,
+                         (wm_hi - pass * WM_PASS) * WROWS, n0, BN, tid, 64 * WAVES_M * WAVES_N);
         }
     } else if constexpr (HasPre<EPI>::value) {
         // one fragment row at a time: its FN fragments' inputs are loaded before any is stored

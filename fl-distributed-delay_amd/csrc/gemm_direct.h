@@ -220,7 +220,8 @@ gemm_direct_kernel(AD ad, BL bl, EPI epi, int ksteps, int tiles_m, int tiles_n) 
     }
 
     if constexpr (STAGED) {
-        static_assert(BN == EPI::NCOL, "staged epilogue needs the full row in one block");
+        static_assert(BN == EPI::NCOL || (IsPartial<EPI>::value && EPI::NCOL % BN == 0),
+                      "staged epilogue needs the full row in one block");
         constexpr int PASSES = (WAVES + WM_PASS - 1) / WM_PASS;
 #pragma unroll 1
         for (int pass = 0; pass < PASSES; ++pass) {
@@ -239,8 +240,8 @@ gemm_direct_kernel(AD ad, BL bl, EPI epi, int ksteps, int tiles_m, int tiles_n) 
             }
             __syncthreads();
             const int w_hi = (pass + 1) * WM_PASS < WAVES ? (pass + 1) * WM_PASS : WAVES;
-            epi.store_rows(lds, STAGE_LD, m0 + pass * WM_PASS * WROWS,
-                           (w_hi - pass * WM_PASS) * WROWS, tid, 64 * WAVES);
+            staged_store(epi, lds, STAGE_LD, m0 + pass * WM_PASS * WROWS,
+                         (w_hi - pass * WM_PASS) * WROWS, n0, BN, tid, 64 * WAVES);
         }
     } else {
 #pragma unroll

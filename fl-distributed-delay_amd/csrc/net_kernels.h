@@ -898,9 +898,10 @@ static int conv_like_sz(const float* X, int S, const float* Wpk, int N, int KP, 
 // VO > 0: only the top-left VO x VO window of the output pixels (dz is zero outside it)
 // DZC: dz is already stored compact over that window ([S][VO][VO][CO]), so its rows are the
 // reduction index as they stand
-// SRC = XsSrc: dz and X in the split form (dzl, Xl their L parts; X6 only)
+// SRC = XsSrc: dz (and X, unless SRCB says otherwise) in the split form (dzl, Xl their L parts;
+// X6 only)
 template <int IH, int IW, int CI, int PAD, int FM, int FN, int WM, int WN, int VO = 0,
-          bool DZC = false, bool X6 = false, class SRC = BufSrc>
+          bool DZC = false, bool X6 = false, class SRC = BufSrc, class SRCB = SRC>
 static int conv_wgrad(const float* dz, const float* X, int S, int CO, int KP, float* slab,
                       float* bslab, int Z, hipStream_t st, int kid, int kreal,
                       int zinit = 0x7fffffff, int* zused = nullptr, const float* dzl = nullptr,
@@ -909,9 +910,9 @@ static int conv_wgrad(const float* dz, const float* X, int S, int CO, int KP, fl
     constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
     constexpr int OFULL = IH + 2 * PAD - 2;
     static_assert(IH == IW && VO <= OFULL, "square maps only");
-    static_assert(X6 || !SRC::SPLIT, "split operands run on the split-bf16 GEMM");
+    static_assert(X6 || (!SRC::SPLIT && !SRCB::SPLIT), "split operands run on the split-bf16 GEMM");
     using AL = RowsKM<BM, NT, (VO > 0 && !DZC ? OFULL : 0), (DZC ? 0 : VO), SRC>;
-    using BL = Im2colKM<IH, IW, CI, PAD, BN, NT, VO, SRC>;
+    using BL = Im2colKM<IH, IW, CI, PAD, BN, NT, VO, SRCB>;
     const int M = S * BL::OH * BL::OW;
     AL al;
     al.P = dz;
@@ -941,14 +942,15 @@ static int conv_wgrad(const float* dz, const float* X, int S, int CO, int KP, fl
 // (profiles/r03f/lab_s640_wgrad.txt: at 640 samples 96x96 4-wave tiles beat the 128-worker
 // chunk's larger ones on conv3/5/6 by 3-10 %, 48x144 beats 48x48 on conv2 by 4 %)
 template <int IH, int IW, int CI, int PAD, int FM, int FN, int WM, int WN, int FMS, int FNS,
-          int WMS, int WNS, int VO = 0, bool DZC = false, bool X6 = false, class SRC = BufSrc>
+          int WMS, int WNS, int VO = 0, bool DZC = false, bool X6 = false, class SRC = BufSrc,
+          class SRCB = SRC>
 static int conv_wgrad_sz(const float* dz, const float* X, int S, int CO, int KP, float* slab,
                          float* bslab, int Z, hipStream_t st, int kid, int kreal, int zinit,
                          int* zused, const float* dzl = nullptr, const float* Xl = nullptr) {
     if (S <= small_chunk_samples())
-        return conv_wgrad<IH, IW, CI, PAD, FMS, FNS, WMS, WNS, VO, DZC, X6, SRC>(
+        return conv_wgrad<IH, IW, CI, PAD, FMS, FNS, WMS, WNS, VO, DZC, X6, SRC, SRCB>(
             dz, X, S, CO, KP, slab, bslab, Z, st, kid, kreal, zinit, zused, dzl, Xl);
-    return conv_wgrad<IH, IW, CI, PAD, FM, FN, WM, WN, VO, DZC, X6, SRC>(
+    return conv_wgrad<IH, IW, CI, PAD, FM, FN, WM, WN, VO, DZC, X6, SRC, SRCB>(
         dz, X, S, CO, KP, slab, bslab, Z, st, kid, kreal, zinit, zused, dzl, Xl);
 }
 

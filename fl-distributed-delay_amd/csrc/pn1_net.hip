@@ -66,7 +66,7 @@ constexpr int ZH = 32;      // head wgrad split
 // gradient-state layout (floats): packed weights + slabs
 struct GradState {
     float* wf[6];  // conv1's fp32 packing (wf[1..5] unused)
-    float* wd[6];  // unused
+    float* wd[6];  // fp32 data-gradient packings of conv2 / conv3 (wd[1], wd[2]; the rest unused)
     XsT wfx[6];    // conv2-6 forward packings, split (wfx[0] unused)
     XsT wdx[6];    // conv2-6 data-gradient packings, split (wdx[0] unused)
     float* sw[6];  // conv weight slabs [ZW][CO][KP]
@@ -115,7 +115,7 @@ static GradState gs_layout(float* base_in) {
     };
     for (int l = 0; l < 6; ++l) {
         g.wf[l] = l ? nullptr : take((long)GEO[l].CO * GEO[l].KP);
-        g.wd[l] = nullptr;
+        g.wd[l] = (l == 1 || l == 2) ? take((long)GEO[l].CI * 9 * GEO[l].CO) : nullptr;
         g.wfx[l] = g.wdx[l] = XsT{nullptr, nullptr};
         if (l) {
             const long nf = (long)GEO[l].CO * GEO[l].KP, nd = (long)GEO[l].CI * 9 * GEO[l].CO;
@@ -156,7 +156,7 @@ struct WS {
     float* gx; float* gy; float* loss_s; float* dlog; int32_t* y;
     uint8_t* i1; uint8_t* i2; uint8_t* i3;
     float* a1l; float* d1l; float* a3l; float* d2l; float* a5l;     // forward split tensors
-    float* a6l; float* a4l; float* a2l; float* gxl;                  // dz6, dz4, dz2, dz5 / dz3
+    float* a6l; float* a4l; float* a2l; float* gxl;                  // dz6, dz4, -, dz5
     long bytes;
     XsT x(float* hm, float* l) const { return XsT{hm, l}; }
 };
@@ -179,8 +179,9 @@ static WS ws_layout(char* base, int S) {
     w.i1 = (uint8_t*)take(15552L * S); w.i2 = (uint8_t*)take(11616L * S);
     w.i3 = (uint8_t*)take(9408L * S);
     w.a1l = tf(55488 / 2); w.d1l = tf(15552 / 2); w.a3l = tf(38400 / 2); w.d2l = tf(11616 / 2);
-    w.a5l = tf(32448 / 2); w.a6l = tf(43200 / 2); w.a4l = tf(46464 / 2); w.a2l = tf(62208 / 2);
-    w.gxl = tf(38400 / 2);
+    w.a5l = tf(32448 / 2); w.a6l = tf(43200 / 2); w.a4l = tf(46464 / 2);
+    w.a2l = tf(0);         // (dz2 is fp32: id kept, no bytes)
+    w.gxl = tf(32448 / 2);
     w.bytes = o;
     return w;
 }
@@ -191,6 +192,11 @@ static int pack_weights(const GradState& g, const float* theta, hipStream_t st) 
     for (int l = 1; l < 6; ++l) {
         const ConvGeo& c = GEO[l];
         RC(pack_conv_xs(theta + P_OFF[2 * l], g.wfx[l], g.wdx[l], c.CO, c.CI, c.KP, st));
+        if (g.wd[l]) {          // conv2 / conv3: the data gradient runs on the fp32 MFMA
+            hipLaunchKernelGGL(k_pack_dgrad, dim3(ceil_div((long)c.CI * 9 * c.CO, 256)), dim3(256),
+                               0, st, theta + P_OFF[2 * l], g.wd[l], c.CO, c.CI);
+            FLSIM_LAUNCH_CHECK();
+        }
     }
     return 0;
 }
@@ -572,7 +578,6 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     // they stand, and the data gradient reads the missing 15th row/column as zero padding.
     RC((pool_scatter_nchw_xs<14, 14, 192>(w.gy, w.i3, w.a6, w.a6l, S, st)));
     const XsT dz6 = w.x(w.a6, w.a6l), dz5 = w.x(w.gx, w.gxl), dz4 = w.x(w.a4, w.a4l);
-    const XsT dz3 = w.x(w.gx, w.gxl), dz2 = w.x(w.a2, w.a2l);
     // ---- conv6: wgrad (input a5), bias, dgrad -> dz5 = . * (a5 > 0) into gx (split) ----
     RC(fork());
     RC((conv_wgrad_sz<13, 13, 192, 2, 6, 3, 2, 2, 3, 3, 2, 2, 14, true, true, XsSrc>(
@@ -590,31 +595,37 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC((xs<13, 13, 192, 0, 4, 3, 4, 2, false, 0>(dz5, S, g.wdx[4], 96, 1728,
         EpiDropScatterXs<11, 11, 96>{dz4.hm, dz4.l, w.d2, w.i2, s25, S * 11 * 11}, st, K_DG5,
         1728)));
-    // ---- conv4: wgrad (input a3), bias, dgrad -> dz3 = . * (a3 > 0) into gx (split) ----
+    // ---- conv4: wgrad (input a3), bias, dgrad -> dz3 = . * (a3 > 0) into gx (fp32) ----
+    // dz3 and dz2 stay fp32: their data gradients have N = 48 columns, where the fp32 MFMA
+    // kernels are faster than any split-bf16 form (profiles/r04b/lab_xs.txt: conv3's 3.8 ms fp32
+    // against 4.4 / 4.9 / 5.6 ms for x6 / dx6 / xs), so conv3 / conv2's weight gradients split
+    // dZ while staging (split-bf16 kernel over an fp32 dZ and a split layer input)
     RC(join());                                   // conv5's wgrad reads gx = dz5: done first
     RC(fork());
     RC((conv_wgrad<20, 20, 96, 2, 3, 3, 2, 2, 0, false, true, XsSrc>(
         dz4.hm, w.a3, S, 96, 864, g.sw[3], g.sb[3], GEO[3].ZW, sw, K_WG4, 864, zi(3), &zu[3],
         dz4.l, w.a3l)));
     RC((xs<22, 22, 96, 0, 4, 3, 4, 2, false, 0>(dz4, S, g.wdx[3], 96, 864,
-        EpiMaskXs<96, true>{dz3.hm, dz3.l, w.a3, S * 20 * 20}, st, K_DG4, 864)));
+        EpiMaskXs<96, false>{w.gx, nullptr, w.a3, S * 20 * 20}, st, K_DG4, 864)));
+    float* dz3 = w.gx;
     // ---- conv3: wgrad (input d1), bias, dgrad -> grad wrt d1 (site 1), scattered through pool1
-    //      straight into dz2 (a2 buffer, split) ----
+    //      straight into dz2 (a2 buffer, fp32) ----
     RC(fork());
-    RC((conv_wgrad_sz<18, 18, 48, 2, 3, 3, 2, 1, 3, 3, 2, 2, 0, false, true, XsSrc>(
-        dz3.hm, w.d1, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW, sw, K_WG3, 432, zi(2), &zu[2],
-        dz3.l, w.d1l)));
-    RC((dx6<20, 20, 96, 0, 3, false, 0>(dz3, S, g.wdx[2], 48, 864,
-        EpiDropScatterXs<18, 18, 48>{dz2.hm, dz2.l, w.d1, w.i1, s25, S * 18 * 18}, st, K_DG3,
-        864)));
-    // ---- conv2: wgrad (input a1), bias, dgrad -> dz1 = . * (a1 > 0) into gx (fp32: conv1's
-    //      weight gradient is an fp32 GEMM) ----
+    RC((conv_wgrad_sz<18, 18, 48, 2, 3, 3, 2, 1, 3, 3, 2, 2, 0, false, true, BufSrc, XsSrc>(
+        dz3, w.d1, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW, sw, K_WG3, 432, zi(2), &zu[2],
+        nullptr, w.d1l)));
+    // (gemm_kernel: the direct-A form measured 3.87 vs 3.78 ms with this staged epilogue, r03b)
+    RC((conv_like_sz<20, 20, 96, 0, 4, 2, 3, 4, 1>(dz3, S, g.wd[2], 48, 864,
+        EpiDropScatterXs<18, 18, 48, false>{w.a2, nullptr, w.d1, w.i1, s25, S * 18 * 18}, st,
+        K_DG3, 864)));
+    float* dz2 = w.a2;
+    // ---- conv2: wgrad (input a1), bias, dgrad -> dz1 = . * (a1 > 0) into gx (fp32) ----
     RC(join());                                   // conv3's wgrad reads gx = dz3: done first
     RC(fork());
-    RC((conv_wgrad_sz<34, 34, 48, 2, 3, 3, 1, 3, 3, 3, 1, 3, 0, false, true, XsSrc>(
-        dz2.hm, w.a1, S, 48, 432, g.sw[1], g.sb[1], GEO[1].ZW, sw, K_WG2, 432, zi(1), &zu[1],
-        dz2.l, w.a1l)));
-    RC((dx6<36, 36, 48, 0, 3, false, 0>(dz2, S, g.wdx[1], 48, 432,
+    RC((conv_wgrad_sz<34, 34, 48, 2, 3, 3, 1, 3, 3, 3, 1, 3, 0, false, true, BufSrc, XsSrc>(
+        dz2, w.a1, S, 48, 432, g.sw[1], g.sb[1], GEO[1].ZW, sw, K_WG2, 432, zi(1), &zu[1],
+        nullptr, w.a1l)));
+    RC((conv_direct_sz<36, 36, 48, 0, 2, 1, 3, 8, 3, 2, false, 0>(dz2, S, g.wd[1], 48, 432,
         EpiMaskXs<48, false>{w.gx, nullptr, w.a1, S * 34 * 34}, st, K_DG2, 432)));
     float* dz1 = w.gx;
     // ---- conv1: wgrad (input x0), bias ----
@@ -668,7 +679,6 @@ int flsim_pn1_workspace_split_part(int which) {
         case 7: return 26;     // a5
         case 8: return 27;     // dz6 (a6 buffer)
         case 5: return 28;     // dz4 (a4 buffer)
-        case 2: return 29;     // dz2 (a2 buffer)
         default: return -1;
     }
 }
