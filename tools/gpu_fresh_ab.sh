@@ -21,4 +21,6 @@ timeout -k 10 400 python3 -u bench.py --no-cpu-baseline > $OUT/bench.json 2> $OU
 python3 tools/bench_summary.py $OUT/bench.json | head -30
 timeout -k 10 300 tools/lab/xp_lab > $OUT/lab_xp.txt 2>&1 || { echo "xp lab failed $?"; tail -5 $OUT/lab_xp.txt; exit 1; }
 cat $OUT/lab_xp.txt
+timeout -k 10 300 tools/lab/xq_lab > $OUT/lab_xq.txt 2>&1 || { echo "xq lab failed $?"; tail -5 $OUT/lab_xq.txt; exit 1; }
+cat $OUT/lab_xq.txt
 bash tools/gpu_prof_r04.sh r04d || exit 1
