@@ -10,6 +10,8 @@
 // MFMAs, smallest terms first (hl, lh, hm, mh, mm, hh), summed in a fresh register and added to
 // the running accumulator once (FLSIM_X6_FRESH's rule, gemm_x6.h).
 #pragma once
+#include <type_traits>
+
 #include "gemm_x6.h"
 
 namespace flsim {
@@ -24,13 +26,13 @@ struct X6QTile {
     __device__ static int off_bytes(int row, int kq) {
         return 4 * KCTile<ROWS>::chunk_off(row, kq >> 1) + 8 * (kq & 1);
     }
-    __device__ static void store(float* s, int row, int kq, const XsUnit& v) {
+    __device__ static void store(float* s, int row, int kq, const XsUnit& v, bool = true) {
         char* b = reinterpret_cast<char*>(s) + off_bytes(row, kq);
         *reinterpret_cast<f32x2*>(b) = f32x2{v.hm.x, v.hm.y};                       // h4
         *reinterpret_cast<f32x2*>(b + 4 * PLANE) = f32x2{v.hm.z, v.hm.w};           // m4
         *reinterpret_cast<f32x2*>(b + 8 * PLANE) = v.l;                              // l4
     }
-    __device__ static void store(float* s, int row, int kq, f32x4 v) {
+    __device__ static void store(float* s, int row, int kq, f32x4 v, bool = true) {
         store(s, row, kq, xs_of(v));
     }
     struct Frag {
@@ -41,6 +43,58 @@ struct X6QTile {
                     read_frag<true, ROWS>(s + 2 * PLANE, r0, lane)};
     }
 };
+
+// k-major operand tile of a 32-k stage (the weight gradients: the pixel is the reduction index of
+// both dZ and im2col): planes h, m, l as [32 k][LD] bf16, LD = ROWS + 8 (as X6Tile's), one spare
+// 8-B slot after each for surplus units; a unit (k row, 4 columns) is three 8-B stores, a
+// fragment (8 consecutive k of 16 columns) two transposing reads per plane
+template <int ROWS>
+struct X6QTileKM {
+    static constexpr int LD = ROWS + 8;
+    static constexpr int PLANE = (2 * GK * LD + 4) / 2;       // floats
+    static constexpr int FL = 3 * PLANE;
+    static constexpr int SPARE = 2 * GK * LD;                 // bf16 units
+    __device__ static void store(float* s, int krow, int c4, const XsUnit& v, bool valid) {
+        const int off = valid ? krow * LD + 4 * c4 : SPARE;
+        __bf16* base = reinterpret_cast<__bf16*>(s) + off;
+        *reinterpret_cast<f32x2*>(base) = f32x2{v.hm.x, v.hm.y};
+        *reinterpret_cast<f32x2*>(base + 2 * PLANE) = f32x2{v.hm.z, v.hm.w};
+        *reinterpret_cast<f32x2*>(base + 4 * PLANE) = v.l;
+    }
+    __device__ static void store(float* s, int krow, int c4, f32x4 v, bool valid) {
+        store(s, krow, c4, xs_of(v), valid);
+    }
+    // 8 consecutive k (8g .. 8g + 7 for lane group g) of tile column r0 + (lane & 15)
+    __device__ static f32x4 read8(const float* plane, int r0, int lane) {
+        const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+        const __bf16* base = reinterpret_cast<const __bf16*>(plane) + (8 * g + q) * LD + r0 + 4 * p;
+        typedef __attribute__((address_space(3))) s16x4v lds_s16x4;
+        const s16x4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base));
+        const s16x4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + 4 * LD));
+        return cat_bf16(__builtin_bit_cast(bf16x4v, lo), __builtin_bit_cast(bf16x4v, hi));
+    }
+    struct Frag {
+        f32x4 h, m, l;
+    };
+    __device__ static Frag frag(const float* s, int r0, int lane) {
+        return Frag{read8(s, r0, lane), read8(s + PLANE, r0, lane), read8(s + 2 * PLANE, r0, lane)};
+    }
+    // column sum over the stage's 32 k rows (the bias gradient): h + m + l per element
+    __device__ static float colsum(const float* s, int col) {
+        const __bf16* ph = reinterpret_cast<const __bf16*>(s);
+        const __bf16* pm = reinterpret_cast<const __bf16*>(s + PLANE);
+        const __bf16* pl = reinterpret_cast<const __bf16*>(s + 2 * PLANE);
+        float a = 0.f;
+#pragma unroll
+        for (int k = 0; k < 2 * GK; ++k)
+            a += ((float)ph[k * LD + col] + (float)pm[k * LD + col]) + (float)pl[k * LD + col];
+        return a;
+    }
+};
+
+// the tile type of a loader: KC planes or k-major planes
+template <class LD_, int ROWS>
+using X6QTileOf = std::conditional_t<LD_::KC, X6QTile<ROWS>, X6QTileKM<ROWS>>;
 
 // one 32-k stage of a 16x16 tile: six single-term MFMAs, fresh sum, one fp32 add
 __device__ __forceinline__ f32x4 x6q_step(f32x4 acc, const f32x4& ah, const f32x4& am,
@@ -65,9 +119,10 @@ gemm_x6q_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, i
                 int tiles_n) {
     constexpr int BM = 16 * FM * WAVES_M;
     constexpr int BN = 16 * FN * WAVES_N;
-    static_assert(AL::ROWS == BM && BL::ROWS == BN && AL::KC && BL::KC, "KC loaders of the tile");
-    using TA = X6QTile<BM>;
-    using TB = X6QTile<BN>;
+    static_assert(AL::ROWS == BM && BL::ROWS == BN, "loader rows != tile");
+    static_assert(!EPI::ASUM || !AL::KC, "ASUM needs a k-major A tile");
+    using TA = X6QTileOf<AL, BM>;
+    using TB = X6QTileOf<BL, BN>;
     constexpr int BUF = TA::FL + TB::FL;
     constexpr bool STAGED = IsStaged<EPI>::value;
     constexpr int STAGE_LD = BN + 4;
@@ -108,6 +163,7 @@ gemm_x6q_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, i
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    float asum = 0.f;
     typename AL::Unit ra[2][AL::UNITS];
     typename BL::Unit rb[2][BL::UNITS];
     // the two loader k-steps of stage s (a second half past ks1 is zeroed: its units are staged
@@ -126,12 +182,18 @@ gemm_x6q_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, i
             for (int j = 0; j < BL::UNITS; ++j) rb[1][j] = typename BL::Unit{};
         }
     };
+    // a KC unit (row, chunk c of the 16-k step h) is 4-k quad 4h + c of the stage; a KM unit
+    // (k row, column chunk) is k row 16h + row
     auto stage = [&](float* s) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            al.each_unit(ra[h], [&](int a, int c, const auto& v, bool) { TA::store(s, a, 4 * h + c, v); });
-            bl.each_unit(rb[h], [&](int a, int c, const auto& v, bool) {
-                TB::store(s + TA::FL, a, 4 * h + c, v);
+            al.each_unit(ra[h], [&](int a, int c, const auto& v, bool ok) {
+                if constexpr (AL::KC) TA::store(s, a, 4 * h + c, v, ok);
+                else TA::store(s, 16 * h + a, c, v, ok);
+            });
+            bl.each_unit(rb[h], [&](int a, int c, const auto& v, bool ok) {
+                if constexpr (BL::KC) TB::store(s + TA::FL, a, 4 * h + c, v, ok);
+                else TB::store(s + TA::FL, 16 * h + a, c, v, ok);
             });
         }
     };
@@ -153,6 +215,9 @@ gemm_x6q_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, i
         }
         const float* A = lds + cur * BUF;
         const float* B = A + TA::FL;
+        if constexpr (EPI::ASUM) {
+            if (tn == 0 && tid < BM) asum += TA::colsum(A, tid);
+        }
         // A fragments of the wave's FM row blocks first, then one B fragment at a time (12 VGPRs
         // live for B instead of 12 FN)
         typename TA::Frag af[FM];
@@ -169,6 +234,9 @@ gemm_x6q_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, i
         cur ^= 1;
     }
 
+    if constexpr (EPI::ASUM) {
+        if (tn == 0 && tid < BM) epi.asum(m0 + tid, tz, asum);
+    }
     if constexpr (STAGED) {
         static_assert(BN == EPI::NCOL || (IsPartial<EPI>::value && EPI::NCOL % BN == 0),
                       "staged epilogue needs the full row in one block");

@@ -92,6 +92,76 @@ static void conv(const char* tag, const Bufs& B, int S) {
     fflush(stdout);
 }
 
+// weight gradient (pad 1 convolution of X): slab[z][co][kk] = sum over the split's pixels of
+// dz[p][co] im2col(X)[p][kk], both operands split (RowsKM / Im2colKM over HM + L)
+template <int IH, int CI, int CO, int Z, int FM, int FN, int WM, int WN, int QFM, int QFN, int QWM,
+          int QWN>
+static void wgrad(const char* tag, const Bufs& B, float* S0, float* S1, float* B0, float* B1,
+                  int S) {
+    constexpr int PAD = 1;
+    const int KP = 9 * CI;
+    constexpr int NT = 64 * WM * WN, BM = 16 * FM * WM, BN = 16 * FN * WN;
+    using AL = RowsKM<BM, NT, 0, 0, XsSrc>;
+    using BL = Im2colKM<IH, IH, CI, PAD, BN, NT, 0, XsSrc>;
+    const int M = S * BL::OH * BL::OW;
+    AL al;
+    al.P = B.Xhm;
+    al.PL = B.Xl;
+    al.ld = CO;
+    al.NK = M;
+    al.NC = CO;
+    BL bl;
+    bl.X = B.Xhm;
+    bl.XL = B.Xl;
+    bl.M = M;
+    const int ks = ceil_div(M, GK);
+    const int per = ceil_div(ks, Z);
+    const int tm = ceil_div(CO, BM), tn = ceil_div(KP, BN);
+    EpiSlabAcc e0{S0, CO, KP, (long)CO * KP, B0, 0};
+    const double t0 = timeit(gemm_x6_kernel<FM, FN, WM, WN, AL, BL, EpiSlabAcc>,
+                             dim3(tm * tn * Z), NT, al, bl, e0, ks, per, tm, tn);
+    constexpr int QNT = 64 * QWM * QWN, QBM = 16 * QFM * QWM, QBN = 16 * QFN * QWN;
+    using ALq = RowsKM<QBM, QNT, 0, 0, XsSrc>;
+    using BLq = Im2colKM<IH, IH, CI, PAD, QBN, QNT, 0, XsSrc>;
+    ALq alq;
+    alq.P = B.Xhm;
+    alq.PL = B.Xl;
+    alq.ld = CO;
+    alq.NK = M;
+    alq.NC = CO;
+    BLq blq;
+    blq.X = B.Xhm;
+    blq.XL = B.Xl;
+    blq.M = M;
+    const int qtm = ceil_div(CO, QBM), qtn = ceil_div(KP, QBN);
+    const int qper = 2 * ceil_div(ks, 2 * Z);             // whole 32-k stages per split
+    EpiSlabAcc e1{S1, CO, KP, (long)CO * KP, B1, 0};
+    const double t1 = timeit(gemm_x6q_kernel<QFM, QFN, QWM, QWN, ALq, BLq, EpiSlabAcc>,
+                             dim3(qtm * qtn * Z), QNT, alq, blq, e1, ks, qper, qtm, qtn);
+    // per-split slabs differ in their split boundaries; compare the slab sums over z
+    auto zsum = [&](const float* sl, long n, int zz) {
+        std::vector<float> h((size_t)zz * n);
+        CK(hipMemcpy(h.data(), sl, h.size() * 4, hipMemcpyDeviceToHost));
+        std::vector<double> o(n, 0.0);
+        for (int z = 0; z < zz; ++z)
+            for (long i = 0; i < n; ++i) o[i] += h[(size_t)z * n + i];
+        return o;
+    };
+    const long n = (long)CO * KP;
+    const std::vector<double> a = zsum(S0, n, Z), b = zsum(S1, n, Z);
+    double d = 0, y = 0;
+    for (long i = 0; i < n; ++i) {
+        d = std::max(d, fabs(a[i] - b[i]));
+        y = std::max(y, fabs(a[i]));
+    }
+    const double flops = 2.0 * M * CO * KP;
+    auto tf = [&](double t) { return flops / (t * 1e-3) / 1e12; };
+    printf("%-10s x6 %3dx%3d %7.3f ms %6.1f | x6q %3dx%3d %7.3f ms %6.1f TF/s (x%.2f) | "
+           "slab sum max|d|/max %.2e\n", tag, BM, BN, t0, tf(t0), QBM, QBN, t1, tf(t1), t0 / t1,
+           d / (y > 0 ? y : 1));
+    fflush(stdout);
+}
+
 int main(int argc, char** argv) {
     const int S = getenv("FLSIM_LAB_S") ? atoi(getenv("FLSIM_LAB_S")) : 16384;
     const size_t big = (size_t)S * 22 * 22 * 96;
@@ -127,5 +197,18 @@ int main(int argc, char** argv) {
     C("fwd4 a", 20, 96, 2, 0, 96, 4, 3, 4, 2, 4, 3, 4, 2)
     C("dg4 a", 22, 96, 0, 0, 96, 4, 3, 4, 2, 4, 3, 4, 2)
     C("fwd3 a", 18, 48, 2, 0, 96, 4, 3, 4, 2, 4, 3, 4, 2)
+    const size_t slabn = (size_t)256 * 192 * 1728;
+    float* S0 = dalloc(slabn, 0.f);
+    float* S1 = dalloc(slabn, 0.f);
+    float* B0 = dalloc(1024 * 192, 0.f);
+    float* B1 = dalloc(1024 * 192, 0.f);
+#define G(tag, IH, CI, CO, Z, FM, FN, WM, WN, QFM, QFN, QWM, QWN) \
+    if (want(tag)) wgrad<IH, CI, CO, Z, FM, FN, WM, WN, QFM, QFN, QWM, QWN>(tag, B, S0, S1, B0, \
+                                                                           B1, S);
+    G("wg6 a", 13, 192, 192, 256, 6, 3, 2, 2, 6, 3, 2, 2)
+    G("wg6 b", 13, 192, 192, 256, 6, 3, 2, 2, 3, 3, 2, 2)
+    G("wg5 a", 11, 96, 192, 512, 6, 3, 2, 2, 6, 3, 2, 2)
+    G("wg5 b", 11, 96, 192, 512, 6, 3, 2, 2, 3, 3, 2, 2)
+    G("wg4 a", 20, 96, 96, 1024, 3, 3, 2, 2, 3, 3, 2, 2)
     return 0;
 }
