@@ -37,14 +37,15 @@ __device__ __forceinline__ f32x4 mfma_x32(f32x4 a, f32x4 b, f32x4 c) {
 }
 
 // One k-step of a 16x16 output tile: the six partial products of its 16 k, A = ([h|m] a0,
-// [h|l] a1), B = ([h|m] b0, [m|h] b1, [l|h] b2), smallest terms first.  FLSIM_X6_FRESH (default):
-// the three MFMAs accumulate into a fresh register from zero and the k-step's sum is added to the
-// running accumulator with one IEEE fp32 add (round to nearest even) per element; otherwise they
-// accumulate straight into the running sum.  The bf16 MFMA's own accumulation is not a chain of
-// correctly rounded fp32 adds: over long reductions (weight gradients, data gradients through
-// several layers) the fresh form measured closer to fp64.
+// [h|l] a1), B = ([h|m] b0, [m|h] b1, [l|h] b2), smallest terms first, accumulated straight into
+// the running sum (default).  FLSIM_X6_FRESH=1 (measurement build): the three MFMAs sum into a
+// fresh register from zero and the k-step's sum is added to the running accumulator with one fp32
+// add.  That measured 1.7-6x FARTHER from fp64 on the teacher-forced gradients (PerformantNet1
+// rel-L2 1.7e-6 against 2.7e-7, VGG-11 5.3e-5 against 3.1e-5; profiles/r04/fresh_ab) and 10-18 %
+// slower: the MFMA adds its 32 products to the accumulator with one rounding, which beats a
+// separate fp32 add.
 #ifndef FLSIM_X6_FRESH
-#define FLSIM_X6_FRESH 1
+#define FLSIM_X6_FRESH 0
 #endif
 __device__ __forceinline__ f32x4 x6_step(f32x4 acc, f32x4 a0, f32x4 a1, f32x4 b0, f32x4 b1,
                                          f32x4 b2) {

@@ -7,8 +7,7 @@
 // planes h, m, l (6 B per element), laid out like the fp32 KC tile (64-B rows, 16-B chunks
 // XOR-swizzled), and every fragment is one ds_read_b128 of one plane.  A staged 4-k unit goes in
 // as three 8-B stores (h4, m4, l4).  Per stage and 16x16 output tile the six products are six
-// MFMAs, smallest terms first (hl, lh, hm, mh, mm, hh), summed in a fresh register and added to
-// the running accumulator once (FLSIM_X6_FRESH's rule, gemm_x6.h).
+// MFMAs, smallest terms first (hl, lh, hm, mh, mm, hh), accumulated into the running sum.
 #pragma once
 #include <type_traits>
 
@@ -96,17 +95,17 @@ struct X6QTileKM {
 template <class LD_, int ROWS>
 using X6QTileOf = std::conditional_t<LD_::KC, X6QTile<ROWS>, X6QTileKM<ROWS>>;
 
-// one 32-k stage of a 16x16 tile: six single-term MFMAs, fresh sum, one fp32 add
+// one 32-k stage of a 16x16 tile: six single-term MFMAs into the running sum, smallest first
+// (straight accumulation: gemm_x6.h FLSIM_X6_FRESH)
 __device__ __forceinline__ f32x4 x6q_step(f32x4 acc, const f32x4& ah, const f32x4& am,
                                           const f32x4& al, const f32x4& bh, const f32x4& bm,
                                           const f32x4& bl) {
-    f32x4 t = mfma_x32(ah, bl, f32x4{0.f, 0.f, 0.f, 0.f});
-    t = mfma_x32(al, bh, t);
-    t = mfma_x32(ah, bm, t);
-    t = mfma_x32(am, bh, t);
-    t = mfma_x32(am, bm, t);
-    t = mfma_x32(ah, bh, t);
-    return acc + t;
+    acc = mfma_x32(ah, bl, acc);
+    acc = mfma_x32(al, bh, acc);
+    acc = mfma_x32(ah, bm, acc);
+    acc = mfma_x32(am, bh, acc);
+    acc = mfma_x32(am, bm, acc);
+    return mfma_x32(ah, bh, acc);
 }
 
 // Same contract as gemm_x6_kernel for KC loader pairs (each_unit over 16-deep k-steps): the grid

@@ -384,7 +384,7 @@ int main(int argc, char** argv) {
                        B.Wl, (long)wn / 4);
     B.Wp = planes(192 * 1760);
     B.b = dalloc(256, 0.01f);
-    const size_t ybig = (size_t)S * 15 * 15 * 192;
+    const size_t ybig = big;             // S * 22 * 22 * 96: the largest output (fwd4)
     B.Y0 = dalloc(ybig, 0.f);
     B.Y1 = dalloc(ybig, 0.f);
     CK(hipDeviceSynchronize());

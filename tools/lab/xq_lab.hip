@@ -178,7 +178,7 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL(k_to_xs, dim3(ceil_div((long)wn / 4, 256)), dim3(256), 0, 0, W, B.Whm,
                        B.Wl, (long)wn / 4);
     B.b = dalloc(256, 0.01f);
-    const size_t ybig = (size_t)S * 15 * 15 * 192;
+    const size_t ybig = big;             // S * 22 * 22 * 96: the largest output (fwd4)
     B.Y0 = dalloc(ybig, 0.f);
     B.Y1 = dalloc(ybig, 0.f);
     CK(hipDeviceSynchronize());
