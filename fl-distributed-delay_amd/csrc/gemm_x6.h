@@ -72,13 +72,40 @@ __device__ __forceinline__ bf16x4v read_km_half(const float* plane, int LD, int 
     return __builtin_bit_cast(bf16x4v, v);
 }
 
+// Row stride (bf16 units) of a k-major plane [16 k][LD].  A transposing read serves 32 lanes per
+// LDS cycle: 8 k rows x 32 B, conflict-free when the 8 rows' 32-B pieces cover the 256 B of the
+// 64 banks, i.e. when the row stride 2 LD bytes is an odd multiple of 32 (LD = 16 mod 32).  Of
+// those strides
+// the smallest >= ROWS whose ds_write_b64 unit stores (16 lanes per cycle on 32 banks; TPR lanes
+// per k row, so a 16-lane group may span two rows) are conflict-free too, else the smallest.
+// (ROWS + 8, used before, cost 2 extra LDS cycles per transposed read: SQ_LDS_BANK_CONFLICT
+// 0.4-1.0 G cycles per weight-gradient launch, profiles/r04/prof_r04e.)
+constexpr bool km_writes_free(int ld, int tpr) {
+    if (tpr >= 16) return true;
+    bool used[16] = {};
+    for (int l = 0; l < 16; ++l) {
+        const int row = l / tpr, c = l % tpr;
+        const int chunk = ((row * 2 * ld + 8 * c) % 128) / 8;
+        if (used[chunk]) return false;
+        used[chunk] = true;
+    }
+    return true;
+}
+constexpr int km_ld(int rows, int tpr) {
+    for (int ld = rows; ld < rows + 128; ++ld)
+        if (ld % 32 == 16 && km_writes_free(ld, tpr)) return ld;
+    for (int ld = rows; ld < rows + 32; ++ld)
+        if (ld % 32 == 16) return ld;
+    return rows + 8;
+}
+
 // One operand tile of a stage.  AROLE: the A side ([h|m], [h|l]) or the B side ([h|m], [m|h],
 // [l|h]).  KC: combination planes laid out like the fp32 KC tile; KM: planes h, m, l as
-// [16][LD] bf16 (LD = ROWS + 8: rows of one transposed read land 4 dwords apart mod 64), one
-// spare 8-B slot after each for surplus units.
-template <bool KC, int ROWS, bool AROLE>
+// [16][LD] bf16 (LD = km_ld: conflict-free transposed reads), one spare 8-B slot after each for
+// surplus units.  TPR: the loader's threads per k row (NT / 16).
+template <bool KC, int ROWS, bool AROLE, int TPR = 16>
 struct X6Tile {
-    static constexpr int LD = ROWS + 8;
+    static constexpr int LD = km_ld(ROWS, TPR);
     static constexpr int NPL = KC ? 2 : 3;
     static constexpr int PLANE_FL = KC ? KCTile<ROWS>::FLOATS : (GK * LD + 4) / 2;
     static constexpr int FL = NPL * PLANE_FL;
@@ -152,8 +179,8 @@ gemm_x6_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, in
     constexpr int BM = 16 * FM * WAVES_M;
     constexpr int BN = 16 * FN * WAVES_N;
     static_assert(AL::ROWS == BM && BL::ROWS == BN, "loader rows != tile");
-    using TA = X6Tile<AL::KC, BM, true>;
-    using TB = X6Tile<BL::KC, BN, false>;
+    using TA = X6Tile<AL::KC, BM, true, 4 * WAVES_M * WAVES_N>;
+    using TB = X6Tile<BL::KC, BN, false, 4 * WAVES_M * WAVES_N>;
     static_assert(!EPI::ASUM || !AL::KC, "ASUM needs a k-major A tile");
     constexpr int BUF = TA::FL + TB::FL;
     constexpr bool STAGED = IsStaged<EPI>::value;

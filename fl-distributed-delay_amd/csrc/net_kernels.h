@@ -11,7 +11,6 @@
 #include "gemm_direct.h"
 #include "gemm_dx6.h"
 #include "gemm_x6.h"
-#include "gemm_x6q.h"
 #include "loaders.h"
 #include "pn1.h"
 #include "probe.h"
@@ -720,23 +719,6 @@ static int launch_gemm(const AL& al, const BL& bl, const EPI& epi, int M, int N,
     return probe_end(ps, kid, alg_flops);
 }
 
-// the planar split-bf16 kernel (gemm_x6q.h): k-steps walked in 32-k stages; a split's
-// k-steps (ksteps_per_split) are rounded up to whole stages
-template <int FM, int FN, int WM, int WN, class AL, class BL, class EPI>
-static int launch_gemm_q(const AL& al, const BL& bl, const EPI& epi, int M, int N, int ksteps,
-                         int Z, hipStream_t st, int kid, double alg_flops) {
-    constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
-    const int per = 2 * ((ksteps + 2 * Z - 1) / (2 * Z));
-    const int tm = ceil_div(M, BM), tn = ceil_div(N, BN);
-    dim3 grid(tm * tn * Z);
-    const ProbeSlot ps = probe_begin();
-    hipExtLaunchKernelGGL((gemm_x6q_kernel<FM, FN, WM, WN, AL, BL, EPI>), grid,
-                          dim3(64 * WM * WN), 0, st, ps.start, ps.stop, 0, al, bl, epi, ksteps,
-                          per, tm, tn);
-    FLSIM_LAUNCH_CHECK();
-    return probe_end(ps, kid, alg_flops);
-}
-
 // direct-A GEMM (gemm_direct.h): rows = output pixels loaded per wave straight into MFMA
 // fragments, B (packed weights) staged through LDS KB k-steps at a time
 template <int FM, int FN, int WAVES, int KB, int DEPTH, class AD, class BL, class EPI>
@@ -918,9 +900,8 @@ static int conv_like_sz(const float* X, int S, const float* Wpk, int N, int KP, 
 // reduction index as they stand
 // SRC = XsSrc: dz (and X, unless SRCB says otherwise) in the split form (dzl, Xl their L parts;
 // X6 only)
-// Q: the planar split-bf16 kernel (gemm_x6q.h) instead of gemm_x6_kernel (X6 must be set too)
 template <int IH, int IW, int CI, int PAD, int FM, int FN, int WM, int WN, int VO = 0,
-          bool DZC = false, bool X6 = false, class SRC = BufSrc, class SRCB = SRC, bool Q = false>
+          bool DZC = false, bool X6 = false, class SRC = BufSrc, class SRCB = SRC>
 static int conv_wgrad(const float* dz, const float* X, int S, int CO, int KP, float* slab,
                       float* bslab, int Z, hipStream_t st, int kid, int kreal,
                       int zinit = 0x7fffffff, int* zused = nullptr, const float* dzl = nullptr,
@@ -945,20 +926,14 @@ static int conv_wgrad(const float* dz, const float* X, int S, int CO, int KP, fl
     bl.M = M;
     EpiSlabAcc epi{slab, CO, KP, (long)CO * KP, bslab, zinit};
     const int tiles = ceil_div(CO, BM) * ceil_div(KP, BN);
-    static_assert(X6 || !Q, "the planar kernel is a split-bf16 kernel");
     const void* kfn;
-    if constexpr (Q)
-        kfn = (const void*)gemm_x6q_kernel<FM, FN, WM, WN, AL, BL, EpiSlabAcc>;
-    else if constexpr (X6)
+    if constexpr (X6)
         kfn = (const void*)gemm_x6_kernel<FM, FN, WM, WN, AL, BL, EpiSlabAcc>;
     else
         kfn = (const void*)gemm_kernel<FM, FN, WM, WN, AL, BL, EpiSlabAcc>;
     static const int cap = resident_blocks(kfn, NT);
     const int zu = wsplit(ceil_div(M, GK), Z, tiles, cap);
     if (zused) *zused = zu;
-    if constexpr (Q)
-        return launch_gemm_q<FM, FN, WM, WN>(al, bl, epi, CO, KP, ceil_div(M, GK), zu, st, kid,
-                                             2.0 * M * CO * kreal);
     return launch_gemm<FM, FN, WM, WN, X6>(al, bl, epi, CO, KP, ceil_div(M, GK), zu, st, kid,
                                            2.0 * M * CO * kreal);
 }
@@ -968,14 +943,14 @@ static int conv_wgrad(const float* dz, const float* X, int S, int CO, int KP, fl
 // chunk's larger ones on conv3/5/6 by 3-10 %, 48x144 beats 48x48 on conv2 by 4 %)
 template <int IH, int IW, int CI, int PAD, int FM, int FN, int WM, int WN, int FMS, int FNS,
           int WMS, int WNS, int VO = 0, bool DZC = false, bool X6 = false, class SRC = BufSrc,
-          class SRCB = SRC, bool Q = false>
+          class SRCB = SRC>
 static int conv_wgrad_sz(const float* dz, const float* X, int S, int CO, int KP, float* slab,
                          float* bslab, int Z, hipStream_t st, int kid, int kreal, int zinit,
                          int* zused, const float* dzl = nullptr, const float* Xl = nullptr) {
     if (S <= small_chunk_samples())
-        return conv_wgrad<IH, IW, CI, PAD, FMS, FNS, WMS, WNS, VO, DZC, X6, SRC, SRCB, Q>(
+        return conv_wgrad<IH, IW, CI, PAD, FMS, FNS, WMS, WNS, VO, DZC, X6, SRC, SRCB>(
             dz, X, S, CO, KP, slab, bslab, Z, st, kid, kreal, zinit, zused, dzl, Xl);
-    return conv_wgrad<IH, IW, CI, PAD, FM, FN, WM, WN, VO, DZC, X6, SRC, SRCB, Q>(
+    return conv_wgrad<IH, IW, CI, PAD, FM, FN, WM, WN, VO, DZC, X6, SRC, SRCB>(
         dz, X, S, CO, KP, slab, bslab, Z, st, kid, kreal, zinit, zused, dzl, Xl);
 }
 
@@ -1007,29 +982,6 @@ static int conv_dx6(XsT X, int S, XsT W, int N, int KP, const EPI& epi, hipStrea
                           epi, KP / GK, tm, tn);
     FLSIM_LAUNCH_CHECK();
     return probe_end(ps, kid, 2.0 * ad.M * N * kreal);
-}
-
-// the same GEMM on the planar split-bf16 kernel (gemm_x6q.h: 32-k stages, three plain planes per
-// tile; not bit-identical to the x6 kernels, which pair two terms per MFMA over 16-k steps)
-template <int IH, int IW, int CI, int PAD, int FM, int FN, int WM, int WN, bool WIN, int OHX,
-          class EPI>
-static int conv_xq(XsT X, int S, XsT W, int N, int KP, const EPI& epi, hipStream_t st, int kid,
-                   int kreal) {
-    constexpr int NT = 64 * WM * WN;
-    constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
-    using AL = Im2colKC<IH, IW, CI, PAD, BM, NT, WIN, OHX, XsSrc>;
-    using BL = RowsKC<BN, NT, XsSrc>;
-    AL al;
-    al.X = X.hm;
-    al.XL = X.l;
-    al.M = S * AL::ROWS_PER_IMG;
-    BL bl;
-    bl.P = W.hm;
-    bl.PL = W.l;
-    bl.ld = KP;
-    bl.NR = N;
-    return launch_gemm_q<FM, FN, WM, WN>(al, bl, epi, al.M, N, KP / GK, 1, st, kid,
-                                         2.0 * al.M * N * kreal);
 }
 
 // the same GEMM on gemm_x6_kernel with both operands staged through LDS (bit-identical to
