@@ -23,12 +23,12 @@ import torch.nn.functional as F
 
 from oracle import model_ref as MR
 
-TF_TOL = 2e-6
-# FLIP_FLOOR: the fp32-MFMA build measured up to 6 flips where the CPU port had none (the CIFAR
-# pool test) and 9 against the port's 4; the split-bf16 build (gemm_x6.h) 7 and 12 on the same
-# inputs, 58 against 45 summed over the 11 checks (profiles/r03w/flips_census.txt).  A wrong
-# mask or argmax rule flips thousands.
-FLIP_C, FLIP_FLOOR = 3, 10
+# Bounds = 1.5 x the split-bf16 build's measured worst (round 4, profiles/r04/prof_r04e/flips.jsonl;
+# the results are bit-reproducible across boxes, r04e = r04f): teacher-forced rel-L2 up to 6.7e-7
+# over the 11 checks; decision flips at most 6 above 3 x the CPU fp32 port's own in one check,
+# 40 against the port's 21 summed.  A wrong mask or argmax rule flips thousands.
+TF_TOL = 1.0e-6
+FLIP_C, FLIP_FLOOR = 3, 9
 GROUP = 1 << 20
 LAYERS = ("a1", "i1", "a3", "i2", "a5", "i3", "e1", "e2")
 

@@ -225,9 +225,9 @@ def test_simulation_matches_oracle_trajectory(pool, thr):
     print("MEASURED", json.dumps(dict(test=f"n4_d2_trajectory_thr{int(thr)}",
                                       drift_gpu=drift_gpu, drift_cpu=drift_cpu,
                                       ratio=drift_gpu / drift_cpu)))
-    # bound = 1.5 x the ratio measured on MI355X (profiles/r03a/trajectory_bounds.json: 1.97
-    # without throttle, 0.95 with)
-    assert drift_gpu <= (3.0 if not thr else 1.45) * drift_cpu, (drift_gpu, drift_cpu)
+    # bound = 1.5 x the ratio the split-bf16 build measured on MI355X (2.39 without throttle,
+    # 1.20 with; profiles/r04/prof_r04e/pytest_gpu.txt MEASURED)
+    assert drift_gpu <= (3.6 if not thr else 1.8) * drift_cpu, (drift_gpu, drift_cpu)
 
 
 def test_warm_start_model_file_trajectory(pool, tmp_path):
@@ -593,7 +593,7 @@ def test_independent_entries_trajectory(pool, thr):
     print("MEASURED", json.dumps(dict(test=f"n4_d2_independent_thr{int(thr)}",
                                       drift_gpu=drift_gpu, drift_cpu=drift_cpu,
                                       ratio=drift_gpu / drift_cpu)))
-    # bound = 1.5 x the ratio measured on MI355X (profiles/r03a/trajectory_bounds.json: 2.98
-    # without throttle, 3.60 with; the GPU sums the fast workers' gradients in GEMM order, the
-    # oracle per worker)
-    assert drift_gpu <= (4.5 if not thr else 5.4) * drift_cpu, (drift_gpu, drift_cpu)
+    # bound = 1.5 x the ratio the split-bf16 build measured on MI355X (3.04 without throttle,
+    # 2.45 with; profiles/r04/prof_r04e/pytest_gpu.txt MEASURED; the GPU sums the fast
+    # workers' gradients in GEMM order, the oracle per worker)
+    assert drift_gpu <= (4.6 if not thr else 3.7) * drift_cpu, (drift_gpu, drift_cpu)

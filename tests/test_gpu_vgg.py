@@ -20,10 +20,10 @@ pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not has_gpu(), reason="needs a
 
 
 # per-tensor rel-L2 of the GPU gradient against the fp64 reference with the GPU's own decisions.
-# The fp32-MFMA build stayed within 2e-5; with every VGG GEMM on the split-bf16 kernel
-# (gemm_x6.h, fp32 accumulation) the worst tensor measured 2.3e-5 and 3.1e-5
-# (profiles/r03z/pytest.log): the bound is 5e-5.  A wrong kernel misses by orders of magnitude.
-TF_TOL = 5e-5
+# The bound is 1.5 x the split-bf16 build's measured worst: features.0.bias at 3.14e-5 (dropout,
+# items2; 1.10e-5 and 2.32e-5 for the other cases; profiles/r04/prof_r04e/tol.jsonl).
+# A wrong kernel misses by orders of magnitude.
+TF_TOL = 4.7e-5
 
 def _tol_log(worst):
     """Per-tensor error census across builds (measurement only: FLSIM_TOL_LOG=<file>)."""

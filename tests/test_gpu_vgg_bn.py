@@ -193,9 +193,9 @@ def test_vgg_bn_gradient_teacher_forced_decisions(pool, dropout, items):
         lrefs.append(lref.item())
     np.testing.assert_allclose(loss, lrefs, atol=1e-5)
     ref = torch.cat([p.grad.reshape(-1) for p in P]).numpy()
-    # 2e-5 on the fp32-MFMA build; the split-bf16 GEMMs measured up to 1.16x that
-    # (profiles/r03z/pytest.log), as in test_gpu_vgg.py's TF_TOL
-    _check_grad(g, ref, rtol=5e-5)
+    # 1.5 x the split-bf16 build's measured worst, 4.31e-5 (features.1.bias, dropout items2;
+    # profiles/r04/prof_r04e/tol.jsonl stores it as 0.861 of the former 5e-5 bound)
+    _check_grad(g, ref, rtol=6.5e-5)
     # per-worker statistics of the chunk vs each worker's own BatchNorm batch (oracle, fp64)
     st = stats.double().cpu().numpy()
     for wi, it in enumerate(items):
