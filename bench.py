@@ -193,20 +193,20 @@ def stream_step_probe(sim, iters=20):
     window (untimed for `value`): rule() + Adam from S_t in a buffer, the stream that follows the
     all-reduce (flsim_aggregate_adam_rule_push), on copies of the run's theta / m / v, for the
     reference's two entry lists at n = 1024: a plain throttled epoch (k = c_t = 512) and the tick
-    epoch t = d (c_t = 512 + the stale S_{t-d}, the FIFO slot written in the same pass).  Bytes:
-    SURVEY 8(d) 4P (1 + stale + 6) (+ 4P for the slot write).  Launch times from the probe."""
+    epoch t = d (c_t = 512 + the stale S_{t-d}).  A tick epoch builds and all-reduces S_t in the
+    FIFO slot it pushes (sim.py epoch), so its stream writes no second copy.  Bytes: SURVEY 8(d)
+    4P (1 + stale + 6).  Launch times from the probe."""
     from flsim._lib import KernelProbe
     from flsim.engine import Rule
     P, dev = sim.P, sim.device
     S = torch.randn(sim.Ppad, device=dev, generator=torch.Generator(device=dev).manual_seed(1))
     S.mul_(1e-3)
     st = S.flip(0).contiguous()
-    slot = torch.empty_like(S)
     p, m, v = sim.theta.clone(), sim.m.clone(), sim.v.clone()
     out = {}
     for name, rule, so, nbytes in (
             ("plain_k512", Rule(512, [], c=512), None, 4 * P * 7),
-            ("tick_k513_fifo", Rule(513, [st], c=512), slot, 4 * P * 9)):
+            ("tick_k513_in_slot", Rule(513, [st], c=512), None, 4 * P * 8)):
         for _ in range(3):
             sim.engine.aggregate_rule(S, rule, p, m, v, max(sim.step, 1), S_out=so)
         torch.cuda.synchronize()
@@ -221,10 +221,10 @@ def stream_step_probe(sim, iters=20):
         cnt, ms, _ = rec
         us = ms / cnt * 1e3
         out[name] = dict(avg_launch_us=round(us, 2), bytes=nbytes,
-                         bytes_8d=4 * P * (7 + (1 if so is not None else 0)),
+                         bytes_8d=4 * P * (7 + len(rule.arrays)),
                          achieved=round(nbytes / us / 1e3, 1), unit="GB/s",
                          frac=round(nbytes / us / 1e3 / HBM_PEAK_GBPS, 4),
-                         frac_8d=round(4 * P * (7 + (1 if so is not None else 0)) / us / 1e3 /
+                         frac_8d=round(4 * P * (7 + len(rule.arrays)) / us / 1e3 /
                                        HBM_PEAK_GBPS, 4))
     return dict(kernel="k_agg_stream_reg (rule() + Adam from S_t after the all-reduce)",
                 bound="hbm", peak=HBM_PEAK_GBPS, **out) if out else None

@@ -144,9 +144,13 @@ class FLSimulation:
         self.coll_events = []
 
     # ---------------------------------------------------------------------------------------------
-    def _slot(self):
-        return self.free_slots.pop() if self.free_slots else \
-            torch.empty(self.Ppad, device=self.device)
+    def _slot(self, n=None):
+        """A FIFO slot of >= n floats (default Ppad): a released one when one is large enough."""
+        n = self.Ppad if n is None else n
+        for j in range(len(self.free_slots) - 1, -1, -1):
+            if self.free_slots[j].numel() >= n:
+                return self.free_slots.pop(j)
+        return torch.empty(n, device=self.device)
 
     def _worker_table(self, t, workers, ks):
         """WorkerRec (t, i, k, 0) of this rank's computing workers, copied host->device from a
@@ -265,9 +269,18 @@ class FLSimulation:
         lo, hi = self.shard(active)
         eng = self.engine
         G = self.G                               # 128-sample groups (units) per worker-step
-        S = self.comm[:self.P]
-        losses = self.comm[self.Ppad:self.Ppad + len(active) * G]
-        stats = self.comm[self.stats_off:self.stats_off + len(active) * self.nstat].view(
+        fused = self.fused and self.world == 1 and hasattr(eng, "server_step")
+        pushes = plan.pushed and self.semantics == "reference"
+        # An epoch that pushes S_t onto the FIFO and ends with the streaming server step (world > 1,
+        # or an engine without the fused step) builds S_t -- and all-reduces it -- straight in the
+        # slot it pushes, a whole [S_t | losses] comm buffer: the stream then reads S_t from the slot
+        # and writes no second copy (4P fewer HBM bytes at every tick).  BatchNorm runs
+        # keep the shared buffer (their comm buffer also holds n x the per-call statistics).
+        in_slot = pushes and not fused and not self.nstat
+        comm = self._slot(self.stats_off) if in_slot else self.comm
+        S = comm[:self.P]
+        losses = comm[self.Ppad:self.Ppad + len(active) * G]
+        stats = comm[self.stats_off:self.stats_off + len(active) * self.nstat].view(
             len(active), self.nstat)
         if self.world > 1:
             losses.zero_()
@@ -287,20 +300,19 @@ class FLSimulation:
             kw = {"stats_out": stats[c0:c1]} if self.nstat else {}
             eng.run_chunk(self.theta, self.pool, wt[c0 - lo * G:c1 - lo * G], c1 - c0, self.n,
                           self.seed, self.dropout, losses[c0:c1], **kw)
-        fused = self.fused and self.world == 1 and hasattr(eng, "server_step")
         if not fused or self.keep_S:
             eng.end_epoch(S)
         self.rank_worker_steps.append(hi - lo)
         if self.world > 1:
             end = self.stats_off + len(active) * self.nstat if self.nstat else \
                 self.Ppad + len(active) * G
-            self._all_reduce(self.comm[:end])
+            self._all_reduce(comm[:end])
         if self.nstat:   # BatchNorm running buffers: every computing worker's call, in order
             eng.update_running(stats, len(active))
         push = None
-        if plan.pushed and self.semantics == "reference":
+        if pushes:
             n_push = int(sum(1 for i in range(self.n) if self.delays[i] != 0 and plan.computes[i]))
-            push = self._slot()
+            push = comm if in_slot else self._slot()
             if fused and self.keep_S:
                 push[:self.P].copy_(S)
             # otherwise the server step writes S_t into the slot in its own pass: the fused
@@ -321,7 +333,8 @@ class FLSimulation:
         elif fused:
             eng.aggregate_rule(S, rule, self.theta, self.m, self.v, self.step, **hp)
         else:
-            eng.aggregate_rule(S, rule, self.theta, self.m, self.v, self.step, S_out=push, **hp)
+            eng.aggregate_rule(S, rule, self.theta, self.m, self.v, self.step,
+                               S_out=None if in_slot else push, **hp)
         for (_, src) in plan.stale:
             if self.semantics == "reference":
                 entry = self.stale_store[src]
