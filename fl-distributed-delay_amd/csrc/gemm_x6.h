@@ -166,6 +166,22 @@ struct X6Tile {
     }
 };
 
+// Epilogues with ASUM_MFMA = true take the bias column sum (ASUM) on the matrix cores: the wave
+// column wn = 0 of the tn = 0 blocks multiplies each A fragment it already holds by a ones operand,
+// [h|m] x [1|1] + [h|l] x [0|1] = sum over the k-step of h + m + l per row, two MFMAs per fragment,
+// instead of the VALU column sum over the LDS tile (TA::colsum: 3 bf16 reads, a convert and an add
+// per element and k, on BM threads while the block waits at the next barrier).
+template <class E, class = void>
+struct AsumMfma : std::false_type {};
+template <class E>
+struct AsumMfma<E, std::void_t<decltype(E::ASUM_MFMA)>> : std::bool_constant<E::ASUM_MFMA> {};
+
+__device__ __forceinline__ f32x4 bf16_ones(bool lo, bool hi) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const uint32_t a = lo ? 0x3f803f80u : 0u, b = hi ? 0x3f803f80u : 0u;
+    return __builtin_bit_cast(f32x4, u32x4{a, a, b, b});
+}
+
 // Same contract as gemm_kernel (gemm_core.h: 1-D XCD-aware grid, register-staged double buffer,
 // one barrier per 16-deep k-step, STAGED / plain / PRE / ASUM epilogues); loaders expose
 // each_unit().  The B side of a KC tile keeps two planes [h|m], [l|h] and pairs
@@ -182,6 +198,7 @@ gemm_x6_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, in
     using TA = X6Tile<AL::KC, BM, true, 4 * WAVES_M * WAVES_N>;
     using TB = X6Tile<BL::KC, BN, false, 4 * WAVES_M * WAVES_N>;
     static_assert(!EPI::ASUM || !AL::KC, "ASUM needs a k-major A tile");
+    constexpr bool AMF = EPI::ASUM && AsumMfma<EPI>::value;
     constexpr int BUF = TA::FL + TB::FL;
     constexpr bool STAGED = IsStaged<EPI>::value;
     constexpr int STAGE_LD = BN + 4;
@@ -223,6 +240,10 @@ gemm_x6_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, in
         for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     float asum = 0.f;
+    f32x4 bacc[AMF ? FM : 1];
+#pragma unroll
+    for (int i = 0; i < (AMF ? FM : 1); ++i) bacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bool bwave = AMF && tn == 0 && wn == 0;     // wave-uniform
     typename AL::Unit ra[AL::UNITS];
     typename BL::Unit rb[BL::UNITS];
     auto stage = [&](float* s) {
@@ -256,7 +277,7 @@ gemm_x6_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, in
         }
         const float* A = lds + cur * BUF;
         const float* B = A + TA::FL;
-        if constexpr (EPI::ASUM) {
+        if constexpr (EPI::ASUM && !AMF) {
             if (tn == 0 && tid < BM) asum += TA::colsum(A, tid);
         }
         typename TB::Frag bf[FN];
@@ -265,6 +286,12 @@ gemm_x6_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, in
 #pragma unroll
         for (int i = 0; i < FM; ++i) {
             const typename TA::Frag af = TA::frag(A, wm * 16 * FM + 16 * i, lane);
+            if constexpr (AMF) {
+                if (bwave) {
+                    bacc[i] = mfma_x32(af.x1, bf16_ones(false, true), bacc[i]);   // l
+                    bacc[i] = mfma_x32(af.x0, bf16_ones(true, true), bacc[i]);    // h + m
+                }
+            }
 #pragma unroll
             for (int j = 0; j < FN; ++j) {
                 acc[i][j] = x6_step(acc[i][j], af.x0, af.x1, bf[j].x0, bf[j].x1, bf[j].x2);
@@ -274,7 +301,16 @@ gemm_x6_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, in
         cur ^= 1;
     }
 
-    if constexpr (EPI::ASUM) {
+    if constexpr (AMF) {
+        // every column of the ones product is the row sum: lanes of column 0 store it
+        if (bwave && (lane & 15) == 0) {
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr)
+                    epi.asum(m0 + wm * 16 * FM + 16 * i + 4 * (lane >> 4) + rr, tz, bacc[i][rr]);
+        }
+    } else if constexpr (EPI::ASUM) {
         if (tn == 0 && tid < BM) epi.asum(m0 + tid, tz, asum);
     }
     if constexpr (STAGED) {

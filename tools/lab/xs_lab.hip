@@ -119,6 +119,15 @@ static void conv(const char* tag, const float* X, const Xs& Xx, const float* W, 
     fflush(stdout);
 }
 
+// the same slab epilogue without the in-loop bias column sum (what the ASUM colsum costs)
+struct EpiSlabAccNA : EpiSlabAcc {
+    static constexpr bool ASUM = false;
+};
+// ... and with the column sum on the matrix cores (gemm_x6.h AsumMfma)
+struct EpiSlabAccMF : EpiSlabAcc {
+    static constexpr bool ASUM_MFMA = true;
+};
+
 // weight gradient: slab[z][co][kk] = sum over the split's pixels of dz[p][co] im2col(X)[p][kk]
 template <int IH, int CI, int CO, int FM, int FN, int WM, int WN>
 static void wgrad(const char* tag, const float* dz, const Xs& dzx, const float* X, const Xs& Xx,
@@ -159,9 +168,30 @@ static void wgrad(const char* tag, const float* dz, const Xs& dzx, const float* 
     const double t1 = timeit(gemm_x6_kernel<FM, FN, WM, WN, ALs, BLs, EpiSlabAcc>,
                              dim3(tm * tn * Z), NT, als, bls, e1, ks, per, tm, tn);
     const size_t d = ndiff(S0, S1, (size_t)Z * CO * KP), db = ndiff(B0, B1, (size_t)Z * CO);
+    EpiSlabAccNA e2;
+    static_cast<EpiSlabAcc&>(e2) = e1;
+    const double t2 = timeit(gemm_x6_kernel<FM, FN, WM, WN, ALs, BLs, EpiSlabAccNA>,
+                             dim3(tm * tn * Z), NT, als, bls, e2, ks, per, tm, tn);
+    std::vector<float> hb1((size_t)Z * CO);
+    hipMemcpy(hb1.data(), B1, hb1.size() * 4, hipMemcpyDeviceToHost);
+    EpiSlabAccMF e3;
+    static_cast<EpiSlabAcc&>(e3) = e1;
+    e3.Bsl = B0;
+    const double t3 = timeit(gemm_x6_kernel<FM, FN, WM, WN, ALs, BLs, EpiSlabAccMF>,
+                             dim3(tm * tn * Z), NT, als, bls, e3, ks, per, tm, tn);
+    std::vector<float> hb3((size_t)Z * CO);
+    hipMemcpy(hb3.data(), B0, hb3.size() * 4, hipMemcpyDeviceToHost);
+    double num = 0, den = 0;
+    for (size_t i = 0; i < hb1.size(); ++i) {
+        num += ((double)hb3[i] - hb1[i]) * ((double)hb3[i] - hb1[i]);
+        den += (double)hb1[i] * hb1[i];
+    }
     auto tf = [&](double t) { return flops / (t * 1e-3) / 1e12; };
-    printf("%-16s x6 %3dx%3d Z %4d %7.3f ms %6.1f | xs %7.3f ms %6.1f TF/s | differ slab %zu bias %zu\n",
-           tag, BM, BN, Z, t0, tf(t0), t1, tf(t1), d, db);
+    printf("%-16s x6 %3dx%3d Z %4d %7.3f ms %6.1f | xs %7.3f ms %6.1f | xs no-bias-sum %7.3f ms "
+           "%6.1f | xs mfma-bias-sum %7.3f ms %6.1f TF/s | differ slab %zu bias %zu | mfma bias "
+           "rel-L2 vs valu %.2e\n",
+           tag, BM, BN, Z, t0, tf(t0), t1, tf(t1), t2, tf(t2), t3, tf(t3), d, db,
+           std::sqrt(num / (den > 0 ? den : 1)));
     fflush(stdout);
 }
 
