@@ -329,7 +329,8 @@ static int dx6(XsT X, int S, XsT W, int N, int KP, const EPI& epi, hipStream_t s
 // The same GEMMs on gemm_x6_kernel with both operands staged through LDS (conv_xs; bit-identical
 // to conv_dx6): WM x WN waves of 16*FM x 16*FN, FM halved for small chunks.  The wide layers
 // (N = 192: conv5/6 forward, conv6 data gradient; N = 96 data gradients of conv4/5) run faster
-// this way (profiles/r04b/lab_xs.txt: conv6 data gradient 8.8 vs 10.7 ms, forward 11.1 vs 12.0)
+// this way (profiles/r04/lab/lab_xs_r04b.txt: conv6 data gradient 8.8 vs 10.7 ms, forward
+// 11.1 vs 12.0)
 template <int IH, int IW, int CI, int PAD, int FM, int FN, int WM, int WN, bool WIN, int OHX,
           class EPI>
 static int xs(XsT X, int S, XsT W, int N, int KP, const EPI& epi, hipStream_t st, int kid,
@@ -597,9 +598,9 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
         1728)));
     // ---- conv4: wgrad (input a3), bias, dgrad -> dz3 = . * (a3 > 0) into gx (fp32) ----
     // dz3 and dz2 stay fp32: their data gradients have N = 48 columns, where the fp32 MFMA
-    // kernels are faster than any split-bf16 form (profiles/r04b/lab_xs.txt: conv3's 3.8 ms fp32
-    // against 4.4 / 4.9 / 5.6 ms for x6 / dx6 / xs), so conv3 / conv2's weight gradients split
-    // dZ while staging (split-bf16 kernel over an fp32 dZ and a split layer input)
+    // kernels are faster than any split-bf16 form (profiles/r04/lab/lab_xs_r04b.txt: conv3's
+    // 3.8 ms fp32 against 4.4 / 4.9 / 5.6 ms for x6 / dx6 / xs), so conv3 / conv2's weight
+    // gradients split dZ while staging (split-bf16 kernel over an fp32 dZ and a split layer input)
     RC(join());                                   // conv5's wgrad reads gx = dz5: done first
     RC(fork());
     RC((conv_wgrad<20, 20, 96, 2, 3, 3, 2, 2, 0, false, true, XsSrc>(
