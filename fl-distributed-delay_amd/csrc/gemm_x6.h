@@ -1,8 +1,10 @@
 // fp32 GEMM on the bf16 matrix cores at fp32 accuracy ("bf16x6"), for k-contiguous operand pairs.
 //
 // gfx950's fp32 MFMA (v_mfma_f32_16x16x4_f32) runs at 1/16 of the bf16 rate.  Each fp32 operand
-// x is split when it is staged into LDS: h = bf16(x), m = bf16(x - h), l = bf16(x - h - m) (round
-// to nearest even; x - h and x - h - m are exact in fp32), so x = h + m + l to within 2^-25 |x|.
+// x is split into h = bf16(x), m = bf16(x - h), l = bf16(x - h - m) (round to nearest even; x - h
+// and x - h - m are exact in fp32), so x = h + m + l exactly (split.h).  Operands that their
+// producer already wrote in that split form (split.h "xs" tensors: XsSrc loaders) are staged as
+// they stand; fp32 operands (BufSrc loaders) are split by the thread that stages them.
 // A product a*b is the sum of six exact partial products
 //     ah*bh + am*bh  +  ah*bm + am*bm  +  ah*bl + al*bh
 // (the three dropped, am*bl + al*bm + al*bl, are below 2^-25 |a b|), accumulated in fp32.
