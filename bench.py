@@ -429,7 +429,7 @@ def main():
             # into three bf16 parts and sum six exact partial products on the bf16 matrix cores
             # (gemm_x6.h): fp32 accuracy, not a reduced-precision mode
             "math": "bf16x6 split of the fp32 operands, fp32 accumulate (conv2-6 forward and "
-                    "weight gradients, conv5/6 data gradients, linear1 forward and weight "
+                    "weight gradients, conv4/5/6 data gradients, linear1 forward and weight "
                     "gradient; all of VGG); fp32 MFMA for the rest",
             "data": f"synthetic: seeded CIFAR-shaped u8 pool in HBM, "
                     + (f"{args.model} warm-started from {os.path.basename(args.model_file)}"

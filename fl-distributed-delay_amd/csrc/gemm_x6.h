@@ -268,40 +268,51 @@ gemm_x6_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, in
     if constexpr (WAVES_M * WAVES_N == 8) {
         if (wave >= 4) __builtin_amdgcn_s_setprio(1);
     }
+    // The main loop in two compiled forms, chosen per wave before it starts: with the bias column
+    // sum (ASUM: the waves that hold it in the tn = 0 blocks) and without.  A branch around the
+    // column sum inside the loop cost every block 4-9 % (the compiler then drains the stage's LDS
+    // stores before it; lab: conv6 weight gradient 9.76 ms with the branch, 8.93 ms without any
+    // column sum, profiles/r04/r04h/lab_wg.txt)
     int cur = 0;
-    for (int ks = ks0; ks < ks1; ++ks) {
-        if (ks + 1 < ks1) {
-            stage(lds + (cur ^ 1) * BUF);
-            if (ks + 2 < ks1) {
-                al.load(ks + 2, ra);
-                bl.load(ks + 2, rb);
+    auto main_loop = [&](auto with_sum) {
+        constexpr bool WS = decltype(with_sum)::value;
+        for (int ks = ks0; ks < ks1; ++ks) {
+            if (ks + 1 < ks1) {
+                stage(lds + (cur ^ 1) * BUF);
+                if (ks + 2 < ks1) {
+                    al.load(ks + 2, ra);
+                    bl.load(ks + 2, rb);
+                }
             }
-        }
-        const float* A = lds + cur * BUF;
-        const float* B = A + TA::FL;
-        if constexpr (EPI::ASUM && !AMF) {
-            if (tn == 0 && tid < BM) asum += TA::colsum(A, tid);
-        }
-        typename TB::Frag bf[FN];
+            const float* A = lds + cur * BUF;
+            const float* B = A + TA::FL;
+            if constexpr (WS && !AMF) {
+                if (tid < BM) asum += TA::colsum(A, tid);
+            }
+            typename TB::Frag bf[FN];
 #pragma unroll
-        for (int j = 0; j < FN; ++j) bf[j] = TB::frag(B, wn * 16 * FN + 16 * j, lane);
+            for (int j = 0; j < FN; ++j) bf[j] = TB::frag(B, wn * 16 * FN + 16 * j, lane);
 #pragma unroll
-        for (int i = 0; i < FM; ++i) {
-            const typename TA::Frag af = TA::frag(A, wm * 16 * FM + 16 * i, lane);
-            if constexpr (AMF) {
-                if (bwave) {
+            for (int i = 0; i < FM; ++i) {
+                const typename TA::Frag af = TA::frag(A, wm * 16 * FM + 16 * i, lane);
+                if constexpr (WS && AMF) {
                     bacc[i] = mfma_x32(af.x1, bf16_ones(false, true), bacc[i]);   // l
                     bacc[i] = mfma_x32(af.x0, bf16_ones(true, true), bacc[i]);    // h + m
                 }
-            }
 #pragma unroll
-            for (int j = 0; j < FN; ++j) {
-                acc[i][j] = x6_step(acc[i][j], af.x0, af.x1, bf[j].x0, bf[j].x1, bf[j].x2);
+                for (int j = 0; j < FN; ++j) {
+                    acc[i][j] = x6_step(acc[i][j], af.x0, af.x1, bf[j].x0, bf[j].x1, bf[j].x2);
+                }
             }
+            __syncthreads();
+            cur ^= 1;
         }
-        __syncthreads();
-        cur ^= 1;
-    }
+    };
+    bool sum_wave = false;
+    if constexpr (AMF) sum_wave = bwave;
+    else if constexpr (EPI::ASUM) sum_wave = tn == 0 && wave * 64 < BM;
+    if (sum_wave) main_loop(std::true_type{});
+    else main_loop(std::false_type{});
 
     if constexpr (AMF) {
         // every column of the ones product is the row sum: lanes of column 0 store it
