@@ -269,10 +269,10 @@ gemm_x6_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, in
         if (wave >= 4) __builtin_amdgcn_s_setprio(1);
     }
     // The main loop in two compiled forms, chosen per wave before it starts: with the bias column
-    // sum (ASUM: the waves that hold it in the tn = 0 blocks) and without.  A branch around the
-    // column sum inside the loop cost every block 4-9 % (the compiler then drains the stage's LDS
-    // stores before it; lab: conv6 weight gradient 9.76 ms with the branch, 8.93 ms without any
-    // column sum, profiles/r04/r04h/lab_wg.txt)
+    // sum (ASUM: the waves that hold it in the tn = 0 blocks) and without.  With the sum behind a
+    // branch inside the loop the weight gradients ran 2-9 % slower than with no sum at all
+    // (conv6 9.76 against 8.93 ms, profiles/r04/r04h/lab_wg.txt); chosen per wave and taken on the
+    // MFMA (AsumMfma) they run within 1.3 % of that, or faster (profiles/r04/r04i/lab_wg.txt)
     int cur = 0;
     auto main_loop = [&](auto with_sum) {
         constexpr bool WS = decltype(with_sum)::value;

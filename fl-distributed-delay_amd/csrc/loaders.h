@@ -768,6 +768,7 @@ struct EpiDropScatterRows {
 // the slabs): those blocks store instead of accumulating
 struct EpiSlabAcc {
     static constexpr bool ASUM = true;
+    static constexpr bool ASUM_MFMA = true;     // split-bf16 kernels: the column sum on the MFMA
     float* S;
     int M, N;
     long zstride;

@@ -123,7 +123,11 @@ static void conv(const char* tag, const float* X, const Xs& Xx, const float* W, 
 struct EpiSlabAccNA : EpiSlabAcc {
     static constexpr bool ASUM = false;
 };
-// ... and with the column sum on the matrix cores (gemm_x6.h AsumMfma)
+// ... with the column sum on the vector unit (the round-3 form), and on the matrix cores (the
+// product's EpiSlabAcc, gemm_x6.h AsumMfma)
+struct EpiSlabAccValu : EpiSlabAcc {
+    static constexpr bool ASUM_MFMA = false;
+};
 struct EpiSlabAccMF : EpiSlabAcc {
     static constexpr bool ASUM_MFMA = true;
 };
@@ -163,10 +167,13 @@ static void wgrad(const char* tag, const float* dz, const Xs& dzx, const float* 
     const int tm = ceil_div(CO, BM), tn = ceil_div(KP, BN);
     const double flops = 2.0 * M * CO * KP;
     EpiSlabAcc e0{S0, CO, KP, (long)CO * KP, B0, 0}, e1{S1, CO, KP, (long)CO * KP, B1, 0};
-    const double t0 = timeit(gemm_x6_kernel<FM, FN, WM, WN, AL, BL, EpiSlabAcc>,
-                             dim3(tm * tn * Z), NT, al, bl, e0, ks, per, tm, tn);
-    const double t1 = timeit(gemm_x6_kernel<FM, FN, WM, WN, ALs, BLs, EpiSlabAcc>,
-                             dim3(tm * tn * Z), NT, als, bls, e1, ks, per, tm, tn);
+    EpiSlabAccValu v0, v1;
+    static_cast<EpiSlabAcc&>(v0) = e0;
+    static_cast<EpiSlabAcc&>(v1) = e1;
+    const double t0 = timeit(gemm_x6_kernel<FM, FN, WM, WN, AL, BL, EpiSlabAccValu>,
+                             dim3(tm * tn * Z), NT, al, bl, v0, ks, per, tm, tn);
+    const double t1 = timeit(gemm_x6_kernel<FM, FN, WM, WN, ALs, BLs, EpiSlabAccValu>,
+                             dim3(tm * tn * Z), NT, als, bls, v1, ks, per, tm, tn);
     const size_t d = ndiff(S0, S1, (size_t)Z * CO * KP), db = ndiff(B0, B1, (size_t)Z * CO);
     EpiSlabAccNA e2;
     static_cast<EpiSlabAcc&>(e2) = e1;
@@ -187,8 +194,8 @@ static void wgrad(const char* tag, const float* dz, const Xs& dzx, const float* 
         den += (double)hb1[i] * hb1[i];
     }
     auto tf = [&](double t) { return flops / (t * 1e-3) / 1e12; };
-    printf("%-16s x6 %3dx%3d Z %4d %7.3f ms %6.1f | xs %7.3f ms %6.1f | xs no-bias-sum %7.3f ms "
-           "%6.1f | xs mfma-bias-sum %7.3f ms %6.1f TF/s | differ slab %zu bias %zu | mfma bias "
+    printf("%-16s x6 %3dx%3d Z %4d %7.3f ms %6.1f | xs (valu bias sum) %7.3f ms %6.1f | xs no-bias-sum "
+           "%7.3f ms %6.1f | xs mfma-bias-sum %7.3f ms %6.1f TF/s | differ slab %zu bias %zu | mfma bias "
            "rel-L2 vs valu %.2e\n",
            tag, BM, BN, Z, t0, tf(t0), t1, tf(t1), t2, tf(t2), t3, tf(t3), d, db,
            std::sqrt(num / (den > 0 ? den : 1)));
@@ -233,6 +240,22 @@ int main(int argc, char** argv) {
     C("dg4", 22, 96, 0, 0, 96, 4, 3, 4, 2, 2, 6, 8, 3, 2, 2)
     C("dg3", 20, 96, 0, 0, 48, 8, 3, 4, 1, 2, 3, 8, 3, 2, 2)
     C("dg2", 36, 48, 0, 0, 48, 4, 3, 8, 1, 2, 3, 8, 3, 2, 2)
+    // conv2 forward: direct-kernel variants (DFM DFN waves KB DEPTH NPL) beside the product's 2 3 8 3 2 2
+    C("fwd2v a", 34, 48, 2, 0, 48, 4, 3, 8, 1, 4, 3, 8, 3, 2, 2)
+    C("fwd2v b", 34, 48, 2, 0, 48, 4, 3, 8, 1, 2, 3, 4, 3, 2, 2)
+    C("fwd2v c", 34, 48, 2, 0, 48, 4, 3, 8, 1, 2, 3, 8, 6, 2, 2)
+    C("fwd2v d", 34, 48, 2, 0, 48, 4, 3, 8, 1, 2, 3, 8, 4, 3, 2)
+    C("fwd2v e", 34, 48, 2, 0, 48, 4, 3, 8, 1, 4, 3, 4, 3, 2, 2)
+    C("fwd2v f", 34, 48, 2, 0, 48, 4, 3, 8, 1, 2, 3, 8, 2, 1, 2)
+    C("fwd2v g", 34, 48, 2, 0, 48, 4, 3, 8, 1, 3, 3, 8, 3, 2, 2)
+    // weight-gradient tile variants for conv3 / conv2 (product: wg3 3 3 2 1, wg2 3 3 1 3)
+    G("wg3v 96x96x4", 18, 48, 96, 1024, 3, 3, 2, 2)
+    G("wg3v 96x144x2", 18, 48, 96, 1024, 3, 9, 2, 1)
+    G("wg3v 96x144x6", 18, 48, 96, 1024, 3, 3, 2, 3)
+    G("wg3v 48x48x1", 18, 48, 96, 1024, 3, 3, 1, 1)
+    G("wg2v 48x144x1", 34, 48, 48, 4096, 3, 9, 1, 1)
+    G("wg2v 48x48x1", 34, 48, 48, 4096, 3, 3, 1, 1)
+    G("wg2v 48x96x2", 34, 48, 48, 4096, 3, 3, 1, 2)
     // weight gradients (product tiles and splits: >= 32 k-steps per split)
     G("wg6", 13, 192, 192, 256, 6, 3, 2, 2)
     G("wg5", 11, 96, 192, 512, 6, 3, 2, 2)
