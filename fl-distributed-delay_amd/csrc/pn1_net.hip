@@ -310,19 +310,21 @@ static int conv1_fwd(const float* x0, const float* W, const float* bias, XsT a1,
     return probe_end(ps, K_FWD1, 2.0 * M * 48 * 27);
 }
 
-// The conv2-6 forward and data-gradient GEMMs: split operands on the direct-A kernel
-// (gemm_dx6.h); DX_FM rows per wave and 8 waves per block, B staged DX_KB k-steps at a time.
-// Chunks of at most small_chunk_samples() samples take 128-row blocks (DX_FMS): the same
-// arithmetic per output (bit-identical), twice the blocks.
-constexpr int DX_FM = 2, DX_FMS = 1, DX_KB = 3, DX_DEPTH = 2, DX_NPL = 2;
+// The conv2-4 forward GEMMs: split operands on the direct-A kernel (gemm_dx6.h); FM fragments
+// of 16 rows per wave (16 FM x WAVES rows per block), B staged DX_KB k-steps at a time.  Chunks of
+// at most small_chunk_samples() samples take half-height blocks: the same arithmetic per output
+// (bit-identical), twice the blocks.  conv2 (N = 48) runs 64-row waves, 4 per block: 6.67 against
+// 7.24 ms for 32-row waves, 8 per block (profiles/r04/r04j/lab_fwd2.txt, "fwd2v e")
+constexpr int DX_FM = 2, DX_KB = 3, DX_DEPTH = 2, DX_NPL = 2;
 
-template <int IH, int IW, int CI, int PAD, int FN, bool WIN, int OHX, class EPI>
+template <int IH, int IW, int CI, int PAD, int FN, bool WIN, int OHX, int FM = DX_FM,
+          int WAVES = 8, class EPI>
 static int dx6(XsT X, int S, XsT W, int N, int KP, const EPI& epi, hipStream_t st, int kid,
                int kreal) {
     if (S <= small_chunk_samples())
-        return conv_dx6<IH, IW, CI, PAD, DX_FMS, FN, 8, DX_KB, DX_DEPTH, DX_NPL, WIN, OHX>(
+        return conv_dx6<IH, IW, CI, PAD, FM / 2, FN, WAVES, DX_KB, DX_DEPTH, DX_NPL, WIN, OHX>(
             X, S, W, N, KP, epi, st, kid, kreal);
-    return conv_dx6<IH, IW, CI, PAD, DX_FM, FN, 8, DX_KB, DX_DEPTH, DX_NPL, WIN, OHX>(
+    return conv_dx6<IH, IW, CI, PAD, FM, FN, WAVES, DX_KB, DX_DEPTH, DX_NPL, WIN, OHX>(
         X, S, W, N, KP, epi, st, kid, kreal);
 }
 
@@ -348,7 +350,7 @@ static int forward(const GradState& g, const WS& w, const float* theta, int S,
     // conv1 + ReLU (models.py:29), a1 written split
     RC(conv1_fwd(w.x0, theta + P_OFF[0], theta + P_OFF[1], a1, S, st));
     // conv2 + ReLU + pool1 + dropout1 (models.py:30-32), one fused launch -> d1 (split)
-    RC((dx6<34, 34, 48, 2, 3, true, 0>(a1, S, g.wfx[1], 48, 432,
+    RC((dx6<34, 34, 48, 2, 3, true, 0, 4, 4>(a1, S, g.wfx[1], 48, 432,
         EpiPoolDropXs<18, 18, 48>{d1.hm, d1.l, w.i1, theta + P_OFF[3], workers, seed, SITE_DROP1,
                                   THR_P25, SCALE_P25, dropout, S * 18 * 18 * 4}, st, K_FWD2, 432)));
     // conv3 + ReLU (models.py:33) -> a3 (split)
@@ -612,7 +614,8 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     // ---- conv3: wgrad (input d1), bias, dgrad -> grad wrt d1 (site 1), scattered through pool1
     //      straight into dz2 (a2 buffer, fp32) ----
     RC(fork());
-    RC((conv_wgrad_sz<18, 18, 48, 2, 3, 3, 2, 1, 3, 3, 2, 2, 0, false, true, BufSrc, XsSrc>(
+    // (96 x 96 tiles of 4 waves: 2.96 against 3.54 ms for 96 x 48 of 2, profiles/r04/r04j/lab_wg.txt)
+    RC((conv_wgrad_sz<18, 18, 48, 2, 3, 3, 2, 2, 3, 3, 2, 2, 0, false, true, BufSrc, XsSrc>(
         dz3, w.d1, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW, sw, K_WG3, 432, zi(2), &zu[2],
         nullptr, w.d1l)));
     // (gemm_kernel: the direct-A form measured 3.87 vs 3.78 ms with this staged epilogue, r03b)

@@ -240,15 +240,21 @@ int main(int argc, char** argv) {
     C("dg4", 22, 96, 0, 0, 96, 4, 3, 4, 2, 2, 6, 8, 3, 2, 2)
     C("dg3", 20, 96, 0, 0, 48, 8, 3, 4, 1, 2, 3, 8, 3, 2, 2)
     C("dg2", 36, 48, 0, 0, 48, 4, 3, 8, 1, 2, 3, 8, 3, 2, 2)
-    // conv2 forward: direct-kernel variants (DFM DFN waves KB DEPTH NPL) beside the product's 2 3 8 3 2 2
+    // conv2 forward: direct-kernel variants (DFM DFN waves KB DEPTH NPL) beside round 4's 2 3 8 3 2 2
+    // (KB must divide the 27 / 54 k-steps: r04j's KB 6 / 4 / 2 variants skipped k-steps)
     C("fwd2v a", 34, 48, 2, 0, 48, 4, 3, 8, 1, 4, 3, 8, 3, 2, 2)
     C("fwd2v b", 34, 48, 2, 0, 48, 4, 3, 8, 1, 2, 3, 4, 3, 2, 2)
-    C("fwd2v c", 34, 48, 2, 0, 48, 4, 3, 8, 1, 2, 3, 8, 6, 2, 2)
-    C("fwd2v d", 34, 48, 2, 0, 48, 4, 3, 8, 1, 2, 3, 8, 4, 3, 2)
     C("fwd2v e", 34, 48, 2, 0, 48, 4, 3, 8, 1, 4, 3, 4, 3, 2, 2)
-    C("fwd2v f", 34, 48, 2, 0, 48, 4, 3, 8, 1, 2, 3, 8, 2, 1, 2)
     C("fwd2v g", 34, 48, 2, 0, 48, 4, 3, 8, 1, 3, 3, 8, 3, 2, 2)
-    // weight-gradient tile variants for conv3 / conv2 (product: wg3 3 3 2 1, wg2 3 3 1 3)
+    C("fwd2v h", 34, 48, 2, 0, 48, 4, 3, 8, 1, 4, 3, 4, 9, 2, 2)
+    C("fwd2v i", 34, 48, 2, 0, 48, 4, 3, 8, 1, 2, 3, 8, 9, 2, 2)
+    C("fwd2v k", 34, 48, 2, 0, 48, 4, 3, 8, 1, 8, 3, 2, 3, 2, 2)
+    C("fwd2v l", 34, 48, 2, 0, 48, 4, 3, 8, 1, 4, 3, 2, 3, 2, 2)
+    // conv3 / conv4 forward (product: DFM 2, 8 waves, KB 3)
+    C("fwd3v a", 18, 48, 2, 0, 96, 4, 3, 4, 2, 4, 6, 4, 3, 2, 2)
+    C("fwd4v a", 20, 96, 2, 0, 96, 4, 3, 4, 2, 4, 6, 4, 3, 2, 2)
+    C("fwd4v b", 20, 96, 2, 0, 96, 4, 3, 4, 2, 2, 6, 8, 6, 2, 2)
+    // weight-gradient tile variants for conv3 / conv2 (product: wg3 3 3 2 2 since r04j, wg2 3 3 1 3)
     G("wg3v 96x96x4", 18, 48, 96, 1024, 3, 3, 2, 2)
     G("wg3v 96x144x2", 18, 48, 96, 1024, 3, 9, 2, 1)
     G("wg3v 96x144x6", 18, 48, 96, 1024, 3, 3, 2, 3)
