@@ -262,6 +262,16 @@ int main(int argc, char** argv) {
     G("wg2v 48x144x1", 34, 48, 48, 4096, 3, 9, 1, 1)
     G("wg2v 48x48x1", 34, 48, 48, 4096, 3, 3, 1, 1)
     G("wg2v 48x96x2", 34, 48, 48, 4096, 3, 3, 1, 2)
+    // weight-gradient tile variants for conv4 / conv5 / conv6 (product: 3 3 2 2 / 6 3 2 2 / 6 3 2 2)
+    G("wg4v 96x144x2", 20, 96, 96, 1024, 3, 9, 2, 1)
+    G("wg4v 96x144x6", 20, 96, 96, 1024, 3, 3, 2, 3)
+    G("wg4v 96x96x2", 20, 96, 96, 1024, 3, 6, 2, 1)
+    G("wg5v 192x144x6", 11, 96, 192, 512, 6, 3, 2, 3)
+    G("wg5v 192x96x8", 11, 96, 192, 512, 3, 3, 4, 2)
+    G("wg6v 192x192x4", 13, 192, 192, 256, 6, 6, 2, 2)
+    G("wg6v 192x144x6", 13, 192, 192, 256, 6, 3, 2, 3)
+    G("wg6v 192x96x8", 13, 192, 192, 256, 3, 3, 4, 2)
+    G("wg6v 192x192x8", 13, 192, 192, 256, 3, 6, 4, 2)
     // weight gradients (product tiles and splits: >= 32 k-steps per split)
     G("wg6", 13, 192, 192, 256, 6, 3, 2, 2)
     G("wg5", 11, 96, 192, 512, 6, 3, 2, 2)
