@@ -212,9 +212,6 @@ static int pack_weights(const GradState& g, const float* theta, hipStream_t st) 
 // channel): lane slot g holds tap 4s + g, so one float4 load of x0 (NHWC, channel 3 = 0) feeds the
 // four MFMAs.  Tap 8 is one MFMA whose k slot g is the input channel.  27 real MFMA k-values (plus
 // the zero 4th channel), 9 MFMAs per 16x16 output tile.
-#ifndef FLSIM_C1_PAIRS
-#define FLSIM_C1_PAIRS 1
-#endif
 constexpr int C1_ROWS = 32;     // output pixels per wave iteration (two 16-row tiles)
 constexpr int C1_LD = 52;       // staging row stride (floats): 16-B aligned, rows on different banks
 __global__ void __launch_bounds__(256)
@@ -287,30 +284,15 @@ k_conv1_fwd(const float* __restrict__ x0, const float* __restrict__ W, const flo
                 for (int r = 0; r < 4; ++r)
                     st[(16 * t + 4 * g + r) * C1_LD + 16 * j + i] = fmaxf(acc[t][j][r] + bj[j], 0.f);
         __builtin_amdgcn_wave_barrier();
-        // a1 in the split form (split.h): each lane splits two consecutive 4-channel units of a
-        // row, so its L part leaves as one 16-B store (FLSIM_C1_PAIRS=0: one unit per lane, the
-        // L part as 8-B stores)
-#if FLSIM_C1_PAIRS
-#pragma unroll
-        for (int q0 = 0; q0 < C1_ROWS * 6; q0 += 64) {
-            const int q = q0 + lane, row = q / 6, c8 = q - (q / 6) * 6;
-            const float* src = st + row * C1_LD + 8 * c8;
-            const XsUnit x0 = xs_of(*reinterpret_cast<const f32x4*>(src));
-            const XsUnit x1 = xs_of(*reinterpret_cast<const f32x4*>(src + 4));
-            const long u0 = u * C1_ROWS * 12 + 2 * q;        // even: the L pair is 16-B aligned
-            __builtin_nontemporal_store(x0.hm, reinterpret_cast<f32x4*>(a1) + u0);
-            __builtin_nontemporal_store(x1.hm, reinterpret_cast<f32x4*>(a1) + u0 + 1);
-            __builtin_nontemporal_store(f32x4{x0.l.x, x0.l.y, x1.l.x, x1.l.y},
-                                        reinterpret_cast<f32x4*>(a1l) + u0 / 2);
-        }
-#else
+        // a1 in the split form (split.h): each lane splits whole 4-channel units of its rows.
+        // (Two units per lane, their L parts as one 16-B store, measured 2.06 against 1.23 ms:
+        // the lanes' HM stores then land 32 B apart, half lines per instruction; profiles/r04/r04l)
 #pragma unroll
         for (int q0 = 0; q0 < C1_ROWS * 12; q0 += 64) {
             const int q = q0 + lane, row = q / 12, c4 = q - (q / 12) * 12;
             xs_store(a1, a1l, u * C1_ROWS * 12 + q,
                      *reinterpret_cast<const f32x4*>(st + row * C1_LD + 4 * c4));
         }
-#endif
         __builtin_amdgcn_wave_barrier();
     }
 }
@@ -603,7 +585,9 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     const XsT dz6 = w.x(w.a6, w.a6l), dz5 = w.x(w.gx, w.gxl), dz4 = w.x(w.a4, w.a4l);
     // ---- conv6: wgrad (input a5), bias, dgrad -> dz5 = . * (a5 > 0) into gx (split) ----
     RC(fork());
-    RC((conv_wgrad_sz<13, 13, 192, 2, 6, 3, 2, 2, 3, 3, 2, 2, 14, true, true, XsSrc>(
+    // (192 x 192 tiles of 8 waves: 9.10-9.13 against 9.41 ms for 192 x 96 of 4,
+    // profiles/r04/r04l/lab_wg6v.txt)
+    RC((conv_wgrad_sz<13, 13, 192, 2, 3, 6, 4, 2, 3, 3, 2, 2, 14, true, true, XsSrc>(
         dz6.hm, w.a5, S, 192, 1728, g.sw[5], g.sb[5], GEO[5].ZW, sw, K_WG6, 1728, zi(5), &zu[5],
         dz6.l, w.a5l)));
     RC((xs<14, 14, 192, 0, 4, 6, 4, 2, false, 13>(dz6, S, g.wdx[5], 192, 1728,

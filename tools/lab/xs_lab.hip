@@ -262,6 +262,17 @@ int main(int argc, char** argv) {
     G("wg2v 48x144x1", 34, 48, 48, 4096, 3, 9, 1, 1)
     G("wg2v 48x48x1", 34, 48, 48, 4096, 3, 3, 1, 1)
     G("wg2v 48x96x2", 34, 48, 48, 4096, 3, 3, 1, 2)
+    // staged (xs) tile variants for the N = 192 / 96 forward and data-gradient GEMMs
+    // (product: fwd5/fwd6/dg6 4 6 4 2, dg4/dg5 4 3 4 2)
+    C("fwd6v a", 13, 192, 2, 0, 192, 3, 6, 4, 2, 2, 6, 8, 3, 2, 2)
+    C("fwd6v b", 13, 192, 2, 0, 192, 2, 6, 4, 2, 2, 6, 8, 3, 2, 2)
+    C("dg6v a", 14, 192, 0, 13, 192, 3, 6, 4, 2, 2, 6, 8, 3, 2, 2)
+    C("dg6v b", 14, 192, 0, 13, 192, 2, 6, 4, 2, 2, 6, 8, 3, 2, 2)
+    C("fwd5v a", 11, 96, 2, 0, 192, 3, 6, 4, 2, 2, 6, 8, 3, 2, 2)
+    C("dg5v a", 13, 192, 0, 0, 96, 4, 6, 4, 1, 2, 6, 8, 3, 2, 2)
+    C("dg5v b", 13, 192, 0, 0, 96, 2, 3, 4, 2, 2, 6, 8, 3, 2, 2)
+    C("dg4v a", 22, 96, 0, 0, 96, 4, 6, 4, 1, 2, 6, 8, 3, 2, 2)
+    C("dg4v b", 22, 96, 0, 0, 96, 2, 3, 4, 2, 2, 6, 8, 3, 2, 2)
     // weight-gradient tile variants for conv4 / conv5 / conv6 (product: 3 3 2 2 / 6 3 2 2 / 6 3 2 2)
     G("wg4v 96x144x2", 20, 96, 96, 1024, 3, 9, 2, 1)
     G("wg4v 96x144x6", 20, 96, 96, 1024, 3, 3, 2, 3)
