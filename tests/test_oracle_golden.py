@@ -149,9 +149,11 @@ def test_training_trajectory(golden, thr):
     for t in range(len(ref_losses)):
         loss = sim.epoch()
         # the first two epochs agree to the last bits; later ones drift with the host CPU's fp32
-        # kernels (Adam turns 1-ulp gradient differences into O(lr) moves): 1.2e-4 at
-        # epoch 4 on an EPYC build host whose oneDNN paths differ from the golden generator's
-        tol = 1e-6 if t < 2 else 1e-3
+        # kernels (Adam turns 1-ulp gradient differences into O(lr) moves).  Measured on
+        # the build host against the golden f32 losses: thr0 4.8e-7 / 2.6e-5 / 1.2e-4 at epochs
+        # 2 / 3 / 4, thr1 0 throughout (the golden f32 run itself is 6.1e-7 / 1.5e-6 / 6.8e-5
+        # from the golden f64 one); bounds 8-20x those
+        tol = (1e-6, 1e-6, 1e-5, 2e-4, 1e-3)[min(t, 4)]
         assert abs(loss - ref_losses[t]) <= tol, (t, loss, ref_losses[t])
         n_entries, n_distinct = g[f"{key}_comp{t}"]
         assert len(sim.trace[-1]["appended"]) == n_entries
