@@ -20,6 +20,7 @@
 #include <mutex>
 #include <unordered_map>
 
+#include "c1fuse.h"
 #include "net_kernels.h"
 #include "slabstep.h"
 
@@ -535,6 +536,17 @@ static int debug_stop() {
     return v;
 }
 
+// conv1's weight gradient inside conv2's data gradient (c1fuse.h); FLSIM_C1_FUSE=0 (measurement)
+// runs the two GEMMs apart, through dz1 in HBM
+static bool fuse_conv1() {
+    static int f = -1;
+    if (f < 0) {
+        const char* e = getenv("FLSIM_C1_FUSE");
+        f = e ? atoi(e) != 0 : 1;
+    }
+    return f != 0;
+}
+
 static int backward(const GradState& g, const WS& w, const float* theta, int S, int dropout,
                     hipStream_t st, EpochRows* er) {
     constexpr int ALL = 0x7fffffff;
@@ -633,13 +645,20 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC((conv_wgrad_sz<34, 34, 48, 2, 3, 3, 1, 3, 3, 3, 1, 3, 0, false, true, BufSrc, XsSrc>(
         dz2, w.a1, S, 48, 432, g.sw[1], g.sb[1], GEO[1].ZW, sw, K_WG2, 432, zi(1), &zu[1],
         nullptr, w.a1l)));
-    RC((conv_direct_sz<36, 36, 48, 0, 2, 1, 3, 8, 3, 2, false, 0>(dz2, S, g.wd[1], 48, 432,
-        EpiMaskXs<48, false>{w.gx, nullptr, w.a1, S * 34 * 34}, st, K_DG2, 432)));
-    float* dz1 = w.gx;
-    // ---- conv1: wgrad (input x0), bias ----
-    // (3 waves of 16 rows each: 0.272 vs 0.325 ms for one 48x48 wave, profiles/r01c/lab_conv1.txt)
-    RC((conv_wgrad<32, 32, 4, 2, 1, 3, 3, 1>(dz1, w.x0, S, 48, 48, g.sw[0], g.sb[0], GEO[0].ZW, st,
-                                            K_WG1, 27, zi(0), &zu[0])));
+    if (fuse_conv1()) {
+        // ---- conv2's dgrad with conv1's wgrad + bias fused in (c1fuse.h): dz1 stays on chip ----
+        RC((conv2_dgrad_conv1_wgrad<2, 1, 3, 8, 3, 2>(dz2, S, g.wd[1], 432, w.a1, w.x0, g.sw[0],
+                                                       g.sb[0], GEO[0].ZW, 48, zi(0), &zu[0], st,
+                                                       K_DG2)));
+    } else {
+        RC((conv_direct_sz<36, 36, 48, 0, 2, 1, 3, 8, 3, 2, false, 0>(dz2, S, g.wd[1], 48, 432,
+            EpiMaskXs<48, false>{w.gx, nullptr, w.a1, S * 34 * 34}, st, K_DG2, 432)));
+        float* dz1 = w.gx;
+        // ---- conv1: wgrad (input x0), bias ----
+        // (3 waves of 16 rows each: 0.272 vs 0.325 ms for one 48x48 wave, profiles/r01c/lab_conv1.txt)
+        RC((conv_wgrad<32, 32, 4, 2, 1, 3, 3, 1>(dz1, w.x0, S, 48, 48, g.sw[0], g.sb[0], GEO[0].ZW,
+                                                st, K_WG1, 27, zi(0), &zu[0])));
+    }
     RC(join());                                   // the next chunk's forward rewrites a1, a2
     if (er)
         for (int i = 0; i < 8; ++i)
