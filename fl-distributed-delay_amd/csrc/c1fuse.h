@@ -34,7 +34,7 @@ struct C1Fuse {
 // accumulator registers; a partial spread over all 8 waves took 24 and cost the main loop its
 // occupancy or spilled its address registers into scratch).
 template <int FM, int FN, int WAVES, int KB, int DEPTH, class AD, class BL>
-__global__ void __launch_bounds__(64 * WAVES)
+__global__ void __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(4, 8)))
 k_dgrad2_wgrad1(AD ad, BL bl, C1Fuse c, int ksteps) {
     constexpr int BM = 16 * FM * WAVES;
     constexpr int BN = 16 * FN;
@@ -118,25 +118,15 @@ k_dgrad2_wgrad1(AD ad, BL bl, C1Fuse c, int ksteps) {
             __syncthreads();
         }
         // ---- epilogue: dz1 rows masked in LDS, times conv1's input columns ----
+        // Per pass: the pass's global loads (mask h parts, x0 values) go out first, under the
+        // accumulator writes and the barrier; the main loop's last barrier already freed the LDS
+        // for pass 0.  The partial product runs as four independent MFMA chains (16 x 16 x 4 f32:
+        // a dependent chain waits out each MFMA's latency), summed into cacc at the pass end.
 #pragma unroll 1
         for (int pass = 0; pass < PASSES; ++pass) {
-            __syncthreads();
             float* T = lds + T_OFF;
             float* X = lds + X_OFF;
-            if (wave / WM_PASS == pass) {
-#pragma unroll
-                for (int i = 0; i < FM; ++i)
-#pragma unroll
-                    for (int j = 0; j < FN; ++j) {
-                        const int ml = (wave - pass * WM_PASS) * WROWS + 16 * i + 4 * (lane >> 4);
-                        const int nl = 16 * j + (lane & 15);
-#pragma unroll
-                        for (int rr = 0; rr < 4; ++rr) T[(ml + rr) * TLD + nl] = acc[i][j][rr];
-                    }
-            }
-            __syncthreads();
             const int mp = m0 + pass * PR;
-            // the mask units' h parts and the x0 values, all loads issued before any store
             constexpr int MU = PR * 12 / NT, XU = PR * 32 / NT;
             static_assert(PR * 12 % NT == 0 && PR * 32 % NT == 0, "whole units per thread");
             f32x2 hv[MU];
@@ -167,11 +157,17 @@ k_dgrad2_wgrad1(AD ad, BL bl, C1Fuse c, int ksteps) {
                 }
                 xv[it] = v;
             }
+            if (pass > 0) __syncthreads();           // the previous pass's MFMAs read T, X
+            if (wave / WM_PASS == pass) {
 #pragma unroll
-            for (int it = 0; it < MU; ++it) {
-                const int q = tid + it * NT, r = q / 12, cu = q - r * 12;
-                f32x4* p = reinterpret_cast<f32x4*>(T + r * TLD + 4 * cu);
-                *p = mask4(*p, xs_pos4(hv[it]));     // rows past M: h = 0, masked to zero
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int j = 0; j < FN; ++j) {
+                        const int ml = (wave - pass * WM_PASS) * WROWS + 16 * i + 4 * (lane >> 4);
+                        const int nl = 16 * j + (lane & 15);
+#pragma unroll
+                        for (int rr = 0; rr < 4; ++rr) T[(ml + rr) * TLD + nl] = acc[i][j][rr];
+                    }
             }
 #pragma unroll
             for (int it = 0; it < XU; ++it) {
@@ -179,14 +175,23 @@ k_dgrad2_wgrad1(AD ad, BL bl, C1Fuse c, int ksteps) {
                 X[(q >> 5) * XLD + (q & 31)] = xv[it];
             }
             __syncthreads();
+#pragma unroll
+            for (int it = 0; it < MU; ++it) {
+                const int q = tid + it * NT, r = q / 12, cu = q - r * 12;
+                f32x4* p = reinterpret_cast<f32x4*>(T + r * TLD + 4 * cu);
+                *p = mask4(*p, xs_pos4(hv[it]));     // rows past M: h = 0, masked to zero
+            }
+            __syncthreads();
             // channels [16 pi, +16) x columns [16 pj, +16) over the pass's rows, 4 rows per MFMA
             if (wave < 6) {
-#pragma unroll 8
+                f32x4 ch[4] = {zero4(), zero4(), zero4(), zero4()};
+#pragma unroll
                 for (int s = 0; s < PR / 4; ++s) {
                     const int r = 4 * s + (lane >> 4);
-                    cacc = mfma16(T[r * TLD + 16 * pi + (lane & 15)],
-                                  X[r * XLD + 16 * pj + (lane & 15)], cacc);
+                    ch[s & 3] = mfma16(T[r * TLD + 16 * pi + (lane & 15)],
+                                       X[r * XLD + 16 * pj + (lane & 15)], ch[s & 3]);
                 }
+                cacc += (ch[0] + ch[1]) + (ch[2] + ch[3]);
             }
         }
         __syncthreads();                         // the next tile's B stage reuses this LDS
