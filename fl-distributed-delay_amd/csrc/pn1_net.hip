@@ -536,13 +536,15 @@ static int debug_stop() {
     return v;
 }
 
-// conv1's weight gradient inside conv2's data gradient (c1fuse.h); FLSIM_C1_FUSE=0 (measurement)
-// runs the two GEMMs apart, through dz1 in HBM
+// conv1's weight gradient inside conv2's data gradient (c1fuse.h) with FLSIM_C1_FUSE=1.  Not the
+// default: the fused launch took 7.27-7.29 ms against 6.14-6.17 + 0.87-0.88 ms for the two GEMMs
+// apart (headline 1331.8 / 1335.1 against 1342.7 / 1346.3 worker-steps/s, profiles/r04/r04n,
+// r04o): its epilogue holds the data gradient at two blocks per CU instead of three
 static bool fuse_conv1() {
     static int f = -1;
     if (f < 0) {
         const char* e = getenv("FLSIM_C1_FUSE");
-        f = e ? atoi(e) != 0 : 1;
+        f = e ? atoi(e) != 0 : 0;
     }
     return f != 0;
 }

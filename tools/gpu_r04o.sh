@@ -14,7 +14,7 @@ echo "pytest rc $rc"; tail -2 $OUT/pytest_gpu.txt; grep -E "^FAILED" $OUT/pytest
 timeout -k 10 400 python3 -u bench.py --no-cpu-baseline > $OUT/bench.json 2> $OUT/bench.err \
     || { echo "bench failed $?"; tail -5 $OUT/bench.err; exit 1; }
 python3 tools/bench_summary.py $OUT/bench.json > $OUT/bench.txt; head -9 $OUT/bench.txt
-FLSIM_C1_FUSE=0 timeout -k 10 400 python3 -u bench.py --no-cpu-baseline > $OUT/bench_unfused.json 2> $OUT/bench_unfused.err \
+FLSIM_C1_FUSE=1 timeout -k 10 400 python3 -u bench.py --no-cpu-baseline > $OUT/bench_unfused.json 2> $OUT/bench_unfused.err \
     || { echo "bench unfused failed $?"; tail -5 $OUT/bench_unfused.err; exit 1; }
 python3 tools/bench_summary.py $OUT/bench_unfused.json > $OUT/bench_unfused.txt; head -9 $OUT/bench_unfused.txt
 echo r04o-ok
