@@ -314,95 +314,6 @@ __global__ void __launch_bounds__(256) k_agg_stream_reg(AggArgs A) {
     }
 }
 
-// The reference-order stream as a persistent, software-pipelined loop (FLSIM_AGG_PIPE=1): a grid
-// of resident blocks walks the 1024-element chunks of k_agg_stream_reg<1, NY> (block b: chunks b,
-// b + nstream, ...; edge-covered chunks skipped, edge pieces as there), and each thread issues the
-// next chunk's loads before it runs the current chunk's program and Adam, so every wave keeps a
-// chunk of loads in flight while it computes.  Same arithmetic per element.
-template <int NY>
-__global__ void __launch_bounds__(256) k_agg_stream_pipe(AggArgs A, int nchunks, int nstream) {
-    const ProgRef<true> prog{A.R};
-    const int tid = threadIdx.x;
-    if ((int)blockIdx.x < A.nedge) {
-        const long e = A.edge_lo[blockIdx.x] + tid;
-        if (e < A.lo || e >= A.hi) return;
-        const float x = A.S[e];
-        float p = A.p[e], m = A.m[e], v = A.v[e];
-        auto yf = [&](int q) -> float { return A.R.arr[q] ? A.R.arr[q][e] : 0.f; };
-        const CascVals<float> cv = casc_values(x, A.R.info.need, A.R.info.lp);
-        const bool tail = in_tail(A, e);
-        float s = 0.f;
-        if (!tail) s = casc_run_macro(prog, 0, cv, yf);
-        if (tail) s = casc_run_macro(prog, A.R.info.tail_off, cv, yf);
-        adam_elem(A.ac, s, p, m, v);
-        A.p[e] = p;
-        A.m[e] = m;
-        A.v[e] = v;
-        if (A.S_out) A.S_out[e] = x;
-        return;
-    }
-    auto ld = [](const float* ptr) -> f32x4 {
-        return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(ptr));
-    };
-    auto st = [](float* ptr, f32x4 val) {
-        __builtin_nontemporal_store(val, reinterpret_cast<f32x4*>(ptr));
-    };
-    struct Grp {
-        f32x4 x, p, m, v, y[NY > 0 ? NY : 1];
-    };
-    auto elem = [&](int c) { return 4 * (A.g0 + (long)c * 256) + 4 * tid; };
-    auto load = [&](int c, Grp& g) {
-        const long e = elem(c);
-#pragma unroll
-        for (int q = 0; q < NY; ++q)
-            g.y[q] = A.R.arr[q] ? ld(A.R.arr[q] + e) : f32x4{0.f, 0.f, 0.f, 0.f};
-        g.x = ld(A.S + e);
-        g.p = ld(A.p + e);
-        g.m = ld(A.m + e);
-        g.v = ld(A.v + e);
-    };
-    // the block's next chunk after c that no edge piece covers (uniform)
-    auto next = [&](int c) {
-        for (c += nstream; c < nchunks && block_touch(A, 4 * (A.g0 + (long)c * 256)); c += nstream) {
-        }
-        return c;
-    };
-    int c = (int)blockIdx.x - A.nedge;
-    if (c < nchunks && block_touch(A, 4 * (A.g0 + (long)c * 256))) c = next(c);
-    if (c >= nchunks) return;
-    Grp cur;
-    load(c, cur);
-    for (;;) {
-        const int cn = next(c);
-        Grp nxt;
-        if (cn < nchunks) load(cn, nxt);
-        const long e = elem(c);
-        auto yf = [&](int q) -> f32x4 {
-            if constexpr (NY == 0) return f32x4{0.f, 0.f, 0.f, 0.f};
-            else if constexpr (NY == 1) return cur.y[0];
-            else return q == 0 ? cur.y[0] : cur.y[1];
-        };
-        const f32x4 sum = casc_run_macro<true>(
-            prog, 0, casc_values(cur.x, A.R.info.need, A.R.info.lp), yf);
-        f32x4 p = cur.p, m = cur.m, v = cur.v;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            float pp = p[u], mm = m[u], vv = v[u];
-            adam_elem(A.ac, sum[u], pp, mm, vv);
-            p[u] = pp;
-            m[u] = mm;
-            v[u] = vv;
-        }
-        st(A.p + e, p);
-        st(A.m + e, m);
-        st(A.v + e, v);
-        if (A.S_out) st(A.S_out + e, cur.x);
-        if (cn >= nchunks) break;
-        c = cn;
-        cur = nxt;
-    }
-}
-
 // ================================================================================================
 // k_slab_step: slabs -> S_t [-> S_out] [-> rule() + Adam], one launch
 // ================================================================================================
@@ -1049,10 +960,7 @@ int flsim_aggregate_adam_rule_push(const float* S, float* S_out, const flsim_rul
     if (const char* e = getenv("FLSIM_AGG_G")) agg_g = atoi(e);
     if (agg_g < 0 || agg_g > AGG_GMAX) agg_g = 1;
     const bool reg = A.R.prog == nullptr && A.R.narr <= 2 && agg_g > 0;
-    // FLSIM_AGG_PIPE=1: the persistent pipelined form of the register stream (chunks of G = 1)
-    const char* pe = getenv("FLSIM_AGG_PIPE");
-    const bool pipe = reg && pe && atoi(pe) != 0;
-    const int G = reg && !pipe ? agg_g : 1;
+    const int G = reg ? agg_g : 1;
     A.S = S;
     A.S_out = S_out;
     A.p = p;
@@ -1113,22 +1021,7 @@ int flsim_aggregate_adam_rule_push(const float* S, float* S_out, const flsim_rul
         const double bytes = 4.0 * (double)(hi - lo) * (7 + A.R.distinct + (S_out ? 1 : 0));
         const ProbeSlot ps = probe_begin();
         const dim3 grid((unsigned)(nblk + A.nedge));
-        if (pipe) {
-            auto k = A.R.narr == 0 ? k_agg_stream_pipe<0>
-                                   : A.R.narr == 1 ? k_agg_stream_pipe<1> : k_agg_stream_pipe<2>;
-            static int cap[3] = {0, 0, 0};
-            int& cp = cap[A.R.narr];
-            if (!cp) {
-                int dev = 0, cus = 0, per = 0;
-                FLSIM_CHECK_HIP(hipGetDevice(&dev));
-                FLSIM_CHECK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-                FLSIM_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, 256, 0));
-                cp = cus * (per > 0 ? per : 1);
-            }
-            const int nstream = (int)(nblk < cp ? nblk : cp);
-            hipExtLaunchKernelGGL(k, dim3((unsigned)(nstream + A.nedge)), dim3(256), 0, stream,
-                                  ps.start, ps.stop, 0, A, (int)nblk, nstream);
-        } else if (reg) {
+        if (reg) {
             auto k = G == 2 ? (A.R.narr == 0 ? k_agg_stream_reg<2, 0>
                                : A.R.narr == 1 ? k_agg_stream_reg<2, 1> : k_agg_stream_reg<2, 2>)
                             : (A.R.narr == 0 ? k_agg_stream_reg<1, 0>

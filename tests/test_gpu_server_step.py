@@ -127,9 +127,8 @@ def test_stream_rule_reference_tick_bit_exact_vs_oracle():
 
 @pytest.mark.parametrize("narr", [0, 1, 2])
 def test_stream_variants_and_fifo_write_agree(narr, monkeypatch):
-    """The register-array stream (k_agg_stream_reg, 1 and 2 float4 groups per thread), its
-    persistent pipelined form (FLSIM_AGG_PIPE=1) and the LDS-staged k_agg_stream (FLSIM_AGG_G=0)
-    give the same bits for the reference order with 0, 1
+    """The register-array stream (k_agg_stream_reg, 1 and 2 float4 groups per thread) and the
+    LDS-staged k_agg_stream (FLSIM_AGG_G=0) give the same bits for the reference order with 0, 1
     and 2 stale arrays, on every tensor edge and tail; S_out (the FIFO slot written in the same
     pass, world > 1 at a tick) equals S_t."""
     from flsim.engine import PN1_SIZES, Rule, aggregate_rule
@@ -140,19 +139,15 @@ def test_stream_variants_and_fifo_write_agree(narr, monkeypatch):
     base = [torch.randn(P + 64, generator=g).to(DEV), (torch.randn(P + 64, generator=g) * 1e-3).to(DEV),
             (torch.rand(P + 64, generator=g) * 1e-5).to(DEV)]
     outs = {}
-    for G in ("0", "1", "2", "pipe"):
-        if G == "pipe":          # the persistent pipelined form (k_agg_stream_pipe)
-            monkeypatch.setenv("FLSIM_AGG_G", "1")
-            monkeypatch.setenv("FLSIM_AGG_PIPE", "1")
-        else:
-            monkeypatch.setenv("FLSIM_AGG_G", G)
+    for G in ("0", "1", "2"):
+        monkeypatch.setenv("FLSIM_AGG_G", G)
         a = [t.clone() for t in base]
         slot = torch.full_like(S, float("nan"))
         aggregate_rule(S, Rule(512 + narr, arrs, c=512), *a, 7, PN1_SIZES, S_out=slot)
         torch.cuda.synchronize()
         assert torch.equal(slot[:P], S[:P]), G
         outs[G] = a
-    for G in ("1", "2", "pipe"):
+    for G in ("1", "2"):
         for x, y, what in zip(outs[G], outs["0"], "pmv"):
             bad = int((x[:P].view(torch.int32) != y[:P].view(torch.int32)).sum())
             assert bad == 0, (G, what, bad)

@@ -1,8 +1,7 @@
 """Microbenchmark of the post-all-reduce server step (flsim_aggregate_adam_rule_push: rule() + Adam
 from S_t in a buffer [+ the FIFO slot write]) at PerformantNet1's P, for the stream variants
 (FLSIM_AGG_G = 0: LDS-staged k_agg_stream; 1, 2: register-array stream with 1 / 2 float4 groups per
-thread; pipe: FLSIM_AGG_PIPE=1, the persistent pipelined register stream).  Bytes are SURVEY
-8(d)'s: 4P (1 + distinct stale + 3 + 3) [+ 4P for the slot write].
+thread).  Bytes are SURVEY 8(d)'s: 4P (1 + distinct stale + 3 + 3) [+ 4P for the slot write].
 
   python tools/agg_bench.py [--iters 50]
 """
@@ -31,9 +30,8 @@ def main():
     m = torch.zeros(P + 64, device=dev)
     v = torch.zeros(P + 64, device=dev)
     res = []
-    for G in ("0", "1", "2", "pipe"):
-        os.environ["FLSIM_AGG_G"] = "1" if G == "pipe" else G
-        os.environ["FLSIM_AGG_PIPE"] = "1" if G == "pipe" else "0"
+    for G in ("0", "1", "2"):
+        os.environ["FLSIM_AGG_G"] = G
         for c, ns, out in [(512, 0, False), (1023, 0, False), (512, 1, False), (512, 1, True)]:
             rule = Rule(c + ns, [st] * ns, c=c)
             so = slot if out else None
@@ -48,7 +46,7 @@ def main():
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) / args.iters * 1e3
             byts = 4 * P * (1 + ns + 6 + (1 if out else 0))
-            r = dict(G=G, c=c, stale=ns, fifo_write=out, us=round(us, 2), bytes=byts,
+            r = dict(G=int(G), c=c, stale=ns, fifo_write=out, us=round(us, 2), bytes=byts,
                      GBps=round(byts / us / 1e3, 1), frac=round(byts / us / 1e3 / 8000, 4))
             res.append(r)
             print(json.dumps(r), flush=True)
