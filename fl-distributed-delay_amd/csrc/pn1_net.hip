@@ -541,12 +541,8 @@ static int debug_stop() {
 // apart (headline 1331.8 / 1335.1 against 1342.7 / 1346.3 worker-steps/s, profiles/r04/r04n,
 // r04o): its epilogue holds the data gradient at two blocks per CU instead of three
 static bool fuse_conv1() {
-    static int f = -1;
-    if (f < 0) {
-        const char* e = getenv("FLSIM_C1_FUSE");
-        f = e ? atoi(e) != 0 : 0;
-    }
-    return f != 0;
+    const char* e = getenv("FLSIM_C1_FUSE");      // read per call: tests switch it in-process
+    return e && atoi(e) != 0;
 }
 
 static int backward(const GradState& g, const WS& w, const float* theta, int S, int dropout,
