@@ -1,4 +1,4 @@
-// fp32 GEMM on the bf16 matrix cores at fp32 accuracy ("bf16x6"), for k-contiguous operand pairs.
+// fp32 GEMM on the bf16 matrix cores at fp32 accuracy ("bf16x6").
 //
 // gfx950's fp32 MFMA (v_mfma_f32_16x16x4_f32) runs at 1/16 of the bf16 rate.  Each fp32 operand
 // x is split into h = bf16(x), m = bf16(x - h), l = bf16(x - h - m) (round to nearest even; x - h
@@ -20,9 +20,9 @@
 // each laid out and swizzled exactly like the fp32 KC tile; every fragment is one ds_read_b128,
 // and B's [m|h] is its [h|m] fragment with the two halves swapped in registers.
 // k-major operands (the weight gradients: the pixel is the reduction index of both dZ and im2col)
-// keep three plain planes h, m, l as [16 k][rows] bf16 and read each 4-k half with gfx950's
-// transposing ds_read_b64_tr_b16 (lane 4q+p of a 16-lane group addresses k row q, columns
-// 4p..4p+3; lane i receives column i's four k), the halves paired in registers.
+// keep three plain planes h, m, l as [16 k][LD] bf16 (LD = km_ld) and read each 4-k half with
+// gfx950's transposing ds_read_b64_tr_b16 (lane 4q+p of a 16-lane group addresses k row q,
+// columns 4p..4p+3; lane i receives column i's four k), the halves paired in registers.
 // Three 16-cycle bf16 MFMAs replace four 32-cycle fp32 ones per k-step (profiles/r03v:
 // bf16x6 max error 1.0-3.1 x 2^-24 of sum |a b| against the fp32 MFMA's 1.6-3.3 on the same
 // data, K = 1728 and 16384; pre-split operands run the inner loop at 312-316 fp32-equivalent

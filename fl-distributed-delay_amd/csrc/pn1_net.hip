@@ -596,16 +596,11 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     // ---- conv6: wgrad (input a5), bias, dgrad -> dz5 = . * (a5 > 0) into gx (split) ----
     RC(fork());
     // (192 x 192 tiles of 8 waves ran 9.10-9.13 against 9.41 ms in the lab,
-    // profiles/r04/r04l/lab_wg6v.txt, but 9.26 against 9.11 in the product on another box, r04m;
-    // FLSIM_WG6_WIDE=1 selects them, measurement only)
-    if (getenv("FLSIM_WG6_WIDE") && atoi(getenv("FLSIM_WG6_WIDE")))
-        RC((conv_wgrad_sz<13, 13, 192, 2, 3, 6, 4, 2, 3, 3, 2, 2, 14, true, true, XsSrc>(
-            dz6.hm, w.a5, S, 192, 1728, g.sw[5], g.sb[5], GEO[5].ZW, sw, K_WG6, 1728, zi(5),
-            &zu[5], dz6.l, w.a5l)));
-    else
-        RC((conv_wgrad_sz<13, 13, 192, 2, 6, 3, 2, 2, 3, 3, 2, 2, 14, true, true, XsSrc>(
-            dz6.hm, w.a5, S, 192, 1728, g.sw[5], g.sb[5], GEO[5].ZW, sw, K_WG6, 1728, zi(5),
-            &zu[5], dz6.l, w.a5l)));
+    // profiles/r04/r04l/lab_wg6v.txt, but 9.26-9.29 against 9.10-9.12 in the product, A B A B on
+    // one box, profiles/r04/r04s: kept 192 x 96)
+    RC((conv_wgrad_sz<13, 13, 192, 2, 6, 3, 2, 2, 3, 3, 2, 2, 14, true, true, XsSrc>(
+        dz6.hm, w.a5, S, 192, 1728, g.sw[5], g.sb[5], GEO[5].ZW, sw, K_WG6, 1728, zi(5), &zu[5],
+        dz6.l, w.a5l)));
     RC((xs<14, 14, 192, 0, 4, 6, 4, 2, false, 13>(dz6, S, g.wdx[5], 192, 1728,
         EpiMaskXs<192, true>{dz5.hm, dz5.l, w.a5, S * 13 * 13}, st, K_DG6, 1728)));
     if (debug_stop() == 6) return join();         // (debug: dz5 stays in gx / gxl)
