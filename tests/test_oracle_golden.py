@@ -205,8 +205,9 @@ def test_vgg11_oracle_trajectory(golden):
     sim = MR.OracleSim(3, delay=2, throttle=True, pool=(imgs, labels), model="vgg11")
     for t, ref in enumerate(g["train_losses"]):
         loss = sim.epoch()
-        # host-CPU fp32 drift after the first Adam steps, as in test_training_trajectory
-        assert abs(loss - ref) <= (1e-5 if t < 2 else 1e-3), (t, loss, ref)
+        # host-CPU fp32 drift after the first Adam steps, as in test_training_trajectory: exact
+        # at epochs 0-1 and 2.1e-5 at epoch 2 on the build host; bound 5x that
+        assert abs(loss - ref) <= (1e-5 if t < 2 else 1e-4), (t, loss, ref)
         np.testing.assert_allclose(
             [float((a.astype(np.float64) ** 2).sum()) for a in MR.split_flat(sim.theta, "vgg11")],
             g[f"train_theta{t}_stats"][:, 1], rtol=1e-3)
@@ -259,16 +260,17 @@ def test_vgg11_bn_oracle_trajectory_and_eval(golden):
     sim = MR.OracleSim(3, delay=2, throttle=True, pool=(imgs, labels), model="vgg11_bn")
     for t, ref in enumerate(g["train_losses"]):
         loss = sim.epoch()
-        # host-CPU fp32 drift after the first Adam steps, as in test_training_trajectory
-        assert abs(loss - ref) <= (1e-5 if t < 2 else 1e-3), (t, loss, ref)
+        # host-CPU fp32 drift after the first Adam steps, as in test_training_trajectory: exact
+        # at epochs 0-1 and 2.1e-5 at epoch 2 on the build host; bound 5x that
+        assert abs(loss - ref) <= (1e-5 if t < 2 else 1e-4), (t, loss, ref)
         np.testing.assert_allclose(
             [float((a.astype(np.float64) ** 2).sum())
              for a in MR.split_flat(sim.theta, "vgg11_bn")][2::4],     # BatchNorm weights
             g[f"train_theta{t}_stats"][2::4, 1], rtol=1e-4)
     assert sim.bn.num_batches_tracked == int(g["train_nbt"][0])
     # running_mean: the pre-BatchNorm conv biases' Adam steps of +-lr on rounding noise enter it
-    # directly, so two hosts differ by up to lr * epochs (8e-4 seen on an EPYC build host);
-    # running_var within 1e-2 (2.7e-3 seen there in the 512-channel layers)
+    # directly, so two hosts differ by up to lr * epochs (8e-4 and 1.6e-3 seen on EPYC build
+    # hosts); running_var within 1e-2 (2.7e-3 seen there in the 512-channel layers)
     _check_running(sim.bn.flat(), g["train_running"], rm_atol=3e-3, rv_rtol=1e-2)
     timgs, _ = O.make_test_pool(0)
     params = [torch.from_numpy(a) for a in MR.split_flat(sim.theta, "vgg11_bn")]
