@@ -619,157 +619,4 @@ __host__ __device__ inline T casc_run_macro(const PROG2& prog, int pc, const Cas
     }
 }
 
-// ---- the same interpreter with consecutive words overlapped (general orders) -------------------
-// A word's "head" (its x-run, y, x-run: all into a0) and the previous word's "tail" (C1 and what
-// follows: the bx run into a1, C2, the g1 run into a2, C3, the g2 run, FIN / LX / LY / RS) touch
-// different accumulators whenever the previous word carries (C1: a0 += into a1, then a0 = 0, and a
-// FIN after it reads that a0 = +0).  So the next word's head runs into a fresh register b0 beside the
-// current word's bx / g1 runs, as paired straight runs (two independent add chains per step instead
-// of one).  Every accumulator gets exactly the adds of casc_run_macro in the same order: bit-identical.
-constexpr uint32_t MW_HEAD = 0x1ffffu;   // x-run (bits 0-4), MW_Y + q (5-11), x-run (12-16)
-
-// a += va (na times) and b += vb (nb times), interleaved; both runs < 32
-template <class T>
-__host__ __device__ inline void casc_run5_pair(T& a, const T& va, uint32_t na, T& b, const T& vb,
-                                               uint32_t nb) {
-    const uint32_t m = na < nb ? na : nb;
-    if (m & 16u) {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            a += va;
-            b += vb;
-        }
-        casc_pin(a);
-        casc_pin(b);
-    }
-    if (m & 8u) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            a += va;
-            b += vb;
-        }
-        casc_pin(a);
-        casc_pin(b);
-    }
-    if (m & 4u) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            a += va;
-            b += vb;
-        }
-        casc_pin(a);
-        casc_pin(b);
-    }
-    if (m & 2u) {
-        a += va;
-        b += vb;
-        a += va;
-        b += vb;
-        casc_pin(a);
-        casc_pin(b);
-    }
-    if (m & 1u) {
-        a += va;
-        b += vb;
-        casc_pin(a);
-        casc_pin(b);
-    }
-    if (na > m) casc_run5(a, va, na - m);
-    if (nb > m) casc_run5(b, vb, nb - m);
-}
-
-// a word's head sections into a
-template <class T, class YF>
-__host__ __device__ inline void casc_head(T& a, uint32_t lo, const CascVals<T>& c, YF&& y) {
-    uint32_t n = lo & 31u;
-    if (n) casc_run5(a, c.x, n);
-    if (lo & MW_Y) {
-        a += y((int)((lo >> 6) & 63u));
-        casc_pin(a);
-    }
-    n = (lo >> 12) & 31u;
-    if (n) casc_run5(a, c.x, n);
-}
-
-template <bool MAIN_ONLY = false, class T, class PROG2, class YF>
-__host__ __device__ inline T casc_run_macro_pipe(const PROG2& prog, int pc, const CascVals<T>& c,
-                                                 YF&& y) {
-    T a0 = T(0.f), a1 = T(0.f), a2 = T(0.f), a3 = T(0.f);
-    T r0 = T(0.f), r1 = T(0.f), r2 = T(0.f), r3 = T(0.f);
-    uint32_t lo = prog.lo(pc), hi = prog.hi(pc);
-    if (lo & MW_HEAD) casc_head(a0, lo, c, y);
-    lo &= ~MW_HEAD;
-    for (;;) {
-        ++pc;
-        const uint32_t nlo = prog.lo(pc), nhi = prog.hi(pc);     // the next pair, loaded ahead
-        T b0 = T(0.f);
-        const bool carry = (lo & MW_C1) != 0;
-        if (lo) {
-            if (carry) {
-                a1 += a0;
-                a0 = T(0.f);
-                casc_pin(a1);
-                // this word's bx run beside the next word's first x run
-                casc_run5_pair(a1, c.bx, (lo >> 18) & 31u, b0, c.x, nlo & 31u);
-                if (lo & MW_C2) {
-                    a2 += a1;
-                    a1 = T(0.f);
-                    casc_pin(a2);
-                }
-                if (nlo & MW_Y) {
-                    b0 += y((int)((nlo >> 6) & 63u));
-                    casc_pin(b0);
-                }
-                // this word's g1 run beside the next word's second x run
-                casc_run5_pair(a2, c.g1, (lo >> 24) & 31u, b0, c.x, (nlo >> 12) & 31u);
-            } else {
-                uint32_t n = (lo >> 18) & 31u;
-                if (n) casc_run5(a1, c.bx, n);
-                if (lo & MW_C2) {
-                    a2 += a1;
-                    a1 = T(0.f);
-                    casc_pin(a2);
-                }
-                n = (lo >> 24) & 31u;
-                if (n) casc_run5(a2, c.g1, n);
-            }
-            if (lo & MW_C3) {
-                a3 += a2;
-                a2 = T(0.f);
-                casc_pin(a3);
-            }
-        }
-        if (hi) {
-            const int n = (int)(hi & 0xffffu);
-            if (n) casc_add_n(a3, c.g2, n);
-            if (hi & MH_FIN) {
-                T r = a0;
-                r += a1;
-                r += a2;
-                r += a3;
-                a0 = a1 = a2 = a3 = T(0.f);
-                const uint32_t reg = (hi >> 17) & 3u;
-                if (MAIN_ONLY || reg == 0) r0 = r;
-                else if (reg == 1) r1 = r;
-                else if (reg == 2) r2 = r;
-                else r3 = r;
-            }
-            if (hi & MH_LX) r0 += c.x;
-            if (hi & MH_LY) r0 += y((int)((hi >> 21) & 63u));
-            if (hi & MH_RS) {
-                if constexpr (!MAIN_ONLY) {
-                    r0 += r1;
-                    r0 += r2;
-                    r0 += r3;
-                }
-            }
-            if (hi & MH_END) return r0;
-        }
-        if (carry) a0 = b0;                                   // the next head, already run
-        else if (nlo & MW_HEAD) casc_head(a0, nlo, c, y);
-        lo = nlo & ~MW_HEAD;
-        hi = nhi;
-    }
-}
-
 }  // namespace flsim

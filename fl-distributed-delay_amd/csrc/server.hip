@@ -102,20 +102,6 @@ struct ProgRef {
     }
 };
 
-// the interpreter of a launch: word at a time, or with consecutive words overlapped (PIPE,
-// cascade.h casc_run_macro_pipe; bit-identical)
-template <bool PIPE, bool MAIN_ONLY = false, class T, class PROG2, class YF>
-__device__ __forceinline__ T casc_exec(const PROG2& prog, int pc, const CascVals<T>& c, YF&& y) {
-    if constexpr (PIPE) return casc_run_macro_pipe<MAIN_ONLY>(prog, pc, c, y);
-    else return casc_run_macro<MAIN_ONLY>(prog, pc, c, y);
-}
-
-// FLSIM_CASC_PIPE=0 (measurement): general-order launches interpret word at a time
-static bool casc_pipe() {
-    const char* e = getenv("FLSIM_CASC_PIPE");
-    return !e || atoi(e) != 0;
-}
-
 // stage a general-order program into g_casc_prog on `stream` (no-op for inline programs)
 static int stage_program(const RuleProg& R, hipStream_t stream) {
     if (R.prog == nullptr) return 0;
@@ -171,7 +157,7 @@ __device__ __forceinline__ bool block_touch(const AggArgs& A, long blo, long spa
 // per thread; a streaming block that is also an edge block returns at once.  Every load of a
 // thread (S_t, the staged entry arrays, p, m, v) is issued before the arithmetic; loads and
 // stores are non-temporal (each byte is touched once).
-template <bool INL, bool PIPE = false>
+template <bool INL>
 __global__ void __launch_bounds__(256) k_agg_stream(AggArgs A) {
     __shared__ f32x4 ys_lds[NYR * 256];
     const ProgRef<INL> prog{A.R};
@@ -185,8 +171,8 @@ __global__ void __launch_bounds__(256) k_agg_stream(AggArgs A) {
         const CascVals<float> cv = casc_values(x, A.R.info.need, A.R.info.lp);
         const bool tail = in_tail(A, e);
         float s = 0.f;
-        if (!tail) s = casc_exec<PIPE>(prog, 0, cv, yf);
-        if (tail) s = casc_exec<PIPE>(prog, A.R.info.tail_off, cv, yf);
+        if (!tail) s = casc_run_macro(prog, 0, cv, yf);
+        if (tail) s = casc_run_macro(prog, A.R.info.tail_off, cv, yf);
         adam_elem(A.ac, s, p, m, v);
         A.p[e] = p;
         A.m[e] = m;
@@ -216,7 +202,7 @@ __global__ void __launch_bounds__(256) k_agg_stream(AggArgs A) {
         if (q < NYR) return ys_lds[q * 256 + tid];
         return A.R.arr[q] ? ld(A.R.arr[q] + e0) : f32x4{0.f, 0.f, 0.f, 0.f};
     };
-    const f32x4 sum = casc_exec<PIPE, true>(
+    const f32x4 sum = casc_run_macro<true>(
         prog, 0, casc_values(x, A.R.info.need, A.R.info.lp), yf);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -446,7 +432,7 @@ __device__ __forceinline__ bool col_to_param(const SlabSeg& g, long col, long& t
 // Identity-layout segments (the linear layers): tiles of 1024 elements, thread t owns the float4
 // column 4t; it sums its Z slab rows itself (small Z, four accumulators) and finishes with 16-B
 // parameter-side loads and stores; the parameter loads are issued before the slab reads.
-template <bool ADAM, bool INL, bool PIPE = false>
+template <bool ADAM, bool INL>
 __device__ __forceinline__ void slab_step_wide(const StepArgs& A, const SlabSeg& g, int u, int ul,
                                                float* lds) {
     // entry arrays held in registers (the rest load on demand): all of a general-order program's
@@ -571,7 +557,7 @@ __device__ __forceinline__ void slab_step_wide(const StepArgs& A, const SlabSeg&
                         return A.R.arr[q] ? ld(A.R.arr[q] + e) : f32x4{0.f, 0.f, 0.f, 0.f};
                 }
             };
-            const f32x4 sum = casc_exec<PIPE, true>(
+            const f32x4 sum = casc_run_macro<true>(
                 prog, 0, casc_values(a0, A.R.info.need, A.R.info.lp), yf);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -593,7 +579,7 @@ __device__ __forceinline__ void slab_step_wide(const StepArgs& A, const SlabSeg&
 // loads, whose cost does not depend on which XCD the last arriver sits on.  Each thread's
 // parameter-side loads (p, m, v, staged entry arrays) are issued before the slab reduction (whole
 // tiles) or together with the partial loads (split tiles), so the two memory round trips overlap.
-template <bool ADAM, bool INL, bool PIPE = false>
+template <bool ADAM, bool INL>
 __device__ __forceinline__ void slab_step_body(const StepArgs& A, float* lds) {
     const int tid = threadIdx.x;
     // runs of XG consecutive units (a tile's z-units, neighbouring tiles: one parameter region)
@@ -618,7 +604,7 @@ __device__ __forceinline__ void slab_step_body(const StepArgs& A, float* lds) {
     const SlabSeg& g = A.seg[si];
     const int ul = u - g.unit0;
     if (g.wide) {
-        slab_step_wide<ADAM, INL, PIPE>(A, g, u, ul, lds);
+        slab_step_wide<ADAM, INL>(A, g, u, ul, lds);
         return;
     }
     int tile, t_end, j;
@@ -716,7 +702,7 @@ __device__ __forceinline__ void slab_step_body(const StepArgs& A, float* lds) {
                     if (tid >= 64) return;
                     const f32x4* l4 = reinterpret_cast<const f32x4*>(lds);
                     auto yf4 = [&](int q) -> f32x4 { return l4[(L_Y + q * 256) / 4 + tid]; };
-                    const f32x4 sum = casc_exec<PIPE, true>(
+                    const f32x4 sum = casc_run_macro<true>(
                         prog, 0, casc_values(l4[L_S / 4 + tid], A.R.info.need, A.R.info.lp), yf4);
                     const f32x4 pp = l4[L_P / 4 + tid], mm = l4[L_M / 4 + tid],
                                 vv = l4[L_V / 4 + tid];
@@ -737,7 +723,7 @@ __device__ __forceinline__ void slab_step_body(const StepArgs& A, float* lds) {
                 if (tid < 64) {
                     const f32x4* l4 = reinterpret_cast<const f32x4*>(lds);
                     auto yf4 = [&](int q) -> f32x4 { return l4[(L_Y + q * 256) / 4 + tid]; };
-                    const f32x4 sum = casc_exec<PIPE, true>(
+                    const f32x4 sum = casc_run_macro<true>(
                         prog, 0, casc_values(l4[L_S / 4 + tid], A.R.info.need, A.R.info.lp), yf4);
                     f32x4 pp = l4[L_P / 4 + tid], mm = l4[L_M / 4 + tid], vv = l4[L_V / 4 + tid];
 #pragma unroll
@@ -775,8 +761,8 @@ __device__ __forceinline__ void slab_step_body(const StepArgs& A, float* lds) {
             const CascVals<float> cv = casc_values(s, A.R.info.need, A.R.info.lp);
             const bool tail = tl >= (long)(g.numel / 32) * 32;
             float sum = 0.f;
-            if (!tail) sum = casc_exec<PIPE>(prog, 0, cv, yf);
-            if (tail) sum = casc_exec<PIPE>(prog, A.R.info.tail_off, cv, yf);
+            if (!tail) sum = casc_run_macro(prog, 0, cv, yf);
+            if (tail) sum = casc_run_macro(prog, A.R.info.tail_off, cv, yf);
             adam_elem(A.ac, sum, p, m, v);
             A.p[e] = p;
             A.m[e] = m;
@@ -796,11 +782,10 @@ __global__ void __launch_bounds__(256) k_slab_step(StepArgs A) {
 #ifndef SEQ_WAVES
 #define SEQ_WAVES 4
 #endif
-template <bool PIPE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEQ_WAVES, 8)))
 k_slab_step_seq(StepArgs A) {
     __shared__ float lds[L_END];
-    slab_step_body<true, false, PIPE>(A, lds);
+    slab_step_body<true, false>(A, lds);
 }
 
 // ================================================================================================
@@ -927,8 +912,7 @@ int slab_step_launch(float* gradstate, const StepPlan& plan, long cnt_off, long 
                               ps.stop, 0, A);
     } else {
         RC(stage_program(*rule, stream));
-        hipExtLaunchKernelGGL(casc_pipe() ? k_slab_step_seq<true> : k_slab_step_seq<false>,
-                              dim3(nblk), dim3(256), 0, stream, ps.start,
+        hipExtLaunchKernelGGL(k_slab_step_seq, dim3(nblk), dim3(256), 0, stream, ps.start,
                               ps.stop, 0, A);
     }
     FLSIM_LAUNCH_CHECK();
@@ -1048,8 +1032,7 @@ int flsim_aggregate_adam_rule_push(const float* S, float* S_out, const flsim_rul
                                   0, stream, ps.start, ps.stop, 0, A);
         else {
             RC(stage_program(A.R, stream));
-            hipExtLaunchKernelGGL(casc_pipe() ? k_agg_stream<false, true> : k_agg_stream<false, false>,
-                                  grid, dim3(256),
+            hipExtLaunchKernelGGL(k_agg_stream<false>, grid, dim3(256),
                                   0, stream, ps.start, ps.stop, 0, A);
         }
         FLSIM_LAUNCH_CHECK();
@@ -1123,17 +1106,12 @@ int flsim_cascade_eval_host(const int32_t* prog, const int32_t* info, const floa
         uint32_t lo(int i) const { return (uint32_t)w[2 * i]; }
         uint32_t hi(int i) const { return (uint32_t)w[2 * i + 1]; }
     } hp{prog};
-    // FLSIM_CASC_PIPE=0: the word-at-a-time interpreter (casc_run_macro); default the overlapped
-    // one the general-order device step runs (casc_run_macro_pipe; the two are bit-identical)
-    const char* pe = getenv("FLSIM_CASC_PIPE");
-    const bool pipe = !pe || atoi(pe) != 0;
     for (long e = 0; e < n; ++e) {
         const CascVals<float> cv = casc_values(S[e], info[2], info[3]);
         auto yf = [&](int q) -> float {
             return (q < n_arrays && ys[q]) ? ys[q][e] : 0.f;
         };
-        out[e] = pipe ? casc_run_macro_pipe(hp, (tail && tail[e]) ? info[1] : 0, cv, yf)
-                      : casc_run_macro(hp, (tail && tail[e]) ? info[1] : 0, cv, yf);
+        out[e] = casc_run_macro(hp, (tail && tail[e]) ? info[1] : 0, cv, yf);
     }
     return 0;
 }
