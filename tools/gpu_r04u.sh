@@ -1,6 +1,7 @@
 #!/bin/bash
 # round 4: the general-order interpreter with consecutive words overlapped (casc_run_macro_pipe,
 # default; FLSIM_CASC_PIPE=0 = word at a time): bit-exact tests, then configs[3]'s bench line both ways.
+# (historical: the interpreter was removed after this run, profiles/r04/r04u; the script no longer applies)
 # Usage (repo root, GPU box): bash tools/gpu_r04u.sh <tag>
 set -u
 TAG=${1:-r04u}
