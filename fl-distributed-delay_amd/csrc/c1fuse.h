@@ -20,7 +20,7 @@
 namespace flsim {
 
 struct C1Fuse {
-    const float* a1h;   // HM part of a1 (split.h): the ReLU mask of dz1
+    const float* a1h;   // HM part of a1 (split.h, channel-slice-major): the ReLU mask of dz1
     const float* x0;    // conv1's input [S][32][32][4]
     float* slab;        // conv1's weight slab [Z][48][KP]
     float* bslab;       // conv1's bias slab [Z][48]
@@ -134,9 +134,9 @@ k_dgrad2_wgrad1(AD ad, BL bl, C1Fuse c, int ksteps) {
 #pragma unroll
             for (int it = 0; it < MU; ++it) {
                 const int q = tid + it * NT, r = q / 12, cu = q - r * 12;
-                hv[it] = mp + r < c.M
-                             ? reinterpret_cast<const f32x2*>(c.a1h)[2 * ((long)(mp + r) * 12 + cu)]
-                             : f32x2{0.f, 0.f};
+                hv[it] = mp + r < c.M ? reinterpret_cast<const f32x2*>(c.a1h)[
+                                            2 * xs_unit<48, 1156, true>((unsigned)(mp + r), cu)]
+                                      : f32x2{0.f, 0.f};
             }
 #pragma unroll
             for (int it = 0; it < XU; ++it) {

@@ -16,8 +16,27 @@ __device__ __forceinline__ f32x4 mask4(f32x4 t, uint32_t pos) {
                  (pos & 8) ? t.w : 0.f};
 }
 
-// conv forward: Y = relu(acc + bias) over NC channels, written split (conv3 -> a3, conv5 -> a5)
-template <int NC>
+// In-LDS ReLU mask of a staged tile (rows [m0, m0 + rows), units [n0 / 4, n0 / 4 + n4) of NC
+// channels) from a channel-slice-major split act (split.h xs_unit): threads walk the tile slice by
+// slice, rows fastest, so their act reads are contiguous in the slice-major layout.  Ends with a
+// block barrier (every thread of the block calls it: staged epilogues run block-wide).
+template <int NC, int AHW>
+__device__ __forceinline__ void mask_tile_sm(float* tile, int ld, const float* act, int m0, int rows,
+                                             int n0, int n4, int tid, int nt) {
+    const f32x2* a2 = reinterpret_cast<const f32x2*>(act);
+    const int total = rows * n4;
+    for (int q = tid; q < total; q += nt) {
+        const int s = q / (rows * 4), rem = q - s * rows * 4;
+        const int r = rem >> 2, c = 4 * s + (rem & 3);
+        f32x4* t = reinterpret_cast<f32x4*>(tile + r * ld + 4 * c);
+        *t = mask4(*t, xs_pos4(a2[2 * xs_unit<NC, AHW, true>((unsigned)(m0 + r), n0 / 4 + c)]));
+    }
+    __syncthreads();
+}
+
+// conv forward: Y = relu(acc + bias) over NC channels, written split (conv3 -> a3, conv5 -> a5);
+// SM: Y channel-slice-major over HW pixels per image (split.h xs_unit)
+template <int NC, bool SM = false, int HW = 1>
 struct EpiBiasReluXs {
     static constexpr bool ASUM = false;
     static constexpr bool STAGED = true;
@@ -38,14 +57,15 @@ struct EpiBiasReluXs {
             const f32x4 b = *reinterpret_cast<const f32x4*>(bias + n0 + 4 * c);
             const f32x4 v = {fmaxf(t.x + b.x, 0.f), fmaxf(t.y + b.y, 0.f), fmaxf(t.z + b.z, 0.f),
                              fmaxf(t.w + b.w, 0.f)};
-            xs_store(Yhm, Yl, ((long)(m0 + r) * NC + n0) / 4 + c, v);
+            xs_store(Yhm, Yl, xs_unit<NC, HW, SM>((unsigned)(m0 + r), n0 / 4 + c), v);
         }
     }
 };
 
 // data gradient through a ReLU: Y = acc * (act > 0), act split; Y split (OUT_XS: dz5, dz3) or
-// fp32 (dz1, read by conv1's fp32 weight gradient)
-template <int NC, bool OUT_XS>
+// fp32 (dz1, read by conv1's fp32 weight gradient); ASM: act channel-slice-major over AHW pixels
+// per image (Y stays pixel-major)
+template <int NC, bool OUT_XS, bool ASM = false, int AHW = 1>
 struct EpiMaskXs {
     static constexpr bool ASUM = false;
     static constexpr bool STAGED = true;
@@ -62,6 +82,21 @@ struct EpiMaskXs {
         const int rows = M - m0 < bm ? M - m0 : bm;
         const int n4 = bn / 4;
         const int total = rows * n4;
+        if constexpr (ASM) {
+            static_assert(NC % 16 == 0, "");
+            // slice-major act: mask in LDS (act reads in its order), then store in row order
+            mask_tile_sm<NC, AHW>(const_cast<float*>(tile), ld, act, m0, rows, n0, n4, tid, nt);
+            for (int q = tid; q < total; q += nt) {
+                const int r = q / n4, c = q - r * n4;
+                const f32x4 o = *reinterpret_cast<const f32x4*>(tile + r * ld + 4 * c);
+                const long u = ((long)(m0 + r) * NC + n0) / 4 + c;
+                if constexpr (OUT_XS)
+                    xs_store(Y, Yl, u, o);
+                else
+                    st_nt4(Y + 4 * u, o);
+            }
+            return;
+        }
         auto unit = [&](int q, f32x2 a) {
             const int r = q / n4, c = q - r * n4;
             const f32x4 t = *reinterpret_cast<const f32x4*>(tile + r * ld + 4 * c);
@@ -96,8 +131,8 @@ struct EpiMaskXs {
 // EpiDropScatterRows (loaders.h) over split tensors: the masked, scaled gradient of pooled element
 // (m, n) goes to its argmax position of the 2x2 window in the full-resolution dZ, zeros elsewhere;
 // act (the pooled, dropped activation) is split, dZ is written split (OUT_XS) or fp32.  Full rows
-// (BN == NC).
-template <int PH, int PW, int NC, bool OUT_XS = true>
+// (BN == NC).  ASM: act channel-slice-major (split.h xs_unit).
+template <int PH, int PW, int NC, bool OUT_XS = true, bool ASM = false>
 struct EpiDropScatterXs {
     static constexpr bool ASUM = false;
     static constexpr bool STAGED = true;
@@ -114,7 +149,15 @@ struct EpiDropScatterXs {
     __device__ void store_rows(const float* tile, int ld, int m0, int bm, int tid, int nt) const {
         const int rows = M - m0 < bm ? M - m0 : bm;
         constexpr int N4 = NC / 4;
-        const f32x2* a4 = reinterpret_cast<const f32x2*>(act) + 2 * (long)m0 * N4;   // h parts
+        if constexpr (ASM)      // slice-major act: masked in LDS first, then every unit passes
+            mask_tile_sm<NC, PH * PW>(const_cast<float*>(tile), ld, act, m0, rows, 0, N4, tid, nt);
+        const f32x2* a2 = reinterpret_cast<const f32x2*>(act) + 2 * (long)m0 * N4;   // h parts
+        auto act_h = [&](int q) -> f32x2 {
+            if constexpr (ASM)
+                return __builtin_bit_cast(f32x2, u32x2{0x3f803f80u, 0x3f803f80u});   // h = 1: pass
+            else
+                return a2[2 * q];
+        };
         const uint32_t* i4 = reinterpret_cast<const uint32_t*>(idx + (long)m0 * NC);
         const int total = rows * N4;
         f32x2 av[BATCH];
@@ -123,7 +166,7 @@ struct EpiDropScatterXs {
         for (int it = 0; it < BATCH; ++it) {
             const int q = tid + it * nt;
             if (q < total) {
-                av[it] = a4[2 * q];
+                av[it] = act_h(q);
                 iv[it] = i4[q];
             }
         }
@@ -132,7 +175,7 @@ struct EpiDropScatterXs {
             const int q = tid + it * nt;
             if (q < total) unit(tile, ld, m0, q, av[it], iv[it]);
         }
-        for (int q = tid + BATCH * nt; q < total; q += nt) unit(tile, ld, m0, q, a4[2 * q], i4[q]);
+        for (int q = tid + BATCH * nt; q < total; q += nt) unit(tile, ld, m0, q, act_h(q), i4[q]);
     }
     __device__ void unit(const float* tile, int ld, int m0, int q, f32x2 a, uint32_t id) const {
         constexpr int N4 = NC / 4;
@@ -165,8 +208,9 @@ struct EpiDropScatterXs {
 // and written split (NHWC: conv2 -> d1, conv4 -> d2).  Tile rows are in pool-window order
 // (Im2colKC / Im2colDirect WIN), so rows 4p .. 4p + 3 of the tile are pooled pixel p's window; a
 // thread takes (pooled pixel, 4 channels): the same per-element max / first-argmax / dropout as
-// EpiPoolDrop, one split unit of d and one 4-byte argmax word.  Full rows (BN == C).
-template <int PH, int PW, int C>
+// EpiPoolDrop, one split unit of d and one 4-byte argmax word.  Full rows (BN == C).  SM: d
+// channel-slice-major (split.h xs_unit; the argmax words stay pixel-major).
+template <int PH, int PW, int C, bool SM = false>
 struct EpiPoolDropXs {
     static constexpr bool ASUM = false;
     static constexpr bool STAGED = true;
@@ -222,7 +266,7 @@ struct EpiPoolDropXs {
             }
             const long eo = (long)q * C + 4 * c;
             *reinterpret_cast<uint32_t*>(idx + eo) = id;
-            xs_store(dhm, dl, eo / 4, out);
+            xs_store(dhm, dl, xs_unit<C, PH * PW, SM>((unsigned)q, c), out);
         }
     }
 };

@@ -25,6 +25,9 @@ template <int IH, int IW, int CI, int PAD, int FM, bool WIN = false, int OHX = 0
           class SRC = BufSrc>
 struct Im2colDirect {
     using Unit = typename SRC::Unit;
+    // floats between neighbouring pixels / between channel slices (SRC::SM: slice-major input)
+    static constexpr int PIX = SRC::SM ? GK : CI;
+    static constexpr int SLICE = SRC::SM ? IH * IW * GK : GK;
     static constexpr int OH = OHX > 0 ? OHX : IH + 2 * PAD - 2;
     static constexpr int OW = OHX > 0 ? OHX : IW + 2 * PAD - 2;
     static constexpr int PH = OH / 2, PW = OW / 2;
@@ -60,7 +63,8 @@ struct Im2colDirect {
                     oh = rem / OW;
                     ow = rem - oh * OW;
                 }
-                base = ((long)nimg * IH * IW + (long)(oh - PAD) * IW + (ow - PAD)) * CI + 4 * q;
+                base = (long)nimg * IH * IW * CI + ((long)(oh - PAD) * IW + (ow - PAD)) * PIX +
+                       4 * q;
 #pragma unroll
                 for (int t = 0; t < 9; ++t) {
                     const int ih = oh + t / 3 - PAD, iw = ow + t % 3 - PAD;
@@ -75,7 +79,7 @@ struct Im2colDirect {
         const int cs = ks / 9;                  // uniform
         const int khkw = ks - 9 * cs;
         const int kh = khkw / 3;
-        const unsigned off = (unsigned)(((kh * IW + (khkw - 3 * kh)) * CI + cs * GK) * 4);
+        const unsigned off = (unsigned)(((kh * IW + (khkw - 3 * kh)) * PIX + cs * SLICE) * 4);
 #pragma unroll
         for (int f = 0; f < FM; ++f) r[f] = buf.ld_or0(vb[f] + off, (tapmask[f] >> khkw) & 1);
     }

@@ -38,6 +38,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t raw_rsrc(const void* base, uns
 struct BufSrc {
     using Unit = f32x4;
     static constexpr bool SPLIT = false;
+    static constexpr bool SM = false;
     __amdgpu_buffer_rsrc_t r;
     __device__ __forceinline__ void init(const float* base, unsigned long bytes) {
         r = raw_rsrc(base, bytes);
@@ -59,6 +60,7 @@ struct BufSrc {
 struct XsSrc {
     using Unit = XsUnit;
     static constexpr bool SPLIT = true;
+    static constexpr bool SM = false;
     __amdgpu_buffer_rsrc_t rhm, rl;
     __device__ __forceinline__ void init(const float* hm, const float* l, unsigned long bytes) {
         rhm = raw_rsrc(hm, bytes);
@@ -73,6 +75,14 @@ struct XsSrc {
     __device__ __forceinline__ XsUnit ld_or0(unsigned byte_off, bool ok) const {
         return ld(ok ? byte_off : BUF_OOB);
     }
+};
+
+// A split tensor of C channels stored channel-slice-major, [img][C/16][H][W][16]: the 16 channels of
+// one slice of neighbouring pixels are contiguous, so the 16 rows of a direct-A fragment (16
+// neighbouring output pixels, one tap, one slice) read whole cache lines.  Only the loaders that
+// read conv inputs (Im2colDirect, Im2colKM) accept it; the others assert pixel-major sources.
+struct XsSrcSM : XsSrc {
+    static constexpr bool SM = true;
 };
 
 // r / D for 0 <= r < R by one 24-bit multiply and a shift (exact on that range, checked at
@@ -111,6 +121,7 @@ template <int IH, int IW, int CI, int PAD, int TR, int NT, bool WIN = false, int
           class SRC = BufSrc>
 struct Im2colKC {
     using Unit = typename SRC::Unit;
+    static_assert(!SRC::SM, "pixel-major operand");
     static constexpr int ROWS = TR;
     static constexpr bool KC = true;
     static constexpr int OH = OHX > 0 ? OHX : IH + 2 * PAD - 2;
@@ -228,6 +239,7 @@ struct Im2colKC {
 template <int TR, int NT, class SRC = BufSrc>
 struct RowsKC {
     using Unit = typename SRC::Unit;
+    static_assert(!SRC::SM, "pixel-major operand");
     static constexpr int ROWS = TR;
     static constexpr bool KC = true;
     static constexpr int TOTAL = ROWS * 4;
@@ -307,6 +319,7 @@ __device__ __forceinline__ int km_row(int tid) {
 template <int TR, int NT, int PO = 0, int PV = 0, class SRC = BufSrc>
 struct RowsKM {
     using Unit = typename SRC::Unit;
+    static_assert(!SRC::SM, "pixel-major operand");
     static constexpr int ROWS = TR;
     static constexpr bool KC = false;
     static constexpr int C4 = ROWS / 4;
@@ -399,11 +412,15 @@ struct Im2colKM {
     static_assert(NT % GK == 0, "");
     static constexpr int UNITS = (C4 + TPR - 1) / TPR;
     static_assert(FLSIM_BUFLOAD || !SRC::SPLIT, "split operands use buffer loads");
+    // floats between neighbouring pixels / from channel slice 0 to slice ci / 16 (SRC::SM)
+    static constexpr int PIX = SRC::SM ? GK : CI;
+    static constexpr int SLICE = SRC::SM ? IH * IW * GK : GK;
+    static_assert(!SRC::SM || CI % GK == 0, "slice-major maps have whole 16-channel slices");
     const float* X;
     const float* XL = nullptr;   // SRC = XsSrc: X is the HM part, XL the L part (split.h)
     int M;  // total pixels
     int krow;
-    int coff[UNITS];   // ((kh - PAD) * IW + kw - PAD) * CI + ci: the column's offset from pixel (oh, ow)
+    int coff[UNITS];   // ((kh - PAD) * IW + kw - PAD) * PIX + channel offset: from pixel (oh, ow)
     short kh[UNITS], kw[UNITS];   // tap of the column; kh = -64 when it is padding
     short c4[UNITS];
     SRC buf;
@@ -421,7 +438,9 @@ struct Im2colKM {
             const bool real = c < C4 && khkw < 9;
             kh[j] = (short)(real ? khkw / 3 : -64);
             kw[j] = (short)(khkw % 3);
-            coff[j] = real ? ((khkw / 3 - PAD) * IW + (khkw % 3 - PAD)) * CI + ci : 0;
+            coff[j] = real ? ((khkw / 3 - PAD) * IW + (khkw % 3 - PAD)) * PIX + (ci / GK) * SLICE +
+                                 ci % GK
+                           : 0;
         }
     }
     __device__ void load(int ks, Unit (&r)[UNITS]) const {
@@ -439,7 +458,7 @@ struct Im2colKM {
         const int ow = (int)rem - oh * OW;
         const bool pok = p < M;
         if constexpr (FLSIM_BUFLOAD) {
-            const unsigned xb = (img * (unsigned)(IH * IW) + (unsigned)(oh * IW + ow)) * (CI * 4u);
+            const unsigned xb = img * (unsigned)(IH * IW * CI * 4) + (unsigned)(oh * IW + ow) * (PIX * 4u);
 #pragma unroll
             for (int j = 0; j < UNITS; ++j) {
                 const int ih = oh + kh[j] - PAD, iw = ow + kw[j] - PAD;
@@ -447,6 +466,7 @@ struct Im2colKM {
                 r[j] = buf.ld_or0(xb + (unsigned)coff[j] * 4u, ok);
             }
         } else {
+            static_assert(!SRC::SM, "slice-major maps use buffer loads");
             const long xo = ((long)img * IH * IW + oh * IW + ow) * CI;
 #pragma unroll
             for (int j = 0; j < UNITS; ++j) {

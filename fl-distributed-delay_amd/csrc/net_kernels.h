@@ -958,11 +958,13 @@ static int conv_wgrad_sz(const float* dz, const float* X, int S, int CO, int KP,
 // conv (forward, or data gradient as a valid convolution) over a split input X and split packed
 // weights W [N][KP] on the direct-A kernel (gemm_dx6.h): WAVES waves of 16*FM rows, 16*FN columns
 // per n-tile, B staged KB k-steps a time (NPL planes), A loaded DEPTH k-steps ahead
+// (ASRC = XsSrcSM: X channel-slice-major, loaders.h)
 template <int IH, int IW, int CI, int PAD, int FM, int FN, int WAVES, int KB, int DEPTH, int NPL,
-          bool WIN, int OHX, class EPI>
+          bool WIN, int OHX, class ASRC = XsSrc, class EPI>
 static int conv_dx6(XsT X, int S, XsT W, int N, int KP, const EPI& epi, hipStream_t st, int kid,
                     int kreal) {
-    using AD = Im2colDirect<IH, IW, CI, PAD, FM, WIN, OHX, XsSrc>;
+    static_assert(ASRC::SPLIT, "split input");
+    using AD = Im2colDirect<IH, IW, CI, PAD, FM, WIN, OHX, ASRC>;
     using BL = RowsKCStageXs<16 * FN, 64 * WAVES, NPL>;
     constexpr int BM = 16 * FM * WAVES, BN = 16 * FN;
     FLSIM_REQUIRE((KP / GK) % KB == 0, "direct GEMM: %d k-steps not a multiple of %d", KP / GK, KB);

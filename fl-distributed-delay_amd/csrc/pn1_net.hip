@@ -214,6 +214,7 @@ static int pack_weights(const GradState& g, const float* theta, hipStream_t st) 
 // four MFMAs.  Tap 8 is one MFMA whose k slot g is the input channel.  27 real MFMA k-values (plus
 // the zero 4th channel), 9 MFMAs per 16x16 output tile.
 constexpr int C1_ROWS = 32;     // output pixels per wave iteration (two 16-row tiles)
+static_assert(C1_ROWS == 32, "the a1 store loop maps 64 lanes to 16 rows x 4 units of a slice");
 constexpr int C1_LD = 52;       // staging row stride (floats): 16-B aligned, rows on different banks
 __global__ void __launch_bounds__(256)
 k_conv1_fwd(const float* __restrict__ x0, const float* __restrict__ W, const float* __restrict__ bias,
@@ -285,13 +286,15 @@ k_conv1_fwd(const float* __restrict__ x0, const float* __restrict__ W, const flo
                 for (int r = 0; r < 4; ++r)
                     st[(16 * t + 4 * g + r) * C1_LD + 16 * j + i] = fmaxf(acc[t][j][r] + bj[j], 0.f);
         __builtin_amdgcn_wave_barrier();
-        // a1 in the split form (split.h): each lane splits whole 4-channel units of its rows.
-        // (Two units per lane, their L parts as one 16-B store, measured 2.06 against 1.23 ms:
-        // the lanes' HM stores then land 32 B apart, half lines per instruction; profiles/r04/r04l)
+        // a1 in the split form (split.h), channel-slice-major ([S][3][34*34][16], loaders.h
+        // XsSrcSM): each lane splits whole 4-channel units; the 64 lanes of a store take 16 rows of
+        // one 16-channel slice, 1 KB of HM (512 B of L) contiguous.  (Two units per lane, their L
+        // parts as one 16-B store, measured 2.06 against 1.23 ms: the lanes' HM stores then land
+        // 32 B apart, half lines per instruction; profiles/r04/r04l)
 #pragma unroll
         for (int q0 = 0; q0 < C1_ROWS * 12; q0 += 64) {
-            const int q = q0 + lane, row = q / 12, c4 = q - (q / 12) * 12;
-            xs_store(a1, a1l, u * C1_ROWS * 12 + q,
+            const int q = q0 + lane, slice = q >> 7, row = (q & 127) >> 2, c4 = 4 * slice + (q & 3);
+            xs_store(a1, a1l, xs_unit<48, 1156, true>((unsigned)(u * C1_ROWS + row), c4),
                      *reinterpret_cast<const f32x4*>(st + row * C1_LD + 4 * c4));
         }
         __builtin_amdgcn_wave_barrier();
@@ -324,10 +327,11 @@ template <int IH, int IW, int CI, int PAD, int FN, bool WIN, int OHX, int FM = D
           int WAVES = 8, class EPI>
 static int dx6(XsT X, int S, XsT W, int N, int KP, const EPI& epi, hipStream_t st, int kid,
                int kreal) {
+    // the inputs of conv2-4 (a1, d1, a3) are channel-slice-major (XsSrcSM)
     if (S <= small_chunk_samples())
-        return conv_dx6<IH, IW, CI, PAD, FM / 2, FN, WAVES, DX_KB, DX_DEPTH, DX_NPL, WIN, OHX>(
-            X, S, W, N, KP, epi, st, kid, kreal);
-    return conv_dx6<IH, IW, CI, PAD, FM, FN, WAVES, DX_KB, DX_DEPTH, DX_NPL, WIN, OHX>(
+        return conv_dx6<IH, IW, CI, PAD, FM / 2, FN, WAVES, DX_KB, DX_DEPTH, DX_NPL, WIN, OHX,
+                        XsSrcSM>(X, S, W, N, KP, epi, st, kid, kreal);
+    return conv_dx6<IH, IW, CI, PAD, FM, FN, WAVES, DX_KB, DX_DEPTH, DX_NPL, WIN, OHX, XsSrcSM>(
         X, S, W, N, KP, epi, st, kid, kreal);
 }
 
@@ -354,11 +358,12 @@ static int forward(const GradState& g, const WS& w, const float* theta, int S,
     RC(conv1_fwd(w.x0, theta + P_OFF[0], theta + P_OFF[1], a1, S, st));
     // conv2 + ReLU + pool1 + dropout1 (models.py:30-32), one fused launch -> d1 (split)
     RC((dx6<34, 34, 48, 2, 3, true, 0, 4, 4>(a1, S, g.wfx[1], 48, 432,
-        EpiPoolDropXs<18, 18, 48>{d1.hm, d1.l, w.i1, theta + P_OFF[3], workers, seed, SITE_DROP1,
+        EpiPoolDropXs<18, 18, 48, true>{d1.hm, d1.l, w.i1, theta + P_OFF[3], workers, seed, SITE_DROP1,
                                   THR_P25, SCALE_P25, dropout, S * 18 * 18 * 4}, st, K_FWD2, 432)));
     // conv3 + ReLU (models.py:33) -> a3 (split)
     RC((dx6<18, 18, 48, 2, 6, false, 0>(d1, S, g.wfx[2], 96, 432,
-        EpiBiasReluXs<96>{a3.hm, a3.l, theta + P_OFF[5], S * 20 * 20}, st, K_FWD3, 432)));
+        EpiBiasReluXs<96, true, 400>{a3.hm, a3.l, theta + P_OFF[5], S * 20 * 20}, st, K_FWD3,
+        432)));
     // conv4 + ReLU + pool2 + dropout1 (models.py:34-36) -> d2 (split)
     RC((dx6<20, 20, 96, 2, 6, true, 0>(a3, S, g.wfx[3], 96, 864,
         EpiPoolDropXs<11, 11, 96>{d2.hm, d2.l, w.i2, theta + P_OFF[7], workers, seed, SITE_DROP2,
@@ -620,28 +625,28 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     // gradients split dZ while staging (split-bf16 kernel over an fp32 dZ and a split layer input)
     RC(join());                                   // conv5's wgrad reads gx = dz5: done first
     RC(fork());
-    RC((conv_wgrad<20, 20, 96, 2, 3, 3, 2, 2, 0, false, true, XsSrc>(
+    RC((conv_wgrad<20, 20, 96, 2, 3, 3, 2, 2, 0, false, true, XsSrc, XsSrcSM>(
         dz4.hm, w.a3, S, 96, 864, g.sw[3], g.sb[3], GEO[3].ZW, sw, K_WG4, 864, zi(3), &zu[3],
         dz4.l, w.a3l)));
     RC((xs<22, 22, 96, 0, 4, 3, 4, 2, false, 0>(dz4, S, g.wdx[3], 96, 864,
-        EpiMaskXs<96, false>{w.gx, nullptr, w.a3, S * 20 * 20}, st, K_DG4, 864)));
+        EpiMaskXs<96, false, true, 400>{w.gx, nullptr, w.a3, S * 20 * 20}, st, K_DG4, 864)));
     float* dz3 = w.gx;
     // ---- conv3: wgrad (input d1), bias, dgrad -> grad wrt d1 (site 1), scattered through pool1
     //      straight into dz2 (a2 buffer, fp32) ----
     RC(fork());
     // (96 x 96 tiles of 4 waves: 2.96 against 3.54 ms for 96 x 48 of 2, profiles/r04/r04j/lab_wg.txt)
-    RC((conv_wgrad_sz<18, 18, 48, 2, 3, 3, 2, 2, 3, 3, 2, 2, 0, false, true, BufSrc, XsSrc>(
+    RC((conv_wgrad_sz<18, 18, 48, 2, 3, 3, 2, 2, 3, 3, 2, 2, 0, false, true, BufSrc, XsSrcSM>(
         dz3, w.d1, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW, sw, K_WG3, 432, zi(2), &zu[2],
         nullptr, w.d1l)));
     // (gemm_kernel: the direct-A form measured 3.87 vs 3.78 ms with this staged epilogue, r03b)
     RC((conv_like_sz<20, 20, 96, 0, 4, 2, 3, 4, 1>(dz3, S, g.wd[2], 48, 864,
-        EpiDropScatterXs<18, 18, 48, false>{w.a2, nullptr, w.d1, w.i1, s25, S * 18 * 18}, st,
+        EpiDropScatterXs<18, 18, 48, false, true>{w.a2, nullptr, w.d1, w.i1, s25, S * 18 * 18}, st,
         K_DG3, 864)));
     float* dz2 = w.a2;
     // ---- conv2: wgrad (input a1), bias, dgrad -> dz1 = . * (a1 > 0) into gx (fp32) ----
     RC(join());                                   // conv3's wgrad reads gx = dz3: done first
     RC(fork());
-    RC((conv_wgrad_sz<34, 34, 48, 2, 3, 3, 1, 3, 3, 3, 1, 3, 0, false, true, BufSrc, XsSrc>(
+    RC((conv_wgrad_sz<34, 34, 48, 2, 3, 3, 1, 3, 3, 3, 1, 3, 0, false, true, BufSrc, XsSrcSM>(
         dz2, w.a1, S, 48, 432, g.sw[1], g.sb[1], GEO[1].ZW, sw, K_WG2, 432, zi(1), &zu[1],
         nullptr, w.a1l)));
     if (fuse_conv1()) {
@@ -651,7 +656,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
                                                        K_DG2)));
     } else {
         RC((conv_direct_sz<36, 36, 48, 0, 2, 1, 3, 8, 3, 2, false, 0>(dz2, S, g.wd[1], 48, 432,
-            EpiMaskXs<48, false>{w.gx, nullptr, w.a1, S * 34 * 34}, st, K_DG2, 432)));
+            EpiMaskXs<48, false, true, 1156>{w.gx, nullptr, w.a1, S * 34 * 34}, st, K_DG2, 432)));
         float* dz1 = w.gx;
         // ---- conv1: wgrad (input x0), bias ----
         // (3 waves of 16 rows each: 0.272 vs 0.325 ms for one 48x48 wave, profiles/r01c/lab_conv1.txt)
@@ -707,6 +712,10 @@ int flsim_pn1_workspace_split_part(int which) {
         case 5: return 28;     // dz4 (a4 buffer)
         default: return -1;
     }
+}
+
+int flsim_pn1_workspace_slice_major(int which) {
+    return which == 1 || which == 3 || which == 4;    // a1, d1, a3 (XsSrcSM)
 }
 
 int flsim_pn1_begin_epoch(void* gradstate, const float* theta, hipStream_t stream) {

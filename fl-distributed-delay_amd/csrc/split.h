@@ -87,6 +87,20 @@ __device__ __forceinline__ uint32_t xs_pos4(f32x2 h) {     // h = the first 8 B 
            ((uint32_t)((int32_t)(b & 0xffff0000u) > 0) << 3);
 }
 
+// Unit index of channels 4 c4 .. 4 c4 + 3 of pixel m (pixels counted over all images, HW per image)
+// of a split tensor of C channels: pixel-major [img][HW][C] (SM false), or channel-slice-major
+// [img][C/16][HW][16] (SM true, loaders.h XsSrcSM)
+template <int C, int HW, bool SM>
+__device__ __forceinline__ long xs_unit(unsigned m, int c4) {
+    if constexpr (!SM) {
+        return (long)m * (C / 4) + c4;
+    } else {
+        static_assert(C % 16 == 0, "whole 16-channel slices");
+        const unsigned img = m / (unsigned)HW, p = m - img * (unsigned)HW;
+        return ((long)(img * (C / 16) + (c4 >> 2)) * HW + p) * 4 + (c4 & 3);
+    }
+}
+
 // store the split form of 4 consecutive values (unit index u: elements 4u .. 4u + 3)
 template <bool NT = true>
 __device__ __forceinline__ void xs_store(float* hm, float* l, long u, f32x4 v) {

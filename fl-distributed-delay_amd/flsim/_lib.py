@@ -18,7 +18,7 @@ EXPORTS = [
     "flsim_last_error", "flsim_sched_create", "flsim_sched_destroy", "flsim_sched_epoch",
     "flsim_sched_state", "flsim_pn1_param_count", "flsim_pn1_gradstate_bytes",
     "flsim_pn1_workspace_bytes", "flsim_pn1_workspace_offset", "flsim_pn1_workspace_split_part",
-    "flsim_pn1_begin_epoch",
+    "flsim_pn1_workspace_slice_major", "flsim_pn1_begin_epoch",
     "flsim_pn1_fwd_bwd_chunk", "flsim_pn1_fwd_bwd_input", "flsim_pn1_end_epoch",
     "flsim_pn1_eval_pool", "flsim_vgg11_param_count", "flsim_vgg11_gradstate_bytes",
     "flsim_vgg11_workspace_bytes", "flsim_vgg11_workspace_offset", "flsim_vgg11_begin_epoch",
@@ -100,6 +100,7 @@ def lib():
         f("eval_pool").argtypes = [vp, vp, ctypes.c_int, vp, vp, ctypes.c_int, ctypes.c_int,
                                    vp] + bn + [vp, vp]
     L.flsim_pn1_workspace_split_part.argtypes = [ctypes.c_int]
+    L.flsim_pn1_workspace_slice_major.argtypes = [ctypes.c_int]
     L.flsim_vgg11_bn_update_running.argtypes = [vp, vp, ctypes.c_int, vp]
     L.flsim_pn1_release.argtypes = [vp]
     L.flsim_pn1_release.restype = None

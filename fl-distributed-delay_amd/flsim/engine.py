@@ -241,7 +241,20 @@ class NetEngine:
 
         def f32(b):         # bf16 bits -> fp32 (exact)
             return (b.to(torch.int32) << 16).view(torch.float32)
-        return ((f32(hm[:, 0]) + f32(hm[:, 1])) + f32(lo)).view(shape)
+        vals = (f32(hm[:, 0]) + f32(hm[:, 1])) + f32(lo)
+        if self.slice_major(which):
+            # stored [N][C/16][H][W][16] (loaders.h XsSrcSM): back to [N][H][W][C]
+            n, h, w, c = shape
+            return vals.view(n, c // 16, h, w, 16).permute(0, 2, 3, 1, 4).reshape(shape)
+        return vals.view(shape)
+
+    def slice_major(self, which):
+        """True when workspace tensor `which` is stored channel-slice-major (PN1's a1, d1, a3)."""
+        try:
+            fn = self._fn("workspace_slice_major")
+        except AttributeError:
+            return False
+        return bool(fn(which))
 
     def split_part(self, which):
         """Workspace id of tensor `which`'s L part when it is stored split, else -1."""

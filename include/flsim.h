@@ -71,6 +71,9 @@ int flsim_pn1_workspace_offset(int which, int samples, long* offset_bytes);
 /* (debug / tests) the tensors that feed the split-bf16 GEMMs are stored split (HM + L parts,
  * DESIGN 6g): the workspace id of tensor `which`'s L part, or -1 when it is stored fp32 */
 int flsim_pn1_workspace_split_part(int which);
+/* (debug / tests) 1 when workspace tensor `which` is stored channel-slice-major, [samples][C/16]
+ * [H][W][16] (the inputs of conv2-4: a1, d1, a3), 0 when pixel-major [samples][H][W][C] */
+int flsim_pn1_workspace_slice_major(int which);
 /* packs theta_t into the kernel layouts and zeroes the slabs (start of main.py:126 epoch) */
 int flsim_pn1_begin_epoch(void* gradstate, const float* theta, flsim_stream_t stream);
 /* workers: device array of n_chunk_workers WorkerRec; worker_loss: device float per worker

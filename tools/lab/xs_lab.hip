@@ -23,6 +23,19 @@ struct Xs {
     float* hm;
     float* l;
 };
+
+// [img][pix][CI] split tensor -> channel-slice-major [img][CI/16][pix][16] (whole 16-B HM / 8-B L units)
+static __global__ void k_to_sm(const f32x4* hm, const f32x2* l, f32x4* hm_o, f32x2* l_o, long units,
+                               int hw, int ci4) {
+    const long u = (long)blockIdx.x * 256 + threadIdx.x;
+    if (u >= units) return;
+    const int c4 = (int)(u % ci4);
+    const long pix = u / ci4;
+    const long img = pix / hw, p = pix - img * hw;
+    const long o = ((img * (ci4 / 4) + c4 / 4) * hw + p) * 4 + (c4 & 3);
+    hm_o[o] = hm[u];
+    l_o[o] = l[u];
+}
 static Xs to_xs(const float* x, size_t n) {
     Xs s;
     CK(hipMalloc(&s.hm, n * 4));
@@ -116,6 +129,35 @@ static void conv(const char* tag, const float* X, const Xs& Xx, const float* W, 
            "%6.1f TF/s | differ xs %zu dx6 %zu\n",
            tag, BM, BN, t0, tf(t0), t1, tf(t1), 16 * DFM * DW, 16 * DFN, KB, DEPTH, NPL, t2, tf(t2),
            d1, d2);
+    if (getenv("LAB_SM")) {
+        // the same direct kernel over a channel-slice-major copy of X (A B A B on one box)
+        const long units = (long)S * IH * IH * CI / 4;
+        Xs sm;
+        CK(hipMalloc(&sm.hm, units * 16));
+        CK(hipMalloc(&sm.l, units * 8));
+        hipLaunchKernelGGL(k_to_sm, dim3((units + 255) / 256), dim3(256), 0, 0,
+                           reinterpret_cast<const f32x4*>(Xx.hm), reinterpret_cast<const f32x2*>(Xx.l),
+                           reinterpret_cast<f32x4*>(sm.hm), reinterpret_cast<f32x2*>(sm.l), units,
+                           IH * IH, CI / 4);
+        CK(hipDeviceSynchronize());
+        using AS = Im2colDirect<IH, IH, CI, PAD, DFM, false, OHX, XsSrcSM>;
+        AS as;
+        as.X = sm.hm;
+        as.XL = sm.l;
+        as.M = M;
+        auto kd = gemm_dx6_kernel<DFM, DFN, DW, KB, DEPTH, AD, BD, EpiBiasRelu>;
+        auto ks = gemm_dx6_kernel<DFM, DFN, DW, KB, DEPTH, AS, BD, EpiBiasRelu>;
+        const dim3 g(dtm * dtn);
+        const double s0 = timeit(ks, g, 64 * DW, as, bd, EpiBiasRelu{Y1, b, M, CO}, KP / GK, dtm, dtn);
+        const size_t d3 = ndiff(Y2, Y1, n);
+        const double p1 = timeit(kd, g, 64 * DW, ad, bd, EpiBiasRelu{Y2, b, M, CO}, KP / GK, dtm, dtn);
+        const double s1 = timeit(ks, g, 64 * DW, as, bd, EpiBiasRelu{Y1, b, M, CO}, KP / GK, dtm, dtn);
+        printf("%-16s dx6 %7.3f %7.3f ms | dx6 slice-major %7.3f %7.3f ms %6.1f TF/s (x%.3f) | "
+               "differs from dx6 in %zu\n", tag, t2, p1, s0, s1, tf(0.5 * (s0 + s1)),
+               (t2 + p1) / (s0 + s1), d3);
+        CK(hipFree(sm.hm));
+        CK(hipFree(sm.l));
+    }
     fflush(stdout);
 }
 
