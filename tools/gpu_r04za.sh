@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4: A B A B on one box, pixel-major conv2-4 inputs (tools/abx/libflsim_pm.so, built from the
-# previous commit) against channel-slice-major (the tree's libflsim.so, dgrad masks applied in LDS),
+# previous commit plus a stub of flsim_pn1_workspace_slice_major returning 0) against channel-slice-major (the tree's libflsim.so, dgrad masks applied in LDS),
 # then every GPU test on the tree's library.  Usage (repo root, GPU box): bash tools/gpu_r04za.sh <tag>
 set -u
 TAG=${1:-r04za}
