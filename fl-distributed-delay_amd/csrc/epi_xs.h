@@ -23,38 +23,17 @@ __device__ __forceinline__ f32x4 mask4(f32x4 t, uint32_t pos) {
 template <int NC, int AHW>
 __device__ __forceinline__ void mask_tile_sm(float* tile, int ld, const float* act, int m0, int rows,
                                              int n0, int n4, int tid, int nt) {
+    // (no runtime division and no batched loads: this runs in the GEMM kernels' epilogues, whose
+    // register peak sets their occupancy; r04zb measured a batched form at 104 against 80 VGPRs)
     const f32x2* a2 = reinterpret_cast<const f32x2*>(act);
-    const int total = rows * n4;
-    auto rc = [&](int q, int& r, int& c) {
-        const int s = q / (rows * 4), rem = q - s * rows * 4;
-        r = rem >> 2;
-        c = 4 * s + (rem & 3);
-    };
-    auto ld_h = [&](int q) {
-        int r, c;
-        rc(q, r, c);
-        return a2[2 * xs_unit<NC, AHW, true>((unsigned)(m0 + r), n0 / 4 + c)];
-    };
-    auto apply = [&](int q, f32x2 a) {
-        int r, c;
-        rc(q, r, c);
-        f32x4* t = reinterpret_cast<f32x4*>(tile + r * ld + 4 * c);
-        *t = mask4(*t, xs_pos4(a));
-    };
-    // a thread's first BATCH mask units are loaded before any is applied (one round trip)
-    constexpr int BATCH = 8;
-    f32x2 av[BATCH];
-#pragma unroll
-    for (int it = 0; it < BATCH; ++it) {
-        const int q = tid + it * nt;
-        if (q < total) av[it] = ld_h(q);
+    for (int s = 0; 4 * s < n4; ++s) {
+        for (int q = tid; q < rows * 4; q += nt) {
+            const int r = q >> 2, c = 4 * s + (q & 3);
+            const f32x2 a = a2[2 * xs_unit<NC, AHW, true>((unsigned)(m0 + r), n0 / 4 + c)];
+            f32x4* t = reinterpret_cast<f32x4*>(tile + r * ld + 4 * c);
+            *t = mask4(*t, xs_pos4(a));
+        }
     }
-#pragma unroll
-    for (int it = 0; it < BATCH; ++it) {
-        const int q = tid + it * nt;
-        if (q < total) apply(q, av[it]);
-    }
-    for (int q = tid + BATCH * nt; q < total; q += nt) apply(q, ld_h(q));
     __syncthreads();
 }
 
