@@ -2,6 +2,7 @@
 # round 4: A B A B on one box, pixel-major conv2-4 inputs (tools/abx/libflsim_pm.so, built from the
 # previous commit plus a stub of flsim_pn1_workspace_slice_major returning 0) against channel-slice-major (the tree's libflsim.so, dgrad masks applied in LDS),
 # then every GPU test on the tree's library.  Usage (repo root, GPU box): bash tools/gpu_r04za.sh <tag>
+# (tools/abx is listed in .gpurunignore since the round-4 A/B runs: copy the library back in to rerun)
 set -u
 TAG=${1:-r04za}
 OUT=gpurun_out/$TAG
