@@ -91,6 +91,11 @@ def parse():
                     help="skip timing the post-all-reduce server step (k_agg_stream) after the "
                          "timed window at N = 1")
     ap.add_argument("--no-probe", action="store_true")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="run the N > 1 code path at world size 1 (launch under torchrun "
+                         "--nproc-per-node 1): process group init, the per-epoch all-reduce of "
+                         "[S_t | losses] (RCCL with --backend nccl) and the streaming server step "
+                         "after it, instead of the fused single-GPU step")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI). gloo is for "
                          "rehearsing the N > 1 path with several ranks on one GPU (slow collective)")
@@ -237,11 +242,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         raise SystemExit(f"--gpus {args.gpus} != WORLD_SIZE {world}")
+    dist_on = world > 1 or args.force_dist
+    if args.force_dist and "MASTER_ADDR" not in os.environ:
+        raise SystemExit("--force-dist: launch under torch.distributed.run (MASTER_ADDR unset)")
     if args.backend == "gloo":   # rehearsal: ranks may share the box's GPU(s)
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if dist_on:
         if args.backend == "nccl":
             torch.distributed.init_process_group("nccl", device_id=dev)
         else:
@@ -259,7 +267,7 @@ def main():
         delays = heterogeneous_delays(args.n_workers)
     sim = FLSimulation(args.n_workers, delay=args.delay, delays=delays, throttle=throttle,
                        chunk_workers=args.chunk, device=dev, model=args.model, theta0=theta0,
-                       semantics=args.semantics)
+                       semantics=args.semantics, distributed=dist_on)
     if buffers:
         sim.engine.load_buffers(buffers)
     flop_per_ws = sim.engine.FLOP_PER_WORKER_STEP
@@ -272,9 +280,9 @@ def main():
         sim.epoch(sync_loss=False)
     torch.cuda.synchronize()
     probe = None if args.no_probe else KernelProbe(capacity=64 * 1024)
-    sim.time_collective = world > 1
+    sim.time_collective = dist_on
     sim.rank_worker_steps = []
-    if world > 1:
+    if dist_on:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     # per-epoch device time from events on the compute stream (no host synchronisation in the
@@ -288,19 +296,19 @@ def main():
         ws += int(sim.trace[-1].computes.sum())
         evs[j + 1].record()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
     epoch_ms = [evs[j].elapsed_time(evs[j + 1]) for j in range(args.steps)]
     coll_ms = sim.collective_ms()
     rank_ws = int(sum(sim.rank_worker_steps))
-    if world > 1:
+    if dist_on:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     losses = sim.losses()
     rank_ws_all = [rank_ws]
-    if world > 1:
+    if dist_on:
         t = torch.tensor([rank_ws], device=dev, dtype=torch.int64)
         g = [torch.zeros_like(t) for _ in range(world)]
         torch.distributed.all_gather(g, t)
@@ -361,7 +369,7 @@ def main():
                  "aggregate_adam_seq": "k_agg_stream (general entry order)"}[agg_name]
         # profiles/traffic.json is measured on the default workload (PerformantNet1, n = 1024,
         # one GPU): only borrowed for that workload and the same kernel
-        same = args.model == "PerformantNet1" and delays is None and world == 1 and \
+        same = args.model == "PerformantNet1" and delays is None and not dist_on and \
             args.n_workers == 1024
         traffic = TRAFFIC.get(agg_name) if same else None
         agg = dict(kernel=kname, probe=agg_name, bound="hbm", achieved=round(gbps, 1),
@@ -412,12 +420,12 @@ def main():
                           "(aggregation.alg_bytes_per_launch); this is the rule()+Adam share "
                           "priced at the whole launch time")
     agg_stream = None
-    if world == 1 and probe is not None and args.model == "PerformantNet1" and not args.no_stream:
+    if not dist_on and probe is not None and args.model == "PerformantNet1" and not args.no_stream:
         agg_stream = stream_step_probe(sim)
 
     value = ws / elapsed
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not dist_on and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.n_workers, args.delay, throttle, args.model, args.configs0_epochs)
     if rank == 0:
         line = {
@@ -444,10 +452,11 @@ def main():
                                    + "128 samples/worker-step, Adam lr 1e-3",
                        "executed_worker_steps": ws, "chunk_workers": args.chunk,
                        "timed_epochs": [sim.trace[-args.steps].t, sim.trace[-1].t],
-                       "backend": (args.backend if world > 1 else None),
-                       "world_size": (torch.distributed.get_world_size() if world > 1 else 1),
+                       "backend": (args.backend if dist_on else None),
+                       "world_size": (torch.distributed.get_world_size() if dist_on else 1),
+                       "force_dist": bool(args.force_dist),
                        "parallelism": f"workers sharded over {world} GPU(s), "
-                                      f"{'1 RCCL all-reduce/step' if world > 1 and args.backend == 'nccl' else '1 gloo all-reduce/step (rehearsal)' if world > 1 else 'no collective'}"},
+                                      f"{'1 RCCL all-reduce/step' if dist_on and args.backend == 'nccl' else '1 gloo all-reduce/step (rehearsal)' if dist_on else 'no collective'}"},
             # executed GEMM FLOPs of this rank (the probe's per-launch counts: conv6 skips its
             # never-pooled border) / wall time / the fp32 MFMA peak (the bf16x6 GEMMs count their
             # fp32-equivalent FLOPs, so this can pass 1); the nominal SURVEY 8d count beside it
@@ -473,7 +482,7 @@ def main():
             "last_loss": losses[-1] if losses else None,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist_on:
         torch.distributed.destroy_process_group()
 
 

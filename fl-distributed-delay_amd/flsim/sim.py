@@ -60,7 +60,7 @@ class FLSimulation:
                  semantics="reference", dropout=True, chunk_workers=128, device=None, theta0=None,
                  group=None, max_throttle=32, pool=None, betas=(0.9, 0.999), eps=1e-8,
                  engine=None, device_pool=None, test_pool=None, model="PerformantNet1",
-                 fused=True, keep_S=False, batch_size=128):
+                 fused=True, keep_S=False, batch_size=128, distributed=None):
         if semantics not in SEMANTICS:
             raise NotImplementedError(f"semantics {semantics!r} (supported: {SEMANTICS})")
         self.n = int(n_workers)
@@ -98,6 +98,12 @@ class FLSimulation:
             self.world = dist.get_world_size(group)
         else:
             self.rank, self.world = 0, 1
+        # distributed: the world > 1 code path (sharding, the one all-reduce per epoch, the
+        # streaming server step after it).  Default: on iff world > 1; True at world = 1 runs that
+        # path over a one-rank process group (bench.py --force-dist: RCCL on a single GPU)
+        self.distributed = self.world > 1 if distributed is None else bool(distributed)
+        if self.distributed and not (dist.is_available() and dist.is_initialized()):
+            raise RuntimeError("distributed=True needs an initialised torch.distributed group")
         self.device = torch.device(device) if device is not None else \
             torch.device("cuda", torch.cuda.current_device())
         # engine / device_pool are injectable only so tests can drive the sharding and
@@ -150,7 +156,9 @@ class FLSimulation:
         for j in range(len(self.free_slots) - 1, -1, -1):
             if self.free_slots[j].numel() >= n:
                 return self.free_slots.pop(j)
-        return torch.empty(n, device=self.device)
+        slot = torch.empty(n, device=self.device)
+        slot[self.P:].zero_()     # the [P, Ppad) padding and the tail enter the all-reduce
+        return slot
 
     def _worker_table(self, t, workers, ks):
         """WorkerRec (t, i, k, 0) of this rank's computing workers, copied host->device from a
@@ -269,20 +277,21 @@ class FLSimulation:
         lo, hi = self.shard(active)
         eng = self.engine
         G = self.G                               # 128-sample groups (units) per worker-step
-        fused = self.fused and self.world == 1 and hasattr(eng, "server_step")
+        fused = self.fused and not self.distributed and hasattr(eng, "server_step")
         pushes = plan.pushed and self.semantics == "reference"
         # An epoch that pushes S_t onto the FIFO and ends with the streaming server step (world > 1,
         # or an engine without the fused step) builds S_t -- and all-reduces it -- straight in the
         # slot it pushes, a whole [S_t | losses] comm buffer: the stream then reads S_t from the slot
         # and writes no second copy (4P fewer HBM bytes at every tick).  BatchNorm runs
         # keep the shared buffer (their comm buffer also holds n x the per-call statistics).
-        in_slot = pushes and not fused and not self.nstat
+        # (keep_S: S_t stays in comm[:P], where the caller reads it)
+        in_slot = pushes and not fused and not self.nstat and not self.keep_S
         comm = self._slot(self.stats_off) if in_slot else self.comm
         S = comm[:self.P]
         losses = comm[self.Ppad:self.Ppad + len(active) * G]
         stats = comm[self.stats_off:self.stats_off + len(active) * self.nstat].view(
             len(active), self.nstat)
-        if self.world > 1:
+        if self.distributed:
             losses.zero_()
             stats.zero_()
         eng.begin_epoch(self.theta)
@@ -303,7 +312,7 @@ class FLSimulation:
         if not fused or self.keep_S:
             eng.end_epoch(S)
         self.rank_worker_steps.append(hi - lo)
-        if self.world > 1:
+        if self.distributed:
             end = self.stats_off + len(active) * self.nstat if self.nstat else \
                 self.Ppad + len(active) * G
             self._all_reduce(comm[:end])
@@ -386,7 +395,7 @@ class FLSimulation:
         lo, hi = self.shard(fast)
         S = self.comm[:self.P]
         losses = self.comm[self.Ppad:self.Ppad + len(fast)]
-        if self.world > 1:
+        if self.distributed:
             losses.zero_()
         own_workers = np.asarray([i for _, ws in own for i in ws], np.int64)
         wt = self._worker_table(t, np.concatenate([own_workers, fast[lo:hi]]), ks)
@@ -419,7 +428,7 @@ class FLSimulation:
                 S.add_(slot[:self.P])
                 self.free_slots.append(slot)
         self.rank_worker_steps.append(hi - lo + len(own_workers))
-        if self.world > 1:
+        if self.distributed:
             self._all_reduce(self.comm[:self.Ppad + len(fast)])
         self.step += 1
         eng.aggregate_adam_sum(S, len(fast) + len(plan.stale), self.theta, self.m, self.v,

@@ -59,22 +59,29 @@ class StandInEngine:
         theta -= lr * tot / rule.k
 
 
-def _run(rank, world, n, d, thr, epochs, out, port, delays=None, semantics="reference"):
+def _run(rank, world, n, d, thr, epochs, out, port, delays=None, semantics="reference",
+         force=False):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, os.path.dirname(here))
     sys.path.insert(0, os.path.join(os.path.dirname(here), "fl-distributed-delay_amd"))
-    if world > 1:
+    if world > 1 or force:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
         dist.init_process_group("gloo", rank=rank, world_size=world)
     from flsim.sim import FLSimulation
     sim = FLSimulation(n, delay=d, delays=delays, throttle=thr, device="cpu", semantics=semantics,
-                       engine=StandInEngine(), device_pool=object(), theta0=torch.zeros(P))
+                       engine=StandInEngine(), device_pool=object(), theta0=torch.zeros(P),
+                       distributed=True if force else None)
+    calls = []
+    if force:                    # count the epoch's collectives (events are CUDA-only)
+        inner = sim._all_reduce
+        sim._all_reduce = lambda buf: (calls.append(buf.numel()), inner(buf))
     losses = [sim.epoch() for _ in range(epochs)]
     res = dict(theta=sim.theta.numpy().copy(), losses=losses,
-               trace=[(p.t, p.computes.tobytes(), p.stale) for p in sim.trace])
-    if world > 1:
+               trace=[(p.t, p.computes.tobytes(), p.stale) for p in sim.trace],
+               distributed=sim.distributed, collectives=len(calls))
+    if world > 1 or force:
         dist.destroy_process_group()
     out[rank] = res
 
@@ -128,3 +135,26 @@ def test_two_rank_independent_entries_match_single(delays):
         np.testing.assert_allclose(out[r]["losses"], single[0]["losses"], rtol=0, atol=1e-6)
         np.testing.assert_allclose(out[r]["theta"], single[0]["theta"], rtol=1e-5, atol=1e-7)
     assert np.array_equal(out[0]["theta"], out[1]["theta"])
+
+
+def test_forced_distributed_world1_matches_single():
+    """bench.py --force-dist at world size 1: the N > 1 code path (sharding, the per-epoch
+    all-reduce of [S_t | losses], the streaming server step after it) over a one-rank group must
+    give the single-process run's trace, losses and theta, with one collective per epoch."""
+    n, d, epochs = 11, 3, 7
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
+    single = mgr.dict()
+    _run(0, 1, n, d, True, epochs, single, 0)
+    out = mgr.dict()
+    port = 29500 + (os.getpid() % 1000) + 29
+    p = ctx.Process(target=_run, args=(0, 1, n, d, True, epochs, out, port, None, "reference",
+                                       True))
+    p.start()
+    p.join(300)
+    assert p.exitcode == 0
+    assert out[0]["distributed"] and not single[0]["distributed"]
+    assert out[0]["collectives"] == epochs
+    assert out[0]["trace"] == single[0]["trace"]
+    np.testing.assert_array_equal(out[0]["losses"], single[0]["losses"])
+    np.testing.assert_array_equal(out[0]["theta"], single[0]["theta"])

@@ -81,8 +81,15 @@ def test_n1024_d50_through_first_tick(pool, golden):
 # These 52-epoch ratios are chaotic: builds whose teacher-forced gradients agree to 4 digits measured
 # 1.61 / 0.81-1.27 (fp32 MFMA, r03a), 1.74 / 0.91 (split-bf16, bias column sum on the VALU, r04e)
 # and 2.75 / 1.26 (the same with the column sum on the MFMA, r04j).
-GAP_C = 4.1
+GAP_C = 4.1      # logged only (MEASURED loss_gap_ratio_max), see below
 DRIFT_C = 1.9
+# The gate that is not chaotic: over the epochs where the CPU fp32 port still
+# agrees with fp64 (its running-max loss gap <= AGREE = 5e-5: epochs 0-35 of traj_n10.npz, well
+# before the divergence of epochs 41-44), the GPU's running-max loss gap must stay within 2x the
+# CPU's (SURVEY 8(c)'s factor) plus WINDOW_FLOOR = 2e-5, twice the per-worker-step loss tolerance
+# of the teacher-forced tests (1e-5): a handful of ulps of an fp32 mean of 5 losses near 2.0 that
+# any fp32 forward order can move.
+AGREE, WINDOW_FLOOR = 5e-5, 2e-5
 
 
 def test_n10_d50_trajectory_drift_vs_oracle(pool, golden, tmp_path):
@@ -138,7 +145,16 @@ def test_n10_d50_trajectory_drift_vs_oracle(pool, golden, tmp_path):
         loss_gap_gpu_final=float(gap_gpu[-1]), loss_gap_cpu_final=float(gap_cpu[-1]),
         drift_ratio=[float(a / b) for a, b in zip(d_gpu, d_cpu)],
         drift_gpu=[float(x) for x in d_gpu], drift_cpu=[float(x) for x in d_cpu])))
-    assert np.all(gap_gpu <= GAP_C * gap_cpu + 2e-4), (gap_gpu, gap_cpu)
+    win = gap_cpu <= AGREE
+    assert win[:30].all(), gap_cpu[:30]
+    ratio_win = float(np.max(gap_gpu[win] / (2 * gap_cpu[win] + WINDOW_FLOOR)))
+    print("MEASURED", json.dumps(dict(test="n10_d50_agreement_window", epochs=int(win.sum()),
+                                      gap_gpu=[float(x) for x in gap_gpu[win]],
+                                      gap_cpu=[float(x) for x in gap_cpu[win]],
+                                      ratio_to_bound=ratio_win)))
+    assert ratio_win <= 1.0, (ratio_win, gap_gpu[win], gap_cpu[win])
+    # the 52-epoch loss-gap ratio (chaotic past epoch ~40) is logged above, not asserted
+    # (VERDICT r04 item 1); GAP_C stays as the figure DESIGN 7 tables it against
     for t, dg, dc in zip(at, d_gpu, d_cpu):
         assert dg <= DRIFT_C * dc, (t, dg, dc)
 

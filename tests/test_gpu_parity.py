@@ -405,39 +405,50 @@ def test_gradient_teacher_forced_decisions(pool, dropout, items):
              e1=torch.from_numpy(W(10, (NS, 512))), e2=torch.from_numpy(W(11, (NS, 256))),
              i1=W(19, (NS, 18, 18, 48), torch.uint8), i2=W(20, (NS, 11, 11, 96), torch.uint8),
              i3=W(21, (NS, 7, 7, 192), torch.uint8))
-    P = [torch.tensor(a, requires_grad=True) for a in MR.split_flat(sim.theta.astype(np.float64))]
-    (w1, b1, w2, b2, w3, b3, w4, b4, w5, b5, w6, b6, l1w, l1b, l2w, l2b, l3w, l3b) = P
-    m = lambda t: (t > 0).to(torch.float64)
-    s50 = 2.0 if dropout else 1.0
-    lrefs = []
-    for wi, it in enumerate(items):
-        sl = slice(128 * wi, 128 * (wi + 1))
-        a = {k: v[sl] for k, v in A.items()}
-        x, y = sim.batch(*it, dtype=torch.float64)
-        noise = MR.dropout_noise(0, it[0], it[1], 128, torch.float64) if dropout else None
-        h = F.conv2d(x, w1, b1, padding=2) * m(a["a1"])
-        h = _gather_pool(F.conv2d(h, w2, b2, padding=2), a["i1"]) * m(a["d1"])
-        h = h * noise[0] if dropout else h
-        h = F.conv2d(h, w3, b3, padding=2) * m(a["a3"])
-        h = _gather_pool(F.conv2d(h, w4, b4, padding=2), a["i2"]) * m(a["d2"])
-        h = h * noise[1] if dropout else h
-        h = F.conv2d(h, w5, b5, padding=2) * m(a["a5"])
-        h = _gather_pool(F.conv2d(h, w6, b6, padding=2), a["i3"]).reshape(128, -1) * m(a["d3"])
-        h = h * noise[2].reshape(128, -1) if dropout else h
-        h = F.linear(h, l1w, l1b) * m(a["e1"]) * s50
-        h = F.linear(h, l2w, l2b) * m(a["e2"]) * s50
-        lref = F.cross_entropy(F.linear(h, l3w, l3b), y)
-        lref.backward()
-        lrefs.append(lref.item())
+    import _flips
+
+    def forced(dt):
+        """the reference forward + backward in dtype dt with the GPU's decisions"""
+        np_dt = np.float64 if dt == torch.float64 else np.float32
+        P = [torch.tensor(a, requires_grad=True) for a in MR.split_flat(sim.theta.astype(np_dt))]
+        (w1, b1, w2, b2, w3, b3, w4, b4, w5, b5, w6, b6, l1w, l1b, l2w, l2b, l3w, l3b) = P
+        m = lambda t: (t > 0).to(dt)                                      # noqa: E731
+        s50 = 2.0 if dropout else 1.0
+        lrefs = []
+        for wi, it in enumerate(items):
+            sl = slice(128 * wi, 128 * (wi + 1))
+            a = {k: v[sl] for k, v in A.items()}
+            x, y = sim.batch(*it, dtype=dt)
+            noise = MR.dropout_noise(0, it[0], it[1], 128, dt) if dropout else None
+            h = F.conv2d(x, w1, b1, padding=2) * m(a["a1"])
+            h = _gather_pool(F.conv2d(h, w2, b2, padding=2), a["i1"]) * m(a["d1"])
+            h = h * noise[0] if dropout else h
+            h = F.conv2d(h, w3, b3, padding=2) * m(a["a3"])
+            h = _gather_pool(F.conv2d(h, w4, b4, padding=2), a["i2"]) * m(a["d2"])
+            h = h * noise[1] if dropout else h
+            h = F.conv2d(h, w5, b5, padding=2) * m(a["a5"])
+            h = _gather_pool(F.conv2d(h, w6, b6, padding=2), a["i3"]).reshape(128, -1) * m(a["d3"])
+            h = h * noise[2].reshape(128, -1) if dropout else h
+            h = F.linear(h, l1w, l1b) * m(a["e1"]) * s50
+            h = F.linear(h, l2w, l2b) * m(a["e2"]) * s50
+            lref = F.cross_entropy(F.linear(h, l3w, l3b), y)
+            lref.backward()
+            lrefs.append(lref.item())
+        return torch.cat([p.grad.reshape(-1) for p in P]).double().numpy(), lrefs
+
+    g_tf, lrefs = forced(torch.float64)
+    g_tf32, _ = forced(torch.float32)
     g = S.cpu().numpy().astype(np.float64)
     off = 0
     worst = {}
-    for (name, _), p in zip(PN1_SHAPES, P):
-        n = p.numel()
-        worst[name] = _rel_l2(g[off:off + n], p.grad.reshape(-1).numpy())
+    for (name, shp) in PN1_SHAPES:
+        n = int(np.prod(shp))
+        worst[name] = _rel_l2(g[off:off + n], g_tf[off:off + n])
         off += n
     np.testing.assert_allclose(loss.cpu().numpy(), lrefs, atol=1e-5)
     assert max(worst.values()) <= 2e-5, worst
+    # SURVEY 8(c): per tensor no farther from fp64 than 2x the CPU fp32 port (same decisions)
+    _flips.assert_survey(_flips.survey_ratios(g, g_tf32, g_tf, PN1_SHAPES), "pn1_teacher_forced")
 
 
 def test_eval_predictions_match_oracle(pool):

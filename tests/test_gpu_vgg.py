@@ -66,12 +66,13 @@ def _run(theta_np, items, dropout, pool, n_total=4):
     return eng, S.cpu().numpy().astype(np.float64), loss.cpu().numpy()
 
 
-def _teacher_forced(sim, eng, items, dropout):
+def _teacher_forced(sim, eng, items, dropout, dt=torch.float64):
     """fp64 VGG-11 forward + backward that takes the GPU's own forward decisions (ReLU signs, max-
     pool argmax, dropout masks, read back from the workspace).  Returns the per-tensor gradient,
     the per-worker losses, and the number of GPU decisions that the fp64 pre-activations computed
     on the way disagree with (a ReLU sign, a pool argmax among live windows, a kept unit whose
-    fp64 pre-activation is <= 0): knife-edge decisions any fp32 order can take either way."""
+    fp64 pre-activation is <= 0): knife-edge decisions any fp32 order can take either way.
+    dt = torch.float32: the CPU fp32 port given the same decisions (SURVEY 8(c)'s comparison)."""
     import torch.nn.functional as F
     import _flips
     from flsim.engine import VGG11Engine
@@ -84,25 +85,26 @@ def _teacher_forced(sim, eng, items, dropout):
         return eng.workspace_view(ids[name], shp, dt).cpu().numpy()
 
     def nchw(a):
-        return torch.from_numpy(np.ascontiguousarray(a.transpose(0, 3, 1, 2))).double()
+        return torch.from_numpy(np.ascontiguousarray(a.transpose(0, 3, 1, 2))).to(dt)
 
     A = dict(d1=nchw(W("d1", (NS, 16, 16, 64))), d2=nchw(W("d2", (NS, 8, 8, 128))),
              a3=nchw(W("a3", (NS, 8, 8, 256))), d4=nchw(W("d4", (NS, 4, 4, 256))),
              a5=nchw(W("a5", (NS, 4, 4, 512))), d6=nchw(W("d6", (NS, 2, 2, 512))),
-             a7=nchw(W("a7", (NS, 2, 2, 512))), f0=torch.from_numpy(W("f0", (NS, 512))).double(),
-             e1=torch.from_numpy(W("e1", (NS, 512))).double(),
-             e2=torch.from_numpy(W("e2", (NS, 512))).double(),
+             a7=nchw(W("a7", (NS, 2, 2, 512))), f0=torch.from_numpy(W("f0", (NS, 512))).to(dt),
+             e1=torch.from_numpy(W("e1", (NS, 512))).to(dt),
+             e2=torch.from_numpy(W("e2", (NS, 512))).to(dt),
              i1=W("i1", (NS, 16, 16, 64), torch.uint8), i2=W("i2", (NS, 8, 8, 128), torch.uint8),
              i4=W("i4", (NS, 4, 4, 256), torch.uint8), i6=W("i6", (NS, 2, 2, 512), torch.uint8),
              i8=W("i8", (NS, 1, 1, 512), torch.uint8))
+    np_dt = np.float64 if dt == torch.float64 else np.float32
     P = [torch.tensor(a, requires_grad=True)
-         for a in MR.split_flat(sim.theta.astype(np.float64), M)]
+         for a in MR.split_flat(sim.theta.astype(np_dt), M)]
     cw, cb = P[0:16:2], P[1:16:2]
     l1w, l1b, l2w, l2b, l3w, l3b = P[16:]
     flips = [0]
 
     def m(t):
-        return (t > 0).to(torch.float64)
+        return (t > 0).to(dt)
 
     def conv(h, j):
         return F.conv2d(h, cw[j], cb[j], padding=1)
@@ -127,7 +129,7 @@ def _teacher_forced(sim, eng, items, dropout):
     for wi, it in enumerate(items):
         sl = slice(128 * wi, 128 * (wi + 1))
         a = {k: v[sl] for k, v in A.items()}
-        x, y = sim.batch(*it, dtype=torch.float64)
+        x, y = sim.batch(*it, dtype=dt)
         h = pool(conv(x, 0), a["i1"], a["d1"])
         h = pool(conv(h, 1), a["i2"], a["d2"])
         h = relu(conv(h, 2), a["a3"])
@@ -142,7 +144,7 @@ def _teacher_forced(sim, eng, items, dropout):
         lref = F.cross_entropy(F.linear(h, l3w, l3b), y)
         lref.backward()
         lrefs.append(lref.item())
-    g = np.concatenate([p.grad.reshape(-1).numpy() for p in P])
+    g = np.concatenate([p.grad.reshape(-1).double().numpy() for p in P])
     return g, lrefs, flips[0]
 
 
@@ -198,6 +200,10 @@ def test_vgg_gradient_teacher_forced_decisions(pool, dropout, items):
     np.testing.assert_allclose(loss, lrefs, atol=1e-5)
     assert max(worst.values()) <= TF_TOL, worst
     assert flips <= 8 * len(items), flips
+    # per tensor no farther from fp64 than 2x the CPU fp32 port (same decisions)
+    import _flips
+    g_tf32, _, _ = _teacher_forced(sim, eng, items, dropout, torch.float32)
+    _flips.assert_survey(_flips.survey_ratios(g, g_tf32, g_tf, VGG11_SHAPES), "vgg11_teacher_forced")
 
 
 def test_vgg_simulation_matches_oracle_trajectory(pool):

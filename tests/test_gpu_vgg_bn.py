@@ -160,42 +160,56 @@ def test_vgg_bn_gradient_teacher_forced_decisions(pool, dropout, items):
              i1=W("i1", (NS, 16, 16, 64), torch.uint8), i2=W("i2", (NS, 8, 8, 128), torch.uint8),
              i4=W("i4", (NS, 4, 4, 256), torch.uint8), i6=W("i6", (NS, 2, 2, 512), torch.uint8),
              i8=W("i8", (NS, 1, 1, 512), torch.uint8))
-    P = [torch.tensor(a, requires_grad=True)
-         for a in MR.split_flat(sim.theta.astype(np.float64), M)]
-    cw, cb, gw, gb = P[0:32:4], P[1:32:4], P[2:32:4], P[3:32:4]
-    l1w, l1b, l2w, l2b, l3w, l3b = P[32:]
+    def forced(dt):
+        """fp64 (or, for SURVEY 8(c), the CPU fp32 port's) forward + backward with the GPU's
+        decisions and each worker's own batch statistics"""
+        np_dt = np.float64 if dt == torch.float64 else np.float32
+        P = [torch.tensor(a, requires_grad=True)
+             for a in MR.split_flat(sim.theta.astype(np_dt), M)]
+        cw, cb, gw, gb = P[0:32:4], P[1:32:4], P[2:32:4], P[3:32:4]
+        l1w, l1b, l2w, l2b, l3w, l3b = P[32:]
+        Ad = {k: (v.to(dt) if torch.is_tensor(v) else v) for k, v in A.items()}
 
-    def m(t):
-        return (t > 0).to(torch.float64)
+        def m(t):
+            return (t > 0).to(dt)
 
-    def conv(h, j):
-        z = F.conv2d(h, cw[j], cb[j], padding=1)
-        return F.batch_norm(z, None, None, gw[j], gb[j], True, 0.1, 1e-5)
+        def conv(h, j):
+            z = F.conv2d(h, cw[j], cb[j], padding=1)
+            return F.batch_norm(z, None, None, gw[j], gb[j], True, 0.1, 1e-5)
 
-    s50 = 2.0 if dropout else 1.0
-    lrefs = []
-    for wi, it in enumerate(items):
-        sl = slice(128 * wi, 128 * (wi + 1))
-        a = {k: v[sl] for k, v in A.items()}
-        x, y = sim.batch(*it, dtype=torch.float64)
-        h = _gather_pool(conv(x, 0), a["i1"]) * m(a["d1"])
-        h = _gather_pool(conv(h, 1), a["i2"]) * m(a["d2"])
-        h = conv(h, 2) * m(a["a3"])
-        h = _gather_pool(conv(h, 3), a["i4"]) * m(a["d4"])
-        h = conv(h, 4) * m(a["a5"])
-        h = _gather_pool(conv(h, 5), a["i6"]) * m(a["d6"])
-        h = conv(h, 6) * m(a["a7"])
-        h = _gather_pool(conv(h, 7), a["i8"]).reshape(128, 512) * m(a["f0"]) * s50
-        h = F.linear(h, l1w, l1b) * m(a["e1"]) * s50
-        h = F.linear(h, l2w, l2b) * m(a["e2"])
-        lref = F.cross_entropy(F.linear(h, l3w, l3b), y)
-        lref.backward()
-        lrefs.append(lref.item())
+        s50 = 2.0 if dropout else 1.0
+        lrefs = []
+        for wi, it in enumerate(items):
+            sl = slice(128 * wi, 128 * (wi + 1))
+            a = {k: v[sl] for k, v in Ad.items()}
+            x, y = sim.batch(*it, dtype=dt)
+            h = _gather_pool(conv(x, 0), a["i1"]) * m(a["d1"])
+            h = _gather_pool(conv(h, 1), a["i2"]) * m(a["d2"])
+            h = conv(h, 2) * m(a["a3"])
+            h = _gather_pool(conv(h, 3), a["i4"]) * m(a["d4"])
+            h = conv(h, 4) * m(a["a5"])
+            h = _gather_pool(conv(h, 5), a["i6"]) * m(a["d6"])
+            h = conv(h, 6) * m(a["a7"])
+            h = _gather_pool(conv(h, 7), a["i8"]).reshape(128, 512) * m(a["f0"]) * s50
+            h = F.linear(h, l1w, l1b) * m(a["e1"]) * s50
+            h = F.linear(h, l2w, l2b) * m(a["e2"])
+            lref = F.cross_entropy(F.linear(h, l3w, l3b), y)
+            lref.backward()
+            lrefs.append(lref.item())
+        return P, torch.cat([p.grad.reshape(-1) for p in P]).double().numpy(), lrefs
+
+    P, ref, lrefs = forced(torch.float64)
     np.testing.assert_allclose(loss, lrefs, atol=1e-5)
-    ref = torch.cat([p.grad.reshape(-1) for p in P]).numpy()
     # 1.5 x the split-bf16 build's measured worst, 4.31e-5 (features.1.bias, dropout items2;
     # profiles/r04/prof_r04e/tol.jsonl stores it as 0.861 of the former 5e-5 bound)
     _check_grad(g, ref, rtol=6.5e-5)
+    # SURVEY 8(c): per tensor no farther from fp64 than 2x the CPU fp32 port (same decisions);
+    # the conv biases ahead of a BatchNorm have an exact gradient of 0 (floor: the whole gradient)
+    import _flips
+    _, ref32, _ = forced(torch.float32)
+    _flips.assert_survey(_flips.survey_ratios(
+        g, ref32, ref, VGG11_BN_SHAPES,
+        whole_floor={n for n, _ in VGG11_BN_SHAPES if _is_conv_bias(n)}), "vgg11_bn_teacher_forced")
     # per-worker statistics of the chunk vs each worker's own BatchNorm batch (oracle, fp64)
     st = stats.double().cpu().numpy()
     for wi, it in enumerate(items):

@@ -70,6 +70,14 @@ def main():
                 row[cn.lower()[9:] + "_M"] = round(g(cn) / 1e6, 2)
         if g("GRBM_GUI_ACTIVE") is not None:
             row["grbm_gui_active_M"] = round(g("GRBM_GUI_ACTIVE") / 1e6, 2)
+            cyc = g("GRBM_GUI_ACTIVE") / 8          # cycles per XCD = the kernel's cycles
+            # utilisations over the chip: 1024 SIMDs (MFMA, VALU issue), 256 CUs (LDS array)
+            if g("SQ_VALU_MFMA_BUSY_CYCLES") is not None:
+                row["mfma_util"] = round(g("SQ_VALU_MFMA_BUSY_CYCLES") / (cyc * 1024), 3)
+            if g("SQ_LDS_IDX_ACTIVE") is not None:
+                row["lds_active_per_cu_cycle"] = round(g("SQ_LDS_IDX_ACTIVE") / (cyc * 256), 3)
+            if g("SQ_ACTIVE_INST_VALU") is not None:
+                row["valu_active_per_simd"] = round(4 * g("SQ_ACTIVE_INST_VALU") / (cyc * 1024), 3)
         row["raw"] = c
         rows.append(row)
     for r in rows:

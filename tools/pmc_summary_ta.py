@@ -1,4 +1,4 @@
-"""Per-kernel TA / TD / TCP busy and stall fractions from tools/gpu_r04x.sh's passes.
+"""Per-kernel TA / TD / TCP busy and stall fractions from tools/gpu_job.sh's tatd passes.
 
   python tools/pmc_summary_ta.py gpurun_out/<tag>
 
