@@ -17,6 +17,8 @@
 #   facade            tools/facade_bench.py (the FL.agents reference loop, n = 1024)
 #   configs           tools/gpu_configs_all.sh (the other BASELINE configs)
 #   lab:<bin>[:<arg>] a lab binary from tools/lab (built beforehand on the CPU)
+#   labab:<b0>:<b1>:<arg>  two lab binaries A B A B on the same box
+#   diag[:<pkg>]      tools/survey_diag.py (SURVEY 8(c) per tensor; <pkg>: another build's flsim)
 set -u
 TAG=${1:?tag}
 shift
@@ -131,6 +133,23 @@ for STEP in "$@"; do
         timeout -k 10 300 tools/lab/$BIN $ARG > $OUT/lab_$BIN${ARG:+_$ARG}.txt 2>&1 \
             || { echo "lab $BIN failed $?"; tail -5 $OUT/lab_$BIN*.txt; exit 1; }
         cat $OUT/lab_$BIN${ARG:+_$ARG}.txt ;;
+    labab:*)
+        IFS=: read -r _ B0 B1 ARG <<< "$STEP"
+        for r in 1 2; do
+            for B in $B0 $B1; do
+                timeout -k 10 300 tools/lab/$B $ARG > $OUT/labab_${B}_$r.txt 2>&1 \
+                    || { echo "lab $B failed $?"; tail -5 $OUT/labab_${B}_$r.txt; exit 1; }
+                sed "s/^/$B $r | /" $OUT/labab_${B}_$r.txt
+            done
+        done ;;
+    diag|diag:*)
+        PKG=${STEP#diag}; PKG=${PKG#:}
+        NAME=diag_$(basename ${PKG:-tree})
+        for IT in "0,1,2" "1,0,3 1,2,0"; do
+            timeout -k 10 300 python3 -u tools/survey_diag.py ${PKG:+--pkg $PKG} --items $IT \
+                >> $OUT/$NAME.txt 2>&1 || { echo "diag failed $?"; tail -5 $OUT/$NAME.txt; exit 1; }
+        done
+        grep -v SURVEY_DIAG $OUT/$NAME.txt ;;
     *)
         echo "unknown step $STEP"; exit 2 ;;
     esac

@@ -10,6 +10,7 @@
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -I include \
 //         -I fl-distributed-delay_amd/csrc tools/lab/xs_lab.hip -o tools/lab/xs_lab
 #include <cmath>
+#include <string>
 
 #include "gemm_dx6.h"
 #include "lab_common.h"
@@ -261,8 +262,19 @@ int main(int argc, char** argv) {
     float* S1 = dalloc(slabn, 0.f);
     float* B0 = dalloc(4096 * 192, 0.f);
     float* B1 = dalloc(4096 * 192, 0.f);
-    const char* only = argc > 1 ? argv[1] : "";
-    auto want = [&](const char* t) { return !*only || strstr(t, only); };
+    // argv[1]: a tag substring, or a comma-separated list of exact tags ("fwd6,dg4,wg6")
+    const std::string only = argc > 1 ? argv[1] : "";
+    auto want = [&](const char* t) {
+        if (only.empty()) return true;
+        if (only.find(',') == std::string::npos) return strstr(t, only.c_str()) != nullptr;
+        size_t p0 = 0;
+        while (p0 <= only.size()) {
+            const size_t p1 = std::min(only.find(',', p0), only.size());
+            if (only.compare(p0, p1 - p0, t) == 0 && strlen(t) == p1 - p0) return true;
+            p0 = p1 + 1;
+        }
+        return false;
+    };
     // C(tag, IH, CI, PAD, OHX, CO, x6 tile FM FN WM WN, direct DFM DFN WAVES KB DEPTH NPL)
 #define C(tag, IH, CI, PAD, OHX, CO, FM, FN, WM, WN, DFM, DFN, DW, KB, DEP, NPL) \
     if (want(tag)) conv<IH, CI, PAD, OHX, CO, FM, FN, WM, WN, DFM, DFN, DW, KB, DEP, NPL>( \
