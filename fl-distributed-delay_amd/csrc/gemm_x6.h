@@ -101,48 +101,22 @@ constexpr int km_ld(int rows, int tpr) {
     return rows + 8;
 }
 
-// k-contiguous split tiles hold the HM units as they stand plus a plane of the 8-B L units
-// (FLSIM_KC_HML = 1, round 5) instead of two 16-B combination planes ([h|m] and [h|l] / [l|h]):
-// the h half was stored, and read, twice.  [h|l] and [l|h] are assembled in registers from the
-// HM fragment and one ds_read_b64 of the L plane: 24 instead of 32 LDS bytes per unit written
-// and read.  Bit-identical (the same MFMA operands).
-#ifndef FLSIM_KC_HML
-#define FLSIM_KC_HML 1
-#endif
-
-// L plane of a k-contiguous tile: [rows][4 units x 8 B]; rows r and r + 8 of a fragment would
-// share banks in a ds_read_b64 (32 lanes = 16 rows x 2 units, 32-B rows), so rows with bit 3 set
-// store their units in the other half of the row (unit u at slot u ^ 2): conflict-free reads, and
-// the 16-lane groups of a ds_write_b64 (4 rows x 4 units, 128 contiguous bytes) stay conflict-free
-__device__ __forceinline__ int kc_l_off(int row, int unit) {
-    return 8 * row + 2 * (unit ^ (((row >> 3) & 1) << 1));
-}
-// the same for a fragment read, rows r0 + (lane & 15) with r0 % 16 == 0: the lane-dependent part
-// apart, so the per-fragment part is an immediate offset of one base address
-__device__ __forceinline__ int kc_l_frag_off(int lane) {
-    return 8 * (lane & 15) + 2 * ((lane >> 4) ^ (((lane >> 3) & 1) << 1));
-}
-
 // One operand tile of a stage.  AROLE: the A side ([h|m], [h|l]) or the B side ([h|m], [m|h],
-// [l|h]).  KC: the HM plane laid out and swizzled like the fp32 KC tile plus the L plane
-// (kc_l_off); KM: planes h, m, l as [16][LD] bf16 (LD = km_ld: conflict-free transposed reads),
-// one spare 8-B slot after each for surplus units.  TPR: the loader's threads per k row (NT / 16).
+// [l|h]).  KC: combination planes laid out like the fp32 KC tile; KM: planes h, m, l as
+// [16][LD] bf16 (LD = km_ld: conflict-free transposed reads), one spare 8-B slot after each for
+// surplus units.  TPR: the loader's threads per k row (NT / 16).
 template <bool KC, int ROWS, bool AROLE, int TPR = 16>
 struct X6Tile {
     static constexpr int LD = km_ld(ROWS, TPR);
-    static constexpr bool HML = KC && FLSIM_KC_HML;
     static constexpr int NPL = KC ? 2 : 3;
     static constexpr int PLANE_FL = KC ? KCTile<ROWS>::FLOATS : (GK * LD + 4) / 2;
-    static constexpr int FL = HML ? KCTile<ROWS>::FLOATS + 8 * ROWS : NPL * PLANE_FL;
+    static constexpr int FL = NPL * PLANE_FL;
     struct Frag {
         f32x4 x0, x1, x2;
     };
     // a unit already in the split form (split.h: loaders over HM / L tensors): plane stores only
     __device__ static void store(float* s, int a, int b, const XsUnit& v, bool valid) {
-        if constexpr (HML) {
-            store_unit<true, ROWS>(s, a, b, v.hm);
-            *reinterpret_cast<f32x2*>(s + PLANE_FL + kc_l_off(a, b)) = v.l;
-        } else if constexpr (KC) {
+        if constexpr (KC) {
             store_unit<true, ROWS>(s, a, b, v.hm);
             store_unit<true, ROWS>(s + PLANE_FL, a, b, AROLE ? xs_hl(v) : xs_lh(v));
         } else {
@@ -159,17 +133,7 @@ struct X6Tile {
     }
     __device__ static Frag frag(const float* s, int r0, int lane) {
         Frag f;
-        if constexpr (HML) {
-            f.x0 = read_frag<true, ROWS>(s, r0, lane);                        // [h|m]
-            const f32x2 l = *reinterpret_cast<const f32x2*>(s + PLANE_FL + 8 * r0 +
-                                                            kc_l_frag_off(lane));
-            if constexpr (AROLE) {
-                f.x1 = f32x4{f.x0.x, f.x0.y, l.x, l.y};                       // [h|l]
-            } else {
-                f.x1 = f32x4{f.x0.z, f.x0.w, f.x0.x, f.x0.y};                 // [m|h]
-                f.x2 = f32x4{l.x, l.y, f.x0.x, f.x0.y};                       // [l|h]
-            }
-        } else if constexpr (KC) {
+        if constexpr (KC) {
             f.x0 = read_frag<true, ROWS>(s, r0, lane);                        // [h|m]
             if constexpr (AROLE) {
                 f.x1 = read_frag<true, ROWS>(s + PLANE_FL, r0, lane);         // [h|l]

@@ -531,7 +531,9 @@ static bool concurrent_backward(int S) {
     return S <= smax;
 }
 
-// debug / measurement: FLSIM_DEBUG_BWD_STOP=6 ends the backward pass after conv6's data gradient
+// debug / measurement: FLSIM_DEBUG_BWD_STOP=6 / 5 / 4 ends the backward pass after conv6's /
+// conv5's / conv4's data gradient (dz5 in gx / gxl split; dz4 in a4 / a4l split; dz3 in gx fp32),
+// so each data-gradient GEMM can be checked on its own inputs (tools/gemm_diag.py)
 static int debug_stop() {
     static int v = -1;
     if (v < 0) {
@@ -618,6 +620,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC((xs<13, 13, 192, 0, 4, 3, 4, 2, false, 0>(dz5, S, g.wdx[4], 96, 1728,
         EpiDropScatterXs<11, 11, 96>{dz4.hm, dz4.l, w.d2, w.i2, s25, S * 11 * 11}, st, K_DG5,
         1728)));
+    if (debug_stop() == 5) return join();         // (debug: dz4 in a4 / a4l, dz5 in gx / gxl)
     // ---- conv4: wgrad (input a3), bias, dgrad -> dz3 = . * (a3 > 0) into gx (fp32) ----
     // dz3 and dz2 stay fp32: their data gradients have N = 48 columns, where the fp32 MFMA
     // kernels are faster than any split-bf16 form (profiles/r04/lab/lab_xs_r04b.txt: conv3's
@@ -630,6 +633,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
         dz4.l, w.a3l)));
     RC((xs<22, 22, 96, 0, 4, 3, 4, 2, false, 0>(dz4, S, g.wdx[3], 96, 864,
         EpiMaskXs<96, false, true, 400>{w.gx, nullptr, w.a3, S * 20 * 20}, st, K_DG4, 864)));
+    if (debug_stop() == 4) return join();         // (debug: dz3 in gx fp32, dz4 in a4 / a4l)
     float* dz3 = w.gx;
     // ---- conv3: wgrad (input d1), bias, dgrad -> grad wrt d1 (site 1), scattered through pool1
     //      straight into dz2 (a2 buffer, fp32) ----
@@ -700,8 +704,12 @@ int flsim_pn1_workspace_offset(int which, int samples, long* offset_bytes) {
 }
 
 // a workspace tensor held in the split-bf16 form (split.h): the id of its L part (its HM part is
-// `which` itself), or -1 for an fp32 tensor.  gx is fp32 after a backward pass (dz1).
+// `which` itself), or -1 for an fp32 tensor.  gx is fp32 after a full default backward pass (dz1);
+// with FLSIM_DEBUG_BWD_STOP=6 or 5 it holds the split dz5.  (With FLSIM_C1_FUSE=1, dz1 is never
+// written and gx holds dz3 in fp32.)
 int flsim_pn1_workspace_split_part(int which) {
+    if (which == 14 && (debug_stop() == 6 || debug_stop() == 5))
+        return 30;             // gx holds the split dz5 when the pass stopped after conv6 / conv5
     switch (which) {
         case 1: return 22;     // a1
         case 3: return 23;     // d1

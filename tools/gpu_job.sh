@@ -19,6 +19,8 @@
 #   lab:<bin>[:<arg>] a lab binary from tools/lab (built beforehand on the CPU)
 #   labab:<b0>:<b1>:<arg>  two lab binaries A B A B on the same box
 #   diag[:<pkg>]      tools/survey_diag.py (SURVEY 8(c) per tensor; <pkg>: another build's flsim)
+#   gemmdiag          tools/gemm_diag.py for the conv6 / conv5 / conv4 data-gradient GEMMs
+#   facadetrace       rocprofv3 kernel trace of tools/facade_bench.py + tools/trace_gaps.py
 set -u
 TAG=${1:?tag}
 shift
@@ -126,6 +128,13 @@ for STEP in "$@"; do
         timeout -k 10 600 python3 -u tools/facade_bench.py > $OUT/facade_bench.json 2> $OUT/facade_bench.err \
             || { echo "facade failed $?"; tail -5 $OUT/facade_bench.err; exit 1; }
         cut -c1-400 $OUT/facade_bench.json ;;
+    facadetrace)
+        timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/ftrace -o run \
+            -- python3 tools/facade_bench.py --epochs 2 > $OUT/facade_trace.log 2>&1 \
+            || { echo "facade trace failed $?"; tail -5 $OUT/facade_trace.log; exit 1; }
+        D=$(dirname $(find $OUT/ftrace -name "run_kernel_trace.csv" | head -1))
+        cp $D/run_kernel_stats.csv $OUT/facade_kernel_stats.csv
+        python3 tools/trace_gaps.py $D 0.5 > $OUT/facade_gaps.txt && head -30 $OUT/facade_gaps.txt ;;
     configs)
         bash tools/gpu_configs_all.sh $TAG || exit 1 ;;
     lab:*)
@@ -150,6 +159,12 @@ for STEP in "$@"; do
                 >> $OUT/$NAME.txt 2>&1 || { echo "diag failed $?"; tail -5 $OUT/$NAME.txt; exit 1; }
         done
         grep -v SURVEY_DIAG $OUT/$NAME.txt ;;
+    gemmdiag)
+        for ST in 6 5 4; do
+            FLSIM_DEBUG_BWD_STOP=$ST timeout -k 10 300 python3 -u tools/gemm_diag.py >> $OUT/gemm_diag.txt 2>&1 \
+                || { echo "gemm diag $ST failed $?"; tail -5 $OUT/gemm_diag.txt; exit 1; }
+        done
+        grep GEMM_DIAG $OUT/gemm_diag.txt ;;
     *)
         echo "unknown step $STEP"; exit 2 ;;
     esac
