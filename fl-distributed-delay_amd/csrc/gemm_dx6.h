@@ -160,7 +160,7 @@ gemm_dx6_kernel(AD ad, BL bl, EPI epi, int ksteps, int tiles_m, int tiles_n) {
                     x1 = f32x4{x0.z, x0.w, x0.x, x0.y};
 #pragma unroll
                 for (int i = 0; i < FM; ++i) {
-                    acc[i][j] = x6_step(acc[i][j], a0[i], a1[i], x0, x1, x2);
+                    acc[i][j] = x6_step<x6_fresh(true)>(acc[i][j], a0[i], a1[i], x0, x1, x2);
                 }
             }
             __builtin_amdgcn_sched_barrier(0);

@@ -39,19 +39,23 @@ __device__ __forceinline__ f32x4 mfma_x32(f32x4 a, f32x4 b, f32x4 c) {
 }
 
 // One k-step of a 16x16 output tile: the six partial products of its 16 k, A = ([h|m] a0,
-// [h|l] a1), B = ([h|m] b0, [m|h] b1, [l|h] b2), smallest terms first, accumulated straight into
-// the running sum (default).  FLSIM_X6_FRESH=1 (measurement build): the three MFMAs sum into a
-// fresh register from zero and the k-step's sum is added to the running accumulator with one fp32
-// add.  That measured 1.7-6x FARTHER from fp64 on the teacher-forced gradients (PerformantNet1
-// rel-L2 1.7e-6 against 2.7e-7, VGG-11 5.3e-5 against 3.1e-5; profiles/r04/fresh_ab) and 10-18 %
-// slower: the MFMA adds its 32 products to the accumulator with one rounding, which beats a
-// separate fp32 add.
-#ifndef FLSIM_X6_FRESH
-#define FLSIM_X6_FRESH 0
-#endif
+// [h|l] a1), B = ([h|m] b0, [m|h] b1, [l|h] b2), smallest terms first.
+//
+// How the bf16 MFMA adds (tools/lab/mfma_numerics.hip, profiles/r05/mfma_numerics.txt): it is
+// NOT an exact sum rounded once.  Its addends (the accumulator and the 32 products) are aligned
+// to the largest of them and bits more than ~3 below that one's last bit are dropped, per addend
+// and toward zero (C = 1 plus 32 products of 2^-27 returns 1; 16 x 2^-26 and 16 x -2^-27 on
+// C = 1 return 1 + 2 ulp, the negative ones vanish).  Accumulating a k-step's six products
+// straight into the running sum (FRESH = false) therefore truncates the small terms against the
+// whole sum, a per-MFMA loss of up to ~2^-25 of |C| that leans toward zero: on PerformantNet1's
+// data gradients 2.9-6.0e-7 rel-L2 against torch fp32's 1.0-1.7e-7 on the same inputs
+// (tools/gemm_diag.py, profiles/r05).  FRESH = true sums the k-step's products from zero (so they
+// are truncated against the k-step's own largest product) and adds that to the running sum with
+// one fp32 add (round to nearest even): 1.5-2.1e-7.
+template <bool FRESH>
 __device__ __forceinline__ f32x4 x6_step(f32x4 acc, f32x4 a0, f32x4 a1, f32x4 b0, f32x4 b1,
                                          f32x4 b2) {
-    if constexpr (FLSIM_X6_FRESH) {
+    if constexpr (FRESH) {
         f32x4 t = mfma_x32(a1, b2, f32x4{0.f, 0.f, 0.f, 0.f});   // ah bl + al bh
         t = mfma_x32(a0, b1, t);                                   // ah bm + am bh
         t = mfma_x32(a0, b0, t);                                   // ah bh + am bm
@@ -62,6 +66,17 @@ __device__ __forceinline__ f32x4 x6_step(f32x4 acc, f32x4 a0, f32x4 a1, f32x4 b0
         return mfma_x32(a0, b0, acc);
     }
 }
+
+// Which accumulations are fresh (measurement levels, FLSIM_X6_FRESH): 0 none; 1 every x6 main
+// accumulator (round 4's experiment); 2 the k-contiguous GEMMs (forward and data gradients:
+// gemm_x6 with a KC A tile, gemm_dx6) and the bias column sums; 3 everything.
+#ifndef FLSIM_X6_FRESH
+#define FLSIM_X6_FRESH 0
+#endif
+constexpr bool x6_fresh(bool kc) {
+    return FLSIM_X6_FRESH == 1 || FLSIM_X6_FRESH == 3 || (FLSIM_X6_FRESH == 2 && kc);
+}
+constexpr bool x6_fresh_bias() { return FLSIM_X6_FRESH >= 2; }
 
 typedef short s16x4v __attribute__((ext_vector_type(4)));
 
@@ -296,12 +311,20 @@ gemm_x6_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, in
             for (int i = 0; i < FM; ++i) {
                 const typename TA::Frag af = TA::frag(A, wm * 16 * FM + 16 * i, lane);
                 if constexpr (WS && AMF) {
-                    bacc[i] = mfma_x32(af.x1, bf16_ones(false, true), bacc[i]);   // l
-                    bacc[i] = mfma_x32(af.x0, bf16_ones(true, true), bacc[i]);    // h + m
+                    if constexpr (x6_fresh_bias()) {
+                        f32x4 t = mfma_x32(af.x1, bf16_ones(false, true),
+                                           f32x4{0.f, 0.f, 0.f, 0.f});                // l
+                        t = mfma_x32(af.x0, bf16_ones(true, true), t);                 // h + m
+                        bacc[i] = bacc[i] + t;
+                    } else {
+                        bacc[i] = mfma_x32(af.x1, bf16_ones(false, true), bacc[i]);   // l
+                        bacc[i] = mfma_x32(af.x0, bf16_ones(true, true), bacc[i]);    // h + m
+                    }
                 }
 #pragma unroll
                 for (int j = 0; j < FN; ++j) {
-                    acc[i][j] = x6_step(acc[i][j], af.x0, af.x1, bf[j].x0, bf[j].x1, bf[j].x2);
+                    acc[i][j] = x6_step<x6_fresh(AL::KC)>(acc[i][j], af.x0, af.x1, bf[j].x0,
+                                                           bf[j].x1, bf[j].x2);
                 }
             }
             __syncthreads();

@@ -533,7 +533,9 @@ static bool concurrent_backward(int S) {
 
 // debug / measurement: FLSIM_DEBUG_BWD_STOP=6 / 5 / 4 ends the backward pass after conv6's /
 // conv5's / conv4's data gradient (dz5 in gx / gxl split; dz4 in a4 / a4l split; dz3 in gx fp32),
-// so each data-gradient GEMM can be checked on its own inputs (tools/gemm_diag.py)
+// so each data-gradient GEMM can be checked on its own inputs (tools/gemm_diag.py); the weight
+// gradients that ran (conv6 .. conv<stop>, the linear layers) reach the epoch's slab sum, the
+// others stay zero
 static int debug_stop() {
     static int v = -1;
     if (v < 0) {
@@ -575,6 +577,13 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
         FLSIM_CHECK_HIP(hipStreamWaitEvent(st, ss->to_main, 0));
         return 0;
     };
+    auto finish = [&]() -> int {                   // the last join; record the slab rows written
+        RC(join());
+        if (er)
+            for (int i = 0; i < 8; ++i)
+                if (zu[i] > er->z[i]) er->z[i] = zu[i];
+        return 0;
+    };
     // ---- linear3 weight/bias (head already produced dlog, dh2) ----
     RC(head_wgrad<256>(w.dlog, w.e2, g.l3w, g.l3b, S, ZH, st));
     // ---- linear2: wgrad, bias, dgrad (-> dh1 through dropout/relu of linear1) ----
@@ -610,7 +619,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
         dz6.l, w.a5l)));
     RC((xs<14, 14, 192, 0, 4, 6, 4, 2, false, 13>(dz6, S, g.wdx[5], 192, 1728,
         EpiMaskXs<192, true>{dz5.hm, dz5.l, w.a5, S * 13 * 13}, st, K_DG6, 1728)));
-    if (debug_stop() == 6) return join();         // (debug: dz5 stays in gx / gxl)
+    if (debug_stop() == 6) return finish();       // (debug: dz5 stays in gx / gxl)
     // ---- conv5: wgrad (input d2), bias, dgrad -> grad wrt d2 (dropout site 2), scattered through
     //      pool2 straight into dz4 (a4 buffer, split; no gy round trip) ----
     RC(fork());
@@ -620,7 +629,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC((xs<13, 13, 192, 0, 4, 3, 4, 2, false, 0>(dz5, S, g.wdx[4], 96, 1728,
         EpiDropScatterXs<11, 11, 96>{dz4.hm, dz4.l, w.d2, w.i2, s25, S * 11 * 11}, st, K_DG5,
         1728)));
-    if (debug_stop() == 5) return join();         // (debug: dz4 in a4 / a4l, dz5 in gx / gxl)
+    if (debug_stop() == 5) return finish();       // (debug: dz4 in a4 / a4l, dz5 in gx / gxl)
     // ---- conv4: wgrad (input a3), bias, dgrad -> dz3 = . * (a3 > 0) into gx (fp32) ----
     // dz3 and dz2 stay fp32: their data gradients have N = 48 columns, where the fp32 MFMA
     // kernels are faster than any split-bf16 form (profiles/r04/lab/lab_xs_r04b.txt: conv3's
@@ -633,7 +642,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
         dz4.l, w.a3l)));
     RC((xs<22, 22, 96, 0, 4, 3, 4, 2, false, 0>(dz4, S, g.wdx[3], 96, 864,
         EpiMaskXs<96, false, true, 400>{w.gx, nullptr, w.a3, S * 20 * 20}, st, K_DG4, 864)));
-    if (debug_stop() == 4) return join();         // (debug: dz3 in gx fp32, dz4 in a4 / a4l)
+    if (debug_stop() == 4) return finish();       // (debug: dz3 in gx fp32, dz4 in a4 / a4l)
     float* dz3 = w.gx;
     // ---- conv3: wgrad (input d1), bias, dgrad -> grad wrt d1 (site 1), scattered through pool1
     //      straight into dz2 (a2 buffer, fp32) ----
@@ -667,11 +676,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
         RC((conv_wgrad<32, 32, 4, 2, 1, 3, 3, 1>(dz1, w.x0, S, 48, 48, g.sw[0], g.sb[0], GEO[0].ZW,
                                                 st, K_WG1, 27, zi(0), &zu[0])));
     }
-    RC(join());                                   // the next chunk's forward rewrites a1, a2
-    if (er)
-        for (int i = 0; i < 8; ++i)
-            if (zu[i] > er->z[i]) er->z[i] = zu[i];
-    return 0;
+    return finish();                              // (the next chunk's forward rewrites a1, a2)
 }
 
 }  // namespace flsim

@@ -42,7 +42,10 @@ def main():
     eng.begin_epoch(theta)
     loss = torch.zeros(nw, device=dev)
     eng.run_chunk(theta, DevicePool(dev, 0, pool), worker_table(items, dev), nw, 4, 0, True, loss)
+    S = torch.zeros(eng.P, device=dev)
+    eng.end_epoch(S)          # the weight gradients that ran before the stop (conv6 .. conv<stop>)
     torch.cuda.synchronize()
+    S = S.cpu().double()
     NS = eng.max_samples
     n = 128 * nw
 
@@ -80,18 +83,51 @@ def main():
         a3 = nchw(W(4, (NS, 20, 20, 96)))
         return cgi((n, 96, 20, 20), w(6), dz4, padding=2) * (a3 > 0).to(dt)
 
+    def wgrad(dt):
+        """the layer's weight and bias gradient (the slab GEMM + column sum) in dtype dt on the
+        GPU's own inputs: conv<stop>'s input activation and its dZ"""
+        cgw = torch.nn.grad.conv2d_weight
+        if stop == 6:
+            x_in = nchw(W(7, (NS, 13, 13, 192))).to(dt)
+            dz = torch.zeros(n, 192, 15, 15, dtype=dt)
+            dz[:, :, :14, :14] = nchw(W(8, (NS, 14, 14, 192))).to(dt)
+            shp = (192, 192, 3, 3)
+        elif stop == 5:
+            x_in = nchw(W(6, (NS, 11, 11, 96))).to(dt)
+            dz = nchw(W(14, (NS, 13, 13, 192))).to(dt)
+            shp = (192, 96, 3, 3)
+        else:
+            x_in = nchw(W(4, (NS, 20, 20, 96))).to(dt)
+            dz = nchw(W(5, (NS, 22, 22, 96))).to(dt)
+            shp = (96, 96, 3, 3)
+        return cgw(x_in, shp, dz, padding=2), dz.sum((0, 2, 3))
+
+    def stats(t, r64):
+        rn = float(r64.norm())
+        rr = float((r64 * r64).sum())
+        d = t - r64
+        return dict(rel=float(d.norm()) / rn, alpha=float((d * r64).sum()) / rr,
+                    resid=float((d - (float((d * r64).sum()) / rr) * r64).norm()) / rn)
+
     gpu = {6: lambda: nchw(W(14, (NS, 13, 13, 192))), 5: lambda: nchw(W(5, (NS, 22, 22, 96))),
            4: lambda: nchw(W(14, (NS, 20, 20, 96)))}[stop]().double()
     r64 = gemm(torch.float64)
     r32 = gemm(torch.float32).double()
-    rn = float(r64.norm())
-    rr = float((r64 * r64).sum())
     out = dict(stop=stop, gemm={6: "conv6 dgrad (x6)", 5: "conv5 dgrad (x6) + pool2 scatter",
                                 4: "conv4 dgrad (x6)"}[stop], items=items)
     for name, t in (("gpu", gpu), ("cpu32", r32)):
-        d = t - r64
-        out[name] = dict(rel=float(d.norm()) / rn, alpha=float((d * r64).sum()) / rr,
-                         resid=float((d - (float((d * r64).sum()) / rr) * r64).norm()) / rn)
+        out[name] = stats(t, r64)
+        # what the previous layer's bias gradient sees: the per-channel sums of the output
+        out[name]["chan_sum"] = stats(t.sum((0, 2, 3)), r64.sum((0, 2, 3)))["rel"]
+    # the weight-gradient GEMM of the same layer (it ran before the data gradient)
+    j = {6: 10, 5: 8, 4: 6}[stop]
+    off = int(sum(a.size for a in P[:j]))
+    gw = S[off:off + P[j].size].view(P[j].shape)
+    gb = S[off + P[j].size:off + P[j].size + P[j + 1].size]
+    w64, b64 = wgrad(torch.float64)
+    w32, b32 = wgrad(torch.float32)
+    out["wgrad"] = dict(gpu_w=stats(gw, w64), cpu32_w=stats(w32.double(), w64),
+                        gpu_b=stats(gb, b64), cpu32_b=stats(b32.double(), b64))
     print("GEMM_DIAG", json.dumps(out))
 
 

@@ -63,7 +63,7 @@ def main():
     out = {"pkg": pkg, "items": items, "dropout": args.dropout, "tensors": {}, "activations": {}}
     off = 0
     print(f"{'tensor':16s} {'|g|':>10s} {'e_gpu/|g|':>10s} {'e_cpu/|g|':>10s} {'ratio':>6s} "
-          f"{'coh_gpu':>8s} {'coh_cpu':>8s}")
+          f"{'coh_gpu':>8s} {'coh_cpu':>8s} {'coh_g':>8s} {'a_gpu':>10s} {'a_cpu':>10s}")
     for name, shp in PN1_SHAPES:
         k = int(np.prod(shp))
         sl = slice(off, off + k)
@@ -71,12 +71,16 @@ def main():
         r = g64[sl]
         dg, dc = g_gpu[sl] - r, g32[sl] - r
         nr, eg, ec = (float(np.linalg.norm(v)) for v in (r, dg, dc))
+        rr = float(r @ r)
         rec = dict(norm=nr, e_gpu=eg / nr, e_cpu=ec / nr, ratio=eg / (2 * ec + 1e-7 * nr),
                    coh_gpu=abs(float(dg.sum())) / max(eg, 1e-300),
-                   coh_cpu=abs(float(dc.sum())) / max(ec, 1e-300), n=k)
+                   coh_cpu=abs(float(dc.sum())) / max(ec, 1e-300), n=k,
+                   coh_g=abs(float(r.sum())) / max(nr, 1e-300),
+                   alpha_gpu=float(dg @ r) / rr, alpha_cpu=float(dc @ r) / rr)
         out["tensors"][name] = rec
         print(f"{name:16s} {nr:10.3e} {rec['e_gpu']:10.3e} {rec['e_cpu']:10.3e} {rec['ratio']:6.2f} "
-              f"{rec['coh_gpu']:8.2f} {rec['coh_cpu']:8.2f}")
+              f"{rec['coh_gpu']:8.2f} {rec['coh_cpu']:8.2f} {rec['coh_g']:8.2f} "
+              f"{rec['alpha_gpu']:+10.2e} {rec['alpha_cpu']:+10.2e}")
 
     # forward activations: the GPU's stored tensors against the forced fp64 / fp32 forwards
     def acts(dt):
@@ -122,8 +126,13 @@ def main():
         eg = float((gpu[k].double() - r).norm())
         ec = float((A32[k].double() - r).norm())
         nr = float(r.norm())
-        out["activations"][k] = dict(e_gpu=eg / nr, e_cpu=ec / nr, ratio=eg / max(ec, 1e-300))
-        print(f"{k:16s} {nr:10.3e} {eg / nr:10.3e} {ec / nr:10.3e} {eg / max(ec, 1e-300):6.2f}")
+        rr = float((r * r).sum())
+        ag = float(((gpu[k].double() - r) * r).sum()) / rr
+        ac = float(((A32[k].double() - r) * r).sum()) / rr
+        out["activations"][k] = dict(e_gpu=eg / nr, e_cpu=ec / nr, ratio=eg / max(ec, 1e-300),
+                                     alpha_gpu=ag, alpha_cpu=ac)
+        print(f"{k:16s} {nr:10.3e} {eg / nr:10.3e} {ec / nr:10.3e} {eg / max(ec, 1e-300):6.2f} "
+              f"{ag:+10.2e} {ac:+10.2e}")
     print("SURVEY_DIAG", json.dumps(out))
 
 
