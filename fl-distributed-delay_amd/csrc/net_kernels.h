@@ -522,9 +522,11 @@ static int pack_conv_xs(const float* W, XsT wf, XsT wd, int CO, int CI, int KP, 
     hipLaunchKernelGGL(k_pack_fwd_xs, dim3(ceil_div((long)CO * KP / 4, 256)), dim3(256), 0, st, W,
                        wf.hm, wf.l, CO, CI, KP);
     FLSIM_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_pack_dgrad_xs, dim3(ceil_div((long)CI * 9 * CO / 4, 256)), dim3(256), 0,
-                       st, W, wd.hm, wd.l, CO, CI);
-    FLSIM_LAUNCH_CHECK();
+    if (wd.hm) {           // (no split data-gradient packing when that GEMM runs on fp32)
+        hipLaunchKernelGGL(k_pack_dgrad_xs, dim3(ceil_div((long)CI * 9 * CO / 4, 256)), dim3(256),
+                           0, st, W, wd.hm, wd.l, CO, CI);
+        FLSIM_LAUNCH_CHECK();
+    }
     return 0;
 }
 
@@ -984,6 +986,35 @@ static int conv_dx6(XsT X, int S, XsT W, int N, int KP, const EPI& epi, hipStrea
                           epi, KP / GK, tm, tn);
     FLSIM_LAUNCH_CHECK();
     return probe_end(ps, kid, 2.0 * ad.M * N * kreal);
+}
+
+// conv (a data gradient as a valid convolution) on the fp32 MFMA (gemm_kernel) over a split input
+// read back exactly as fp32 (loaders.h XsF32Src) and fp32 packed weights W [N][KP]; FMS: the
+// fragment rows per wave for chunks of at most small_chunk_samples() samples (the same k order
+// per output, so bit-identical across chunk sizes)
+template <int IH, int IW, int CI, int PAD, int FM, int FMS, int FN, int WM, int WN, int OHX,
+          class EPI>
+static int conv_f32s(XsT X, int S, const float* Wpk, int N, int KP, const EPI& epi,
+                     hipStream_t st, int kid, int kreal) {
+    auto run = [&](auto fm) -> int {
+        constexpr int F = decltype(fm)::value;
+        constexpr int NT = 64 * WM * WN;
+        constexpr int BM = 16 * F * WM, BN = 16 * FN * WN;
+        using AL = Im2colKC<IH, IW, CI, PAD, BM, NT, false, OHX, XsF32Src>;
+        using BL = RowsKC<BN, NT>;
+        AL al;
+        al.X = X.hm;
+        al.XL = X.l;
+        al.M = S * AL::OH * AL::OW;
+        BL bl;
+        bl.P = Wpk;
+        bl.ld = KP;
+        bl.NR = N;
+        return launch_gemm<F, FN, WM, WN>(al, bl, epi, al.M, N, KP / GK, 1, st, kid,
+                                          2.0 * al.M * N * kreal);
+    };
+    if (S <= small_chunk_samples()) return run(std::integral_constant<int, FMS>{});
+    return run(std::integral_constant<int, FM>{});
 }
 
 // the same GEMM on gemm_x6_kernel with both operands staged through LDS (bit-identical to

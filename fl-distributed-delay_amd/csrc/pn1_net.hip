@@ -67,9 +67,9 @@ constexpr int ZH = 32;      // head wgrad split
 // gradient-state layout (floats): packed weights + slabs
 struct GradState {
     float* wf[6];  // conv1's fp32 packing (wf[1..5] unused)
-    float* wd[6];  // fp32 data-gradient packings of conv2 / conv3 (wd[1], wd[2]; the rest unused)
+    float* wd[6];  // fp32 data-gradient packings of conv2-6 (wd[0] unused)
     XsT wfx[6];    // conv2-6 forward packings, split (wfx[0] unused)
-    XsT wdx[6];    // conv2-6 data-gradient packings, split (wdx[0] unused)
+    XsT wdx[6];    // split data-gradient packings (unused: every data gradient runs on fp32)
     float* sw[6];  // conv weight slabs [ZW][CO][KP]
     float* sb[6];  // conv bias slabs [ZW][CO] (fused into the weight-gradient GEMM)
     float* l1w;    // [ZL1W][512][9408]
@@ -116,14 +116,12 @@ static GradState gs_layout(float* base_in) {
     };
     for (int l = 0; l < 6; ++l) {
         g.wf[l] = l ? nullptr : take((long)GEO[l].CO * GEO[l].KP);
-        g.wd[l] = (l == 1 || l == 2) ? take((long)GEO[l].CI * 9 * GEO[l].CO) : nullptr;
+        g.wd[l] = l ? take((long)GEO[l].CI * 9 * GEO[l].CO) : nullptr;
         g.wfx[l] = g.wdx[l] = XsT{nullptr, nullptr};
         if (l) {
-            const long nf = (long)GEO[l].CO * GEO[l].KP, nd = (long)GEO[l].CI * 9 * GEO[l].CO;
+            const long nf = (long)GEO[l].CO * GEO[l].KP;
             g.wfx[l].hm = take(nf);
             g.wfx[l].l = take(nf / 2);
-            g.wdx[l].hm = take(nd);
-            g.wdx[l].l = take(nd / 2);
         }
     }
     const long slab0 = o;
@@ -193,11 +191,10 @@ static int pack_weights(const GradState& g, const float* theta, hipStream_t st) 
     for (int l = 1; l < 6; ++l) {
         const ConvGeo& c = GEO[l];
         RC(pack_conv_xs(theta + P_OFF[2 * l], g.wfx[l], g.wdx[l], c.CO, c.CI, c.KP, st));
-        if (g.wd[l]) {          // conv2 / conv3: the data gradient runs on the fp32 MFMA
-            hipLaunchKernelGGL(k_pack_dgrad, dim3(ceil_div((long)c.CI * 9 * c.CO, 256)), dim3(256),
-                               0, st, theta + P_OFF[2 * l], g.wd[l], c.CO, c.CI);
-            FLSIM_LAUNCH_CHECK();
-        }
+        // every data gradient runs on the fp32 MFMA
+        hipLaunchKernelGGL(k_pack_dgrad, dim3(ceil_div((long)c.CI * 9 * c.CO, 256)), dim3(256), 0,
+                           st, theta + P_OFF[2 * l], g.wd[l], c.CO, c.CI);
+        FLSIM_LAUNCH_CHECK();
     }
     return 0;
 }
@@ -617,7 +614,10 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC((conv_wgrad_sz<13, 13, 192, 2, 6, 3, 2, 2, 3, 3, 2, 2, 14, true, true, XsSrc>(
         dz6.hm, w.a5, S, 192, 1728, g.sw[5], g.sb[5], GEO[5].ZW, sw, K_WG6, 1728, zi(5), &zu[5],
         dz6.l, w.a5l)));
-    RC((xs<14, 14, 192, 0, 4, 6, 4, 2, false, 13>(dz6, S, g.wdx[5], 192, 1728,
+    // (the data gradients of conv4-6 run on the fp32 MFMA over their split dZ: the bf16 MFMA
+    // truncates small addends toward zero, which biases the per-channel sums of its outputs 30-100x
+    // beyond the CPU fp32 port's and failed SURVEY 8(c) on conv1-4 (tools/gemm_diag.py))
+    RC((conv_f32s<14, 14, 192, 0, 4, 2, 3, 4, 2, 13>(dz6, S, g.wd[5], 192, 1728,
         EpiMaskXs<192, true>{dz5.hm, dz5.l, w.a5, S * 13 * 13}, st, K_DG6, 1728)));
     if (debug_stop() == 6) return finish();       // (debug: dz5 stays in gx / gxl)
     // ---- conv5: wgrad (input d2), bias, dgrad -> grad wrt d2 (dropout site 2), scattered through
@@ -626,7 +626,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC((conv_wgrad_sz<11, 11, 96, 2, 6, 3, 2, 2, 3, 3, 2, 2, 0, false, true, XsSrc>(
         dz5.hm, w.d2, S, 192, 864, g.sw[4], g.sb[4], GEO[4].ZW, sw, K_WG5, 864, zi(4), &zu[4],
         dz5.l, w.d2l)));
-    RC((xs<13, 13, 192, 0, 4, 3, 4, 2, false, 0>(dz5, S, g.wdx[4], 96, 1728,
+    RC((conv_f32s<13, 13, 192, 0, 4, 2, 3, 2, 2, 0>(dz5, S, g.wd[4], 96, 1728,
         EpiDropScatterXs<11, 11, 96>{dz4.hm, dz4.l, w.d2, w.i2, s25, S * 11 * 11}, st, K_DG5,
         1728)));
     if (debug_stop() == 5) return finish();       // (debug: dz4 in a4 / a4l, dz5 in gx / gxl)
@@ -640,7 +640,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC((conv_wgrad<20, 20, 96, 2, 3, 3, 2, 2, 0, false, true, XsSrc, XsSrcSM>(
         dz4.hm, w.a3, S, 96, 864, g.sw[3], g.sb[3], GEO[3].ZW, sw, K_WG4, 864, zi(3), &zu[3],
         dz4.l, w.a3l)));
-    RC((xs<22, 22, 96, 0, 4, 3, 4, 2, false, 0>(dz4, S, g.wdx[3], 96, 864,
+    RC((conv_f32s<22, 22, 96, 0, 4, 2, 3, 2, 2, 0>(dz4, S, g.wd[3], 96, 864,
         EpiMaskXs<96, false, true, 400>{w.gx, nullptr, w.a3, S * 20 * 20}, st, K_DG4, 864)));
     if (debug_stop() == 4) return finish();       // (debug: dz3 in gx fp32, dz4 in a4 / a4l)
     float* dz3 = w.gx;
