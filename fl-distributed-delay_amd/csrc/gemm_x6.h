@@ -193,6 +193,14 @@ struct AsumMfma : std::false_type {};
 template <class E>
 struct AsumMfma<E, std::void_t<decltype(E::ASUM_MFMA)>> : std::bool_constant<E::ASUM_MFMA> {};
 
+// Epilogues with X6_FRESH = true make their GEMM's main accumulation fresh whatever the build's
+// FLSIM_X6_FRESH level (x6_step): PerformantNet1's linear1 forward, whose error e1 carries into
+// linear2's weight gradient.
+template <class E, class = void>
+struct X6Fresh : std::false_type {};
+template <class E>
+struct X6Fresh<E, std::void_t<decltype(E::X6_FRESH)>> : std::bool_constant<E::X6_FRESH> {};
+
 __device__ __forceinline__ f32x4 bf16_ones(bool lo, bool hi) {
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     const uint32_t a = lo ? 0x3f803f80u : 0u, b = hi ? 0x3f803f80u : 0u;
@@ -323,7 +331,7 @@ gemm_x6_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, in
                 }
 #pragma unroll
                 for (int j = 0; j < FN; ++j) {
-                    acc[i][j] = x6_step<x6_fresh(AL::KC)>(acc[i][j], af.x0, af.x1, bf[j].x0,
+                    acc[i][j] = x6_step<x6_fresh(AL::KC) || X6Fresh<EPI>::value>(acc[i][j], af.x0, af.x1, bf[j].x0,
                                                            bf[j].x1, bf[j].x2);
                 }
             }

@@ -842,4 +842,9 @@ struct EpiSlabStore {
     }
 };
 
+// EpiSlabStore whose x6 GEMM accumulates each k-step fresh (gemm_x6.h X6Fresh)
+struct EpiSlabStoreFresh : EpiSlabStore {
+    static constexpr bool X6_FRESH = true;
+};
+
 }  // namespace flsim

@@ -784,6 +784,31 @@ static int small_chunk_samples() {
     return s;
 }
 
+// conv_direct_sz over a split input read back exactly as fp32 (loaders.h XsF32Src): the data
+// gradients of conv4-6 on the fp32 MFMA
+template <int IH, int IW, int CI, int PAD, int FM, int FMS, int FN, int WAVES, int KB, int DEPTH,
+          int OHX, class EPI>
+static int conv_direct_s(XsT X, int S, const float* Wpk, int N, int KP, const EPI& epi,
+                         hipStream_t st, int kid, int kreal) {
+    auto run = [&](auto fm) -> int {
+        constexpr int F = decltype(fm)::value;
+        using AD = Im2colDirect<IH, IW, CI, PAD, F, false, OHX, XsF32Src>;
+        using BL = RowsKCStage<16 * FN, 64 * WAVES>;
+        AD ad;
+        ad.X = X.hm;
+        ad.XL = X.l;
+        ad.M = S * AD::ROWS_PER_IMG;
+        BL bl;
+        bl.P = Wpk;
+        bl.ld = KP;
+        bl.NR = N;
+        return launch_direct<F, FN, WAVES, KB, DEPTH>(ad, bl, epi, ad.M, N, KP / GK, st, kid,
+                                                      2.0 * ad.M * N * kreal);
+    };
+    if (S <= small_chunk_samples()) return run(std::integral_constant<int, FMS>{});
+    return run(std::integral_constant<int, FM>{});
+}
+
 template <int IH, int IW, int CI, int PAD, int FM, int FMS, int FN, int WAVES, int KB, int DEPTH,
           bool WIN, int OHX, class EPI>
 static int conv_direct_sz(const float* X, int S, const float* Wpk, int N, int KP, const EPI& epi,
@@ -1066,7 +1091,7 @@ static int conv_pool_fwd(const float* X, int S, const float* Wpk, int KP, float*
 }
 
 // linear layer part[z] = x W^T over the z-th K range (x [M][K] rows, W [N][K] torch layout)
-template <int FM, int FN, int WM, int WN, bool X6 = false>
+template <int FM, int FN, int WM, int WN, bool X6 = false, class EPI = EpiSlabStore>
 static int linear_fwd(const float* x, const float* W, float* part, int M, int N, int K, int Z,
                       hipStream_t st, int kid) {
     constexpr int NT = 64 * WM * WN;
@@ -1074,7 +1099,8 @@ static int linear_fwd(const float* x, const float* W, float* part, int M, int N,
     al.P = x; al.ld = K; al.NR = M;
     RowsKC<16 * FN * WN, NT> bl{};
     bl.P = W; bl.ld = K; bl.NR = N;
-    EpiSlabStore epi{part, M, N, (long)M * N};
+    EPI epi{};
+    static_cast<EpiSlabStore&>(epi) = EpiSlabStore{part, M, N, (long)M * N};
     return launch_gemm<FM, FN, WM, WN, X6>(al, bl, epi, M, N, K / GK, Z, st, kid, 2.0 * M * N * K);
 }
 

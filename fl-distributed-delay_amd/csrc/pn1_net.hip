@@ -379,16 +379,18 @@ static int forward(const GradState& g, const WS& w, const float* theta, int S,
     // small chunks (configs[1]: 640 samples = 5 x 4 tiles of 128 x 128, 80 blocks with the split)
     // take 64 x 64 tiles: the same split, hence the same sums, with 4x the blocks
     // (every tile on the split-bf16 kernel: a chunk's losses must not depend on its size, and
-    // the two kernels round differently)
+    // the two kernels round differently); fresh accumulation (gemm_x6.h x6_step): e1's error
+    // reaches linear2's weight gradient, which the truncating MFMA sum left at the SURVEY 8(c)
+    // bound
     if (S <= 2048)          // 32 x 64 tiles: 640 blocks at configs[1]'s 640 samples
-        RC((linear_fwd<1, 2, 2, 2, true>(w.d3, theta + P_OFF[12], w.part, S, 512, 9408, ZL1F, st,
-                                         K_L1F)));
+        RC((linear_fwd<1, 2, 2, 2, true, EpiSlabStoreFresh>(w.d3, theta + P_OFF[12], w.part, S,
+                                                            512, 9408, ZL1F, st, K_L1F)));
     else if (S <= 4096)
-        RC((linear_fwd<2, 2, 2, 2, true>(w.d3, theta + P_OFF[12], w.part, S, 512, 9408, ZL1F, st,
-                                         K_L1F)));
+        RC((linear_fwd<2, 2, 2, 2, true, EpiSlabStoreFresh>(w.d3, theta + P_OFF[12], w.part, S,
+                                                            512, 9408, ZL1F, st, K_L1F)));
     else
-        RC((linear_fwd<4, 4, 2, 2, true>(w.d3, theta + P_OFF[12], w.part, S, 512, 9408, ZL1F, st,
-                                         K_L1F)));
+        RC((linear_fwd<4, 4, 2, 2, true, EpiSlabStoreFresh>(w.d3, theta + P_OFF[12], w.part, S,
+                                                            512, 9408, ZL1F, st, K_L1F)));
     RC(linear_finish(w.part, ZL1F, theta + P_OFF[13], w.e1, S, 512, workers, seed, SITE_DROP4,
                      THR_P50, SCALE_P50, dropout, st));
     // linear2 + relu + dropout2 (models.py:44-45)
@@ -617,7 +619,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     // (the data gradients of conv4-6 run on the fp32 MFMA over their split dZ: the bf16 MFMA
     // truncates small addends toward zero, which biases the per-channel sums of its outputs 30-100x
     // beyond the CPU fp32 port's and failed SURVEY 8(c) on conv1-4 (tools/gemm_diag.py))
-    RC((conv_f32s<14, 14, 192, 0, 4, 2, 3, 4, 2, 13>(dz6, S, g.wd[5], 192, 1728,
+    RC((conv_direct_s<14, 14, 192, 0, 2, 1, 6, 8, 6, 2, 13>(dz6, S, g.wd[5], 192, 1728,
         EpiMaskXs<192, true>{dz5.hm, dz5.l, w.a5, S * 13 * 13}, st, K_DG6, 1728)));
     if (debug_stop() == 6) return finish();       // (debug: dz5 stays in gx / gxl)
     // ---- conv5: wgrad (input d2), bias, dgrad -> grad wrt d2 (dropout site 2), scattered through
@@ -626,7 +628,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC((conv_wgrad_sz<11, 11, 96, 2, 6, 3, 2, 2, 3, 3, 2, 2, 0, false, true, XsSrc>(
         dz5.hm, w.d2, S, 192, 864, g.sw[4], g.sb[4], GEO[4].ZW, sw, K_WG5, 864, zi(4), &zu[4],
         dz5.l, w.d2l)));
-    RC((conv_f32s<13, 13, 192, 0, 4, 2, 3, 2, 2, 0>(dz5, S, g.wd[4], 96, 1728,
+    RC((conv_direct_s<13, 13, 192, 0, 2, 1, 6, 8, 3, 2, 0>(dz5, S, g.wd[4], 96, 1728,
         EpiDropScatterXs<11, 11, 96>{dz4.hm, dz4.l, w.d2, w.i2, s25, S * 11 * 11}, st, K_DG5,
         1728)));
     if (debug_stop() == 5) return finish();       // (debug: dz4 in a4 / a4l, dz5 in gx / gxl)
@@ -640,7 +642,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC((conv_wgrad<20, 20, 96, 2, 3, 3, 2, 2, 0, false, true, XsSrc, XsSrcSM>(
         dz4.hm, w.a3, S, 96, 864, g.sw[3], g.sb[3], GEO[3].ZW, sw, K_WG4, 864, zi(3), &zu[3],
         dz4.l, w.a3l)));
-    RC((conv_f32s<22, 22, 96, 0, 4, 2, 3, 2, 2, 0>(dz4, S, g.wd[3], 96, 864,
+    RC((conv_direct_s<22, 22, 96, 0, 2, 1, 6, 8, 3, 2, 0>(dz4, S, g.wd[3], 96, 864,
         EpiMaskXs<96, false, true, 400>{w.gx, nullptr, w.a3, S * 20 * 20}, st, K_DG4, 864)));
     if (debug_stop() == 4) return finish();       // (debug: dz3 in gx fp32, dz4 in a4 / a4l)
     float* dz3 = w.gx;
