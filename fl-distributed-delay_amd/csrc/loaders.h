@@ -77,19 +77,6 @@ struct XsSrc {
     }
 };
 
-// A split tensor read by an fp32 GEMM (gemm_kernel): each unit's HM and L parts are loaded as by
-// XsSrc and put back together, (h + m) + l, which is the fp32 value exactly (split.h).  The data
-// gradients of conv4-6 run on the fp32 MFMA over their split dZ this way (the bf16
-// MFMA's truncating accumulation biases their per-channel sums; the fp32 MFMA is an fmaf chain).
-struct XsF32Src : XsSrc {
-    using Unit = f32x4;
-    static constexpr bool SPLIT = false;
-    __device__ __forceinline__ f32x4 ld(unsigned byte_off) const { return xs_value(XsSrc::ld(byte_off)); }
-    __device__ __forceinline__ f32x4 ld_or0(unsigned byte_off, bool ok) const {
-        return ld(ok ? byte_off : BUF_OOB);
-    }
-};
-
 // A split tensor of C channels stored channel-slice-major, [img][C/16][H][W][16]: the 16 channels of
 // one slice of neighbouring pixels are contiguous, so the 16 rows of a direct-A fragment (16
 // neighbouring output pixels, one tap, one slice) read whole cache lines.  Only the loaders that

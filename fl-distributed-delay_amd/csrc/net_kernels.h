@@ -199,16 +199,6 @@ k_pool_scatter_nchw(const float* __restrict__ gy, const uint8_t* __restrict__ id
     }
 }
 
-// pool3's backward into a split dZ (PerformantNet1's dz6, read by conv6's split-bf16 GEMMs)
-template <int H, int W, int C>
-static int pool_scatter_nchw_xs(const float* gy, const uint8_t* idx, float* dzhm, float* dzl, int S,
-                                hipStream_t st) {
-    hipLaunchKernelGGL((k_pool_scatter_nchw<H, W, C, true>), dim3(S), dim3(256), 0, st, gy, idx,
-                       dzhm, dzl);
-    FLSIM_LAUNCH_CHECK();
-    return 0;
-}
-
 template <int H, int W, int C, bool NCHW_G>
 static int pool_scatter(const float* gy, const uint8_t* idx, float* dz, int S, hipStream_t st) {
     if constexpr (NCHW_G) {
@@ -784,31 +774,6 @@ static int small_chunk_samples() {
     return s;
 }
 
-// conv_direct_sz over a split input read back exactly as fp32 (loaders.h XsF32Src): the data
-// gradients of conv4-6 on the fp32 MFMA
-template <int IH, int IW, int CI, int PAD, int FM, int FMS, int FN, int WAVES, int KB, int DEPTH,
-          int OHX, class EPI>
-static int conv_direct_s(XsT X, int S, const float* Wpk, int N, int KP, const EPI& epi,
-                         hipStream_t st, int kid, int kreal) {
-    auto run = [&](auto fm) -> int {
-        constexpr int F = decltype(fm)::value;
-        using AD = Im2colDirect<IH, IW, CI, PAD, F, false, OHX, XsF32Src>;
-        using BL = RowsKCStage<16 * FN, 64 * WAVES>;
-        AD ad;
-        ad.X = X.hm;
-        ad.XL = X.l;
-        ad.M = S * AD::ROWS_PER_IMG;
-        BL bl;
-        bl.P = Wpk;
-        bl.ld = KP;
-        bl.NR = N;
-        return launch_direct<F, FN, WAVES, KB, DEPTH>(ad, bl, epi, ad.M, N, KP / GK, st, kid,
-                                                      2.0 * ad.M * N * kreal);
-    };
-    if (S <= small_chunk_samples()) return run(std::integral_constant<int, FMS>{});
-    return run(std::integral_constant<int, FM>{});
-}
-
 template <int IH, int IW, int CI, int PAD, int FM, int FMS, int FN, int WAVES, int KB, int DEPTH,
           bool WIN, int OHX, class EPI>
 static int conv_direct_sz(const float* X, int S, const float* Wpk, int N, int KP, const EPI& epi,
@@ -1011,35 +976,6 @@ static int conv_dx6(XsT X, int S, XsT W, int N, int KP, const EPI& epi, hipStrea
                           epi, KP / GK, tm, tn);
     FLSIM_LAUNCH_CHECK();
     return probe_end(ps, kid, 2.0 * ad.M * N * kreal);
-}
-
-// conv (a data gradient as a valid convolution) on the fp32 MFMA (gemm_kernel) over a split input
-// read back exactly as fp32 (loaders.h XsF32Src) and fp32 packed weights W [N][KP]; FMS: the
-// fragment rows per wave for chunks of at most small_chunk_samples() samples (the same k order
-// per output, so bit-identical across chunk sizes)
-template <int IH, int IW, int CI, int PAD, int FM, int FMS, int FN, int WM, int WN, int OHX,
-          class EPI>
-static int conv_f32s(XsT X, int S, const float* Wpk, int N, int KP, const EPI& epi,
-                     hipStream_t st, int kid, int kreal) {
-    auto run = [&](auto fm) -> int {
-        constexpr int F = decltype(fm)::value;
-        constexpr int NT = 64 * WM * WN;
-        constexpr int BM = 16 * F * WM, BN = 16 * FN * WN;
-        using AL = Im2colKC<IH, IW, CI, PAD, BM, NT, false, OHX, XsF32Src>;
-        using BL = RowsKC<BN, NT>;
-        AL al;
-        al.X = X.hm;
-        al.XL = X.l;
-        al.M = S * AL::OH * AL::OW;
-        BL bl;
-        bl.P = Wpk;
-        bl.ld = KP;
-        bl.NR = N;
-        return launch_gemm<F, FN, WM, WN>(al, bl, epi, al.M, N, KP / GK, 1, st, kid,
-                                          2.0 * al.M * N * kreal);
-    };
-    if (S <= small_chunk_samples()) return run(std::integral_constant<int, FMS>{});
-    return run(std::integral_constant<int, FM>{});
 }
 
 // the same GEMM on gemm_x6_kernel with both operands staged through LDS (bit-identical to

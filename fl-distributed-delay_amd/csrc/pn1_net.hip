@@ -155,7 +155,7 @@ struct WS {
     float* gx; float* gy; float* loss_s; float* dlog; int32_t* y;
     uint8_t* i1; uint8_t* i2; uint8_t* i3;
     float* a1l; float* d1l; float* a3l; float* d2l; float* a5l;     // forward split tensors
-    float* a6l; float* a4l; float* a2l; float* gxl;                  // dz6, dz4, -, dz5
+    float* a6l; float* a4l; float* a2l; float* gxl;                  // (unused: dZ is fp32)
     long bytes;
     XsT x(float* hm, float* l) const { return XsT{hm, l}; }
 };
@@ -178,9 +178,8 @@ static WS ws_layout(char* base, int S) {
     w.i1 = (uint8_t*)take(15552L * S); w.i2 = (uint8_t*)take(11616L * S);
     w.i3 = (uint8_t*)take(9408L * S);
     w.a1l = tf(55488 / 2); w.d1l = tf(15552 / 2); w.a3l = tf(38400 / 2); w.d2l = tf(11616 / 2);
-    w.a5l = tf(32448 / 2); w.a6l = tf(43200 / 2); w.a4l = tf(46464 / 2);
-    w.a2l = tf(0);         // (dz2 is fp32: id kept, no bytes)
-    w.gxl = tf(32448 / 2);
+    w.a5l = tf(32448 / 2);
+    w.a6l = tf(0); w.a4l = tf(0); w.a2l = tf(0); w.gxl = tf(0);   // (dZ is fp32: ids kept, no bytes)
     w.bytes = o;
     return w;
 }
@@ -531,7 +530,7 @@ static bool concurrent_backward(int S) {
 }
 
 // debug / measurement: FLSIM_DEBUG_BWD_STOP=6 / 5 / 4 ends the backward pass after conv6's /
-// conv5's / conv4's data gradient (dz5 in gx / gxl split; dz4 in a4 / a4l split; dz3 in gx fp32),
+// conv5's / conv4's data gradient (dz5 in gx, dz4 in a4, dz3 in gx; all fp32),
 // so each data-gradient GEMM can be checked on its own inputs (tools/gemm_diag.py); the weight
 // gradients that ran (conv6 .. conv<stop>, the linear layers) reach the epoch's slab sum, the
 // others stay zero
@@ -602,36 +601,40 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     else
         RC((linear_dgrad<4, 4, 2, 2>(w.dh1, theta + P_OFF[12], w.gy, w.d3, s25, S, 512, 9408, st,
                                      K_L1D)));
-    // ---- pool3 backward -> dz6 (a6 buffer: conv6 fwd no longer writes it), split ----
+    // ---- pool3 backward -> dz6 (a6 buffer: conv6 fwd no longer writes it), fp32 ----
     // Row/column 14 of conv6's 15x15 output is never pooled (floor mode), so its dz is zero: dz6
     // is stored compact as [S][14][14][192].  The weight gradient then runs over those rows as
     // they stand, and the data gradient reads the missing 15th row/column as zero padding.
-    RC((pool_scatter_nchw_xs<14, 14, 192>(w.gy, w.i3, w.a6, w.a6l, S, st)));
-    const XsT dz6 = w.x(w.a6, w.a6l), dz5 = w.x(w.gx, w.gxl), dz4 = w.x(w.a4, w.a4l);
-    // ---- conv6: wgrad (input a5), bias, dgrad -> dz5 = . * (a5 > 0) into gx (split) ----
+    // Every dZ is fp32: the data gradients run on the fp32 MFMA and read each dZ element once per
+    // tap (9x), the split-bf16 weight gradients split dZ while staging it (once per block)
+    RC((pool_scatter<14, 14, 192, true>(w.gy, w.i3, w.a6, S, st)));
+    float* const dz6 = w.a6;
+    float* const dz5 = w.gx;
+    float* const dz4 = w.a4;
+    // ---- conv6: wgrad (input a5), bias, dgrad -> dz5 = . * (a5 > 0) into gx ----
     RC(fork());
     // (192 x 192 tiles of 8 waves ran 9.10-9.13 against 9.41 ms in the lab,
     // profiles/r04/r04l/lab_wg6v.txt, but 9.26-9.29 against 9.10-9.12 in the product, A B A B on
     // one box, profiles/r04/r04s: kept 192 x 96)
-    RC((conv_wgrad_sz<13, 13, 192, 2, 6, 3, 2, 2, 3, 3, 2, 2, 14, true, true, XsSrc>(
-        dz6.hm, w.a5, S, 192, 1728, g.sw[5], g.sb[5], GEO[5].ZW, sw, K_WG6, 1728, zi(5), &zu[5],
-        dz6.l, w.a5l)));
-    // (the data gradients of conv4-6 run on the fp32 MFMA over their split dZ: the bf16 MFMA
-    // truncates small addends toward zero, which biases the per-channel sums of its outputs 30-100x
-    // beyond the CPU fp32 port's and failed SURVEY 8(c) on conv1-4 (tools/gemm_diag.py))
-    RC((conv_direct_s<14, 14, 192, 0, 2, 1, 6, 8, 6, 2, 13>(dz6, S, g.wd[5], 192, 1728,
-        EpiMaskXs<192, true>{dz5.hm, dz5.l, w.a5, S * 13 * 13}, st, K_DG6, 1728)));
-    if (debug_stop() == 6) return finish();       // (debug: dz5 stays in gx / gxl)
+    RC((conv_wgrad_sz<13, 13, 192, 2, 6, 3, 2, 2, 3, 3, 2, 2, 14, true, true, BufSrc, XsSrc>(
+        dz6, w.a5, S, 192, 1728, g.sw[5], g.sb[5], GEO[5].ZW, sw, K_WG6, 1728, zi(5), &zu[5],
+        nullptr, w.a5l)));
+    // (every data gradient runs on the fp32 MFMA: the bf16 MFMA truncates small addends toward
+    // zero, which biases the per-channel sums of its outputs 30-100x beyond the CPU fp32 port's
+    // and failed SURVEY 8(c) on conv1-4, conv6's alone too (tools/gemm_diag.py))
+    RC((conv_direct_sz<14, 14, 192, 0, 2, 1, 6, 8, 6, 2, false, 13>(dz6, S, g.wd[5], 192, 1728,
+        EpiMaskXs<192, false>{dz5, nullptr, w.a5, S * 13 * 13}, st, K_DG6, 1728)));
+    if (debug_stop() == 6) return finish();       // (debug: dz5 stays in gx)
     // ---- conv5: wgrad (input d2), bias, dgrad -> grad wrt d2 (dropout site 2), scattered through
-    //      pool2 straight into dz4 (a4 buffer, split; no gy round trip) ----
+    //      pool2 straight into dz4 (a4 buffer; no gy round trip) ----
     RC(fork());
-    RC((conv_wgrad_sz<11, 11, 96, 2, 6, 3, 2, 2, 3, 3, 2, 2, 0, false, true, XsSrc>(
-        dz5.hm, w.d2, S, 192, 864, g.sw[4], g.sb[4], GEO[4].ZW, sw, K_WG5, 864, zi(4), &zu[4],
-        dz5.l, w.d2l)));
-    RC((conv_direct_s<13, 13, 192, 0, 2, 1, 6, 8, 3, 2, 0>(dz5, S, g.wd[4], 96, 1728,
-        EpiDropScatterXs<11, 11, 96>{dz4.hm, dz4.l, w.d2, w.i2, s25, S * 11 * 11}, st, K_DG5,
-        1728)));
-    if (debug_stop() == 5) return finish();       // (debug: dz4 in a4 / a4l, dz5 in gx / gxl)
+    RC((conv_wgrad_sz<11, 11, 96, 2, 6, 3, 2, 2, 3, 3, 2, 2, 0, false, true, BufSrc, XsSrc>(
+        dz5, w.d2, S, 192, 864, g.sw[4], g.sb[4], GEO[4].ZW, sw, K_WG5, 864, zi(4), &zu[4],
+        nullptr, w.d2l)));
+    RC((conv_direct_sz<13, 13, 192, 0, 2, 1, 6, 8, 3, 2, false, 0>(dz5, S, g.wd[4], 96, 1728,
+        EpiDropScatterXs<11, 11, 96, false>{dz4, nullptr, w.d2, w.i2, s25, S * 11 * 11}, st,
+        K_DG5, 1728)));
+    if (debug_stop() == 5) return finish();       // (debug: dz4 in a4, dz5 in gx)
     // ---- conv4: wgrad (input a3), bias, dgrad -> dz3 = . * (a3 > 0) into gx (fp32) ----
     // dz3 and dz2 stay fp32: their data gradients have N = 48 columns, where the fp32 MFMA
     // kernels are faster than any split-bf16 form (profiles/r04/lab/lab_xs_r04b.txt: conv3's
@@ -639,12 +642,12 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     // gradients split dZ while staging (split-bf16 kernel over an fp32 dZ and a split layer input)
     RC(join());                                   // conv5's wgrad reads gx = dz5: done first
     RC(fork());
-    RC((conv_wgrad<20, 20, 96, 2, 3, 3, 2, 2, 0, false, true, XsSrc, XsSrcSM>(
-        dz4.hm, w.a3, S, 96, 864, g.sw[3], g.sb[3], GEO[3].ZW, sw, K_WG4, 864, zi(3), &zu[3],
-        dz4.l, w.a3l)));
-    RC((conv_direct_s<22, 22, 96, 0, 2, 1, 6, 8, 3, 2, 0>(dz4, S, g.wd[3], 96, 864,
+    RC((conv_wgrad<20, 20, 96, 2, 3, 3, 2, 2, 0, false, true, BufSrc, XsSrcSM>(
+        dz4, w.a3, S, 96, 864, g.sw[3], g.sb[3], GEO[3].ZW, sw, K_WG4, 864, zi(3), &zu[3],
+        nullptr, w.a3l)));
+    RC((conv_direct_sz<22, 22, 96, 0, 2, 1, 6, 8, 3, 2, false, 0>(dz4, S, g.wd[3], 96, 864,
         EpiMaskXs<96, false, true, 400>{w.gx, nullptr, w.a3, S * 20 * 20}, st, K_DG4, 864)));
-    if (debug_stop() == 4) return finish();       // (debug: dz3 in gx fp32, dz4 in a4 / a4l)
+    if (debug_stop() == 4) return finish();       // (debug: dz3 in gx, dz4 in a4)
     float* dz3 = w.gx;
     // ---- conv3: wgrad (input d1), bias, dgrad -> grad wrt d1 (site 1), scattered through pool1
     //      straight into dz2 (a2 buffer, fp32) ----
@@ -711,20 +714,15 @@ int flsim_pn1_workspace_offset(int which, int samples, long* offset_bytes) {
 }
 
 // a workspace tensor held in the split-bf16 form (split.h): the id of its L part (its HM part is
-// `which` itself), or -1 for an fp32 tensor.  gx is fp32 after a full default backward pass (dz1);
-// with FLSIM_DEBUG_BWD_STOP=6 or 5 it holds the split dz5.  (With FLSIM_C1_FUSE=1, dz1 is never
-// written and gx holds dz3 in fp32.)
+// `which` itself), or -1 for an fp32 tensor (every dZ: dz6 in a6, dz5 / dz3 / dz1 in gx, dz4 in
+// a4, dz2 in a2).
 int flsim_pn1_workspace_split_part(int which) {
-    if (which == 14 && (debug_stop() == 6 || debug_stop() == 5))
-        return 30;             // gx holds the split dz5 when the pass stopped after conv6 / conv5
     switch (which) {
         case 1: return 22;     // a1
         case 3: return 23;     // d1
         case 4: return 24;     // a3
         case 6: return 25;     // d2
         case 7: return 26;     // a5
-        case 8: return 27;     // dz6 (a6 buffer)
-        case 5: return 28;     // dz4 (a4 buffer)
         default: return -1;
     }
 }

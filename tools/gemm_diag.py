@@ -113,8 +113,8 @@ def main():
            4: lambda: nchw(W(14, (NS, 20, 20, 96)))}[stop]().double()
     r64 = gemm(torch.float64)
     r32 = gemm(torch.float32).double()
-    out = dict(stop=stop, gemm={6: "conv6 dgrad (x6)", 5: "conv5 dgrad (x6) + pool2 scatter",
-                                4: "conv4 dgrad (x6)"}[stop], items=items)
+    out = dict(stop=stop, gemm={6: "conv6 dgrad (fp32)", 5: "conv5 dgrad (fp32) + pool2 scatter",
+                                4: "conv4 dgrad (fp32)"}[stop], items=items)
     for name, t in (("gpu", gpu), ("cpu32", r32)):
         out[name] = stats(t, r64)
         # what the previous layer's bias gradient sees: the per-channel sums of the output

@@ -125,7 +125,7 @@ for STEP in "$@"; do
             echo "n=$N: $(head -1 $OUT/bench_n$N.txt)"
         done ;;
     facade)
-        timeout -k 10 600 python3 -u tools/facade_bench.py > $OUT/facade_bench.json 2> $OUT/facade_bench.err \
+        timeout -k 10 600 python3 -u tools/facade_bench.py --epochs 6 > $OUT/facade_bench.json 2> $OUT/facade_bench.err \
             || { echo "facade failed $?"; tail -5 $OUT/facade_bench.err; exit 1; }
         cut -c1-400 $OUT/facade_bench.json ;;
     facadetrace)
