@@ -238,6 +238,12 @@ def stream_step_probe(sim, iters=20):
 
 def main():
     args = parse()
+    # stdout carries exactly ONE line, the JSON result: RCCL prints a version banner on stdout when
+    # its communicator starts (profiles/r05/bench_forcedist.json), so the process's stdout goes to
+    # stderr and the result line is written to a saved copy of the original stdout
+    sys.stdout.flush()
+    result_fd = os.dup(1)
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -482,7 +488,10 @@ def main():
             "gpu_vs_cpu": round(value / cpu["value"], 1) if cpu else None,
             "last_loss": losses[-1] if losses else None,
         }
-        print(json.dumps(line), flush=True)
+        with os.fdopen(result_fd, "w") as out:
+            out.write(json.dumps(line) + "\n")
+    else:
+        os.close(result_fd)
     if dist_on:
         torch.distributed.destroy_process_group()
 

@@ -329,16 +329,21 @@ gemm_x6_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, in
                         bacc[i] = mfma_x32(af.x0, bf16_ones(true, true), bacc[i]);    // h + m
                     }
                 }
+                constexpr bool FRESH = x6_fresh(AL::KC) || X6Fresh<EPI>::value;
 #pragma unroll
                 for (int j = 0; j < FN; ++j) {
-                    acc[i][j] = x6_step<x6_fresh(AL::KC) || X6Fresh<EPI>::value>(acc[i][j], af.x0, af.x1, bf[j].x0,
-                                                           bf[j].x1, bf[j].x2);
+                    acc[i][j] = x6_step<FRESH>(acc[i][j], af.x0, af.x1, bf[j].x0, bf[j].x1,
+                                               bf[j].x2);
                 }
             }
             __syncthreads();
             cur ^= 1;
         }
     };
+    // Waves of one block may run different compiled forms of the loop, so they meet their
+    // barriers at different call sites.  That is sound on gfx9 (s_barrier counts waves) because
+    // every form runs the same block-uniform k range ks0 .. ks1 with exactly one barrier per
+    // k-step; keep both invariants when changing the loop.
     bool sum_wave = false;
     if constexpr (AMF) sum_wave = bwave;
     else if constexpr (EPI::ASUM) sum_wave = tn == 0 && wave * 64 < BM;

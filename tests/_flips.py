@@ -26,11 +26,12 @@ import torch.nn.functional as F
 
 from oracle import model_ref as MR
 
-# Bounds = 1.5 x the split-bf16 build's measured worst (round 4, profiles/r04/prof_r04e/flips.jsonl;
-# the results are bit-reproducible across boxes, r04e = r04f): teacher-forced rel-L2 up to 6.7e-7
-# over the 11 checks; decision flips at most 6 above 3 x the CPU fp32 port's own in one check,
-# 40 against the port's 21 summed.  A wrong mask or argmax rule flips thousands.
-TF_TOL = 1.0e-6
+# Bounds = 1.5 x the shipped build's measured worst (round 5: every data gradient on the fp32 MFMA,
+# profiles/r05/tol_r05j.jsonl; the results are bit-reproducible across boxes): teacher-forced
+# rel-L2 up to 2.82e-7 over the 12 checks (round 4's all-split build: 6.7e-7); decision flips at
+# most 6 above 3 x the CPU fp32 port's own in one check, 46 against the port's 24 summed.  A wrong
+# mask or argmax rule flips thousands.
+TF_TOL = 4.3e-7
 FLIP_C, FLIP_FLOOR = 3, 9
 GROUP = 1 << 20
 LAYERS = ("a1", "i1", "a3", "i2", "a5", "i3", "e1", "e2")

@@ -76,13 +76,14 @@ def test_n1024_d50_through_first_tick(pool, golden):
 # Stated bounds of the configs[1] trajectory test: the GPU's distance from the fp64 oracle is at
 # most GAP_C times the CPU fp32 port's own distance from it (+ a 2e-4 floor for the first epochs,
 # where both are at the fp32 noise level) in the running-max loss gap, and at most DRIFT_C times
-# it in parameters (JL sketch).  Both are 1.5 x the ratios the shipped build measured on MI355X from
-# the warm start (profiles/r04/r04j/pytest_gpu.txt MEASURED: loss gap 2.75, parameter drift 1.26).
+# it in parameters (JL sketch).  DRIFT_C is 1.5 x the ratio the shipped build measured on MI355X
+# from the warm start (round 5, profiles/r05/tol_r05j.jsonl MEASURED: parameter drift 1.16, loss
+# gap 1.46; round 4's r04j: 1.26 and 2.75).
 # These 52-epoch ratios are chaotic: builds whose teacher-forced gradients agree to 4 digits measured
 # 1.61 / 0.81-1.27 (fp32 MFMA, r03a), 1.74 / 0.91 (split-bf16, bias column sum on the VALU, r04e)
 # and 2.75 / 1.26 (the same with the column sum on the MFMA, r04j).
 GAP_C = 4.1      # logged only (MEASURED loss_gap_ratio_max), see below
-DRIFT_C = 1.9
+DRIFT_C = 1.75
 # The gate that is not chaotic: over the epochs where the CPU fp32 port still
 # agrees with fp64 (its running-max loss gap <= AGREE = 5e-5: epochs 0-35 of traj_n10.npz, well
 # before the divergence of epochs 41-44), the GPU's running-max loss gap must stay within 2x the

@@ -20,10 +20,11 @@ pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not has_gpu(), reason="needs a
 
 
 # per-tensor rel-L2 of the GPU gradient against the fp64 reference with the GPU's own decisions.
-# The bound is 1.5 x the split-bf16 build's measured worst: features.0.bias at 3.14e-5 (dropout,
-# items2; 1.10e-5 and 2.32e-5 for the other cases; profiles/r04/prof_r04e/tol.jsonl).
-# A wrong kernel misses by orders of magnitude.
-TF_TOL = 4.7e-5
+# The bound is 1.5 x the shipped build's measured worst: features.18.weight at 1.35e-6 (dropout,
+# items1; 8.3e-7 and 1.10e-6 for the other cases; profiles/r05/tol_r05j.jsonl).  Round
+# 4's build, with the data gradients on the split-bf16 MFMA, measured 3.14e-5: the MFMA's
+# truncating sums biased them.  A wrong kernel misses by orders of magnitude.
+TF_TOL = 2.1e-6
 
 def _tol_log(worst):
     """Per-tensor error census across builds (measurement only: FLSIM_TOL_LOG=<file>)."""

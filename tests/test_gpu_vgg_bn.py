@@ -12,12 +12,12 @@ order.  Tolerances:
     tools/dbg_bn.py: 1 of 65,536 pooled conv8 values for worker (0, 0, 0)) moves one
     (sample, channel) gradient to another window position, and the BatchNorm backward spreads
     that over the whole channel: 0.1-1.5 % in every feature tensor.  The exactness of every
-    backward kernel is the teacher-forced test's job (the GPU's own decisions, 5e-5);
+    backward kernel is the teacher-forced test's job (the GPU's own decisions, 7e-6);
   * conv biases: a bias in front of a BatchNorm cancels, so its gradient is rounding noise of a
     zero sum -- checked as an absolute error against the whole gradient's norm (<= 1e-6 |g64|,
     or 10x the CPU's);
   * teacher-forced (the GPU's ReLU / argmax / dropout decisions in an fp64 reference with fp64
-    batch statistics): per-tensor rel-L2 <= 5e-5 (conv biases absolute as above), losses 1e-5;
+    batch statistics): per-tensor rel-L2 <= 7e-6 (conv biases absolute as above), losses 1e-5;
   * running buffers: running_var rel 1e-5, running_mean abs 1e-6 after one call (the trajectory
     test: abs 2e-4, see tests/test_oracle_golden._check_running);
   * losses |dloss| <= 1e-4 / 2e-3 / 5e-3 / 1e-2 over epochs 0-3: the near-tie flips above, then
@@ -200,9 +200,10 @@ def test_vgg_bn_gradient_teacher_forced_decisions(pool, dropout, items):
 
     P, ref, lrefs = forced(torch.float64)
     np.testing.assert_allclose(loss, lrefs, atol=1e-5)
-    # 1.5 x the split-bf16 build's measured worst, 4.31e-5 (features.1.bias, dropout items2;
-    # profiles/r04/prof_r04e/tol.jsonl stores it as 0.861 of the former 5e-5 bound)
-    _check_grad(g, ref, rtol=6.5e-5)
+    # 1.5 x the shipped build's measured worst, 4.57e-6 (features.23.weight, dropout items2;
+    # profiles/r05/tol_r05j.jsonl stores it as 0.0703 of the former 6.5e-5 bound; round 4's build,
+    # data gradients on the split-bf16 MFMA: 4.31e-5)
+    _check_grad(g, ref, rtol=7.0e-6)
     # per tensor no farther from fp64 than 2x the CPU fp32 port (same decisions);
     # the conv biases ahead of a BatchNorm have an exact gradient of 0 (floor: the whole gradient)
     import _flips

@@ -206,8 +206,10 @@ def test_vgg11_oracle_trajectory(golden):
     for t, ref in enumerate(g["train_losses"]):
         loss = sim.epoch()
         # host-CPU fp32 drift after the first Adam steps, as in test_training_trajectory: exact
-        # at epochs 0-1 and 2.1e-5 at epoch 2 on the build host; bound 5x that
-        assert abs(loss - ref) <= (1e-5 if t < 2 else 1e-4), (t, loss, ref)
+        # at epochs 0-1, 2.1e-5 at epoch 2 on one build host; other EPYC hosts drift further
+        # (PerformantNet1: 1.2e-4 by epoch 4, running_mean 8e-4 / 1.6e-3 below), so the bound
+        # follows that cross-host spread, not one host's figure
+        assert abs(loss - ref) <= (1e-5 if t < 2 else 5e-4), (t, loss, ref)
         np.testing.assert_allclose(
             [float((a.astype(np.float64) ** 2).sum()) for a in MR.split_flat(sim.theta, "vgg11")],
             g[f"train_theta{t}_stats"][:, 1], rtol=1e-3)
@@ -261,8 +263,10 @@ def test_vgg11_bn_oracle_trajectory_and_eval(golden):
     for t, ref in enumerate(g["train_losses"]):
         loss = sim.epoch()
         # host-CPU fp32 drift after the first Adam steps, as in test_training_trajectory: exact
-        # at epochs 0-1 and 2.1e-5 at epoch 2 on the build host; bound 5x that
-        assert abs(loss - ref) <= (1e-5 if t < 2 else 1e-4), (t, loss, ref)
+        # at epochs 0-1, 2.1e-5 at epoch 2 on one build host; other EPYC hosts drift further
+        # (PerformantNet1: 1.2e-4 by epoch 4, running_mean 8e-4 / 1.6e-3 below), so the bound
+        # follows that cross-host spread, not one host's figure
+        assert abs(loss - ref) <= (1e-5 if t < 2 else 5e-4), (t, loss, ref)
         np.testing.assert_allclose(
             [float((a.astype(np.float64) ** 2).sum())
              for a in MR.split_flat(sim.theta, "vgg11_bn")][2::4],     # BatchNorm weights

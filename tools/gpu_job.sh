@@ -7,6 +7,7 @@
 #   bench             the default bench line (with its CPU baseline) + tools/bench_summary.py
 #   benchq            the default bench line without the CPU baseline
 #   ab:<lib>          bench line of an alternative libflsim.so (FLSIM_LIB=<lib>) beside benchq
+#   abenv:<VAR=VAL>   bench line with one environment setting beside benchq (E1 A1 E2 A2)
 #   trace             rocprofv3 --kernel-trace --stats of a short bench (kernel_stats.csv)
 #   pmc               FETCH/WRITE + two SQ passes on one 128-worker chunk, traffic table, summary
 #   tatd              TA / TD / TCP passes on one 128-worker chunk (tools/pmc_summary_ta.py)
@@ -74,6 +75,9 @@ for STEP in "$@"; do
     ab:*)
         LIB=${STEP#ab:}
         bench_line B1 FLSIM_LIB=$LIB; bench_line A1; bench_line B2 FLSIM_LIB=$LIB; bench_line A2 ;;
+    abenv:*)
+        KV=${STEP#abenv:}
+        bench_line E1 $KV; bench_line A1; bench_line E2 $KV; bench_line A2 ;;
     trace)
         timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run \
             -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-stream > $OUT/trace.log 2>&1 \
