@@ -15,6 +15,7 @@
 #   gloo2             2-rank gloo rehearsal of the N > 1 path through bench.py (n = 256)
 #   forcedist         torchrun --nproc-per-node 1 bench.py --force-dist (RCCL at world size 1)
 #   sizes             the per-rank loads of an N-GPU job on one GPU: n = 128 / 256 / 512
+#   aggceil           tools/agg_ceiling.py (torch streams at the aggregation paths' sizes)
 #   facade            tools/facade_bench.py (the FL.agents reference loop, n = 1024)
 #   configs           tools/gpu_configs_all.sh (the other BASELINE configs)
 #   lab:<bin>[:<arg>] a lab binary from tools/lab (built beforehand on the CPU)
@@ -22,6 +23,8 @@
 #   diag[:<pkg>]      tools/survey_diag.py (SURVEY 8(c) per tensor; <pkg>: another build's flsim)
 #   gemmdiag          tools/gemm_diag.py for the conv6 / conv5 / conv4 data-gradient GEMMs
 #   facadetrace       rocprofv3 kernel trace of tools/facade_bench.py + tools/trace_gaps.py
+#   streampmc         SQ counters of the post-all-reduce stream (tools/agg_bench.py, tools/stream_pmc.py)
+#   c1trace           rocprofv3 kernel trace of configs[1] (n = 10, warm start) + tools/trace_gaps.py
 set -u
 TAG=${1:?tag}
 shift
@@ -128,10 +131,31 @@ for STEP in "$@"; do
             python3 tools/bench_summary.py $OUT/bench_n$N.json > $OUT/bench_n$N.txt
             echo "n=$N: $(head -1 $OUT/bench_n$N.txt)"
         done ;;
+    aggceil)
+        timeout -k 10 300 python3 -u tools/agg_ceiling.py > $OUT/agg_ceiling.txt 2>&1 \
+            || { echo "agg ceiling failed $?"; tail -5 $OUT/agg_ceiling.txt; exit 1; }
+        cat $OUT/agg_ceiling.txt ;;
     facade)
         timeout -k 10 600 python3 -u tools/facade_bench.py --epochs 6 > $OUT/facade_bench.json 2> $OUT/facade_bench.err \
             || { echo "facade failed $?"; tail -5 $OUT/facade_bench.err; exit 1; }
         cut -c1-400 $OUT/facade_bench.json ;;
+    streampmc)
+        D=$OUT/streampmc; mkdir -p $D
+        timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE \
+            --output-format csv -d $D/p1 -o run --kernel-include-regex "k_agg_stream|k_slab_step" \
+            -- python3 tools/agg_bench.py --iters 5 > $D/p1.log 2>&1 || { echo "stream pmc failed $?"; tail -5 $D/p1.log; exit 1; }
+        cp $(find $D/p1 -name "*counter_collection.csv" | head -1) $D/counters.csv
+        python3 tools/stream_pmc.py $D/counters.csv | tee $D/summary.txt ;;
+    c1trace)
+        timeout -k 10 120 python -u tools/warm_start_file.py --out $OUT/warm_start.pt > $OUT/c1_warm.log 2>&1 \
+            || { echo "warm start failed"; exit 1; }
+        timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c1trace -o run \
+            -- python3 bench.py --n_workers 10 --delay 50 --model_file $OUT/warm_start.pt --steps 40 \
+            --warmup 5 --no-cpu-baseline > $OUT/c1trace.log 2>&1 \
+            || { echo "configs1 trace failed $?"; tail -5 $OUT/c1trace.log; exit 1; }
+        D=$(dirname $(find $OUT/c1trace -name "run_kernel_trace.csv" | head -1))
+        cp $D/run_kernel_stats.csv $OUT/c1_kernel_stats.csv
+        python3 tools/trace_gaps.py $D 0.5 > $OUT/c1_gaps.txt && head -30 $OUT/c1_gaps.txt ;;
     facadetrace)
         timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/ftrace -o run \
             -- python3 tools/facade_bench.py --epochs 2 > $OUT/facade_trace.log 2>&1 \
