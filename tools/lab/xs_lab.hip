@@ -337,6 +337,14 @@ int main(int argc, char** argv) {
     G("wg6v 192x144x6", 13, 192, 192, 256, 6, 3, 2, 3)
     G("wg6v 192x96x8", 13, 192, 192, 256, 3, 3, 4, 2)
     G("wg6v 192x192x8", 13, 192, 192, 256, 3, 6, 4, 2)
+    // round 5: larger per-wave fragments at fewer waves
+    C("fwd6wa", 13, 192, 2, 0, 192, 8, 6, 2, 2, 2, 6, 8, 3, 2, 2)
+    C("fwd6wb", 13, 192, 2, 0, 192, 4, 12, 4, 1, 2, 6, 8, 3, 2, 2)
+    C("fwd6wc", 13, 192, 2, 0, 192, 8, 12, 2, 1, 2, 6, 8, 3, 2, 2)
+    C("fwd6wd", 13, 192, 2, 0, 192, 6, 6, 2, 2, 2, 6, 8, 3, 2, 2)
+    G("wg6wa", 13, 192, 192, 256, 6, 6, 2, 1)
+    G("wg6wb", 13, 192, 192, 256, 6, 12, 2, 1)
+    G("wg6wc", 13, 192, 192, 256, 12, 3, 1, 3)
     // weight gradients (product tiles and splits: >= 32 k-steps per split)
     G("wg6", 13, 192, 192, 256, 6, 3, 2, 2)
     G("wg5", 11, 96, 192, 512, 6, 3, 2, 2)
