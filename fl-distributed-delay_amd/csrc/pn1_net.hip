@@ -534,6 +534,14 @@ static bool concurrent_backward(int S) {
 // so each data-gradient GEMM can be checked on its own inputs (tools/gemm_diag.py); the weight
 // gradients that ran (conv6 .. conv<stop>, the linear layers) reach the epoch's slab sum, the
 // others stay zero
+// fragment rows per wave of the conv4-6 fp32 data gradients on chunks of at most
+// small_chunk_samples() samples: 2, the large-chunk tile (configs[1] 984 -> 995 worker-steps/s
+// against 1, A B A B, profiles/r05/c1_dg_fms.txt; measurement override -DFLSIM_DG_FMS=<1|2>)
+#ifndef FLSIM_DG_FMS
+#define FLSIM_DG_FMS 2
+#endif
+constexpr int DG_FMS = FLSIM_DG_FMS;
+
 static int debug_stop() {
     static int v = -1;
     if (v < 0) {
@@ -622,7 +630,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     // (every data gradient runs on the fp32 MFMA: the bf16 MFMA truncates small addends toward
     // zero, which biases the per-channel sums of its outputs 30-100x beyond the CPU fp32 port's
     // and failed SURVEY 8(c) on conv1-4, conv6's alone too (tools/gemm_diag.py))
-    RC((conv_direct_sz<14, 14, 192, 0, 2, 1, 6, 8, 6, 2, false, 13>(dz6, S, g.wd[5], 192, 1728,
+    RC((conv_direct_sz<14, 14, 192, 0, 2, DG_FMS, 6, 8, 6, 2, false, 13>(dz6, S, g.wd[5], 192, 1728,
         EpiMaskXs<192, false>{dz5, nullptr, w.a5, S * 13 * 13}, st, K_DG6, 1728)));
     if (debug_stop() == 6) return finish();       // (debug: dz5 stays in gx)
     // ---- conv5: wgrad (input d2), bias, dgrad -> grad wrt d2 (dropout site 2), scattered through
@@ -631,7 +639,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC((conv_wgrad_sz<11, 11, 96, 2, 6, 3, 2, 2, 3, 3, 2, 2, 0, false, true, BufSrc, XsSrc>(
         dz5, w.d2, S, 192, 864, g.sw[4], g.sb[4], GEO[4].ZW, sw, K_WG5, 864, zi(4), &zu[4],
         nullptr, w.d2l)));
-    RC((conv_direct_sz<13, 13, 192, 0, 2, 1, 6, 8, 3, 2, false, 0>(dz5, S, g.wd[4], 96, 1728,
+    RC((conv_direct_sz<13, 13, 192, 0, 2, DG_FMS, 6, 8, 3, 2, false, 0>(dz5, S, g.wd[4], 96, 1728,
         EpiDropScatterXs<11, 11, 96, false>{dz4, nullptr, w.d2, w.i2, s25, S * 11 * 11}, st,
         K_DG5, 1728)));
     if (debug_stop() == 5) return finish();       // (debug: dz4 in a4, dz5 in gx)
@@ -645,7 +653,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC((conv_wgrad<20, 20, 96, 2, 3, 3, 2, 2, 0, false, true, BufSrc, XsSrcSM>(
         dz4, w.a3, S, 96, 864, g.sw[3], g.sb[3], GEO[3].ZW, sw, K_WG4, 864, zi(3), &zu[3],
         nullptr, w.a3l)));
-    RC((conv_direct_sz<22, 22, 96, 0, 2, 1, 6, 8, 3, 2, false, 0>(dz4, S, g.wd[3], 96, 864,
+    RC((conv_direct_sz<22, 22, 96, 0, 2, DG_FMS, 6, 8, 3, 2, false, 0>(dz4, S, g.wd[3], 96, 864,
         EpiMaskXs<96, false, true, 400>{w.gx, nullptr, w.a3, S * 20 * 20}, st, K_DG4, 864)));
     if (debug_stop() == 4) return finish();       // (debug: dz3 in gx, dz4 in a4)
     float* dz3 = w.gx;

@@ -8,6 +8,7 @@
 #   benchq            the default bench line without the CPU baseline
 #   ab:<lib>          bench line of an alternative libflsim.so (FLSIM_LIB=<lib>) beside benchq
 #   abenv:<VAR=VAL>   bench line with one environment setting beside benchq (E1 A1 E2 A2)
+#   c1abenv:<VAR=VAL> the same on configs[1] (n = 10, d = 50, the warm start)
 #   trace             rocprofv3 --kernel-trace --stats of a short bench (kernel_stats.csv)
 #   pmc               FETCH/WRITE + two SQ passes on one 128-worker chunk, traffic table, summary
 #   tatd              TA / TD / TCP passes on one 128-worker chunk (tools/pmc_summary_ta.py)
@@ -46,9 +47,9 @@ pmc_passes() {   # <dir> <pass>... : one counter group per rocprofv3 run over on
     done
 }
 
-bench_line() {   # <name> [env...] : one bench line without the CPU baseline
+bench_line() {   # <name> [env...] : one bench line without the CPU baseline ($BENCH_ARGS appended)
     local name=$1; shift
-    env "$@" timeout -k 10 400 python3 -u bench.py --no-cpu-baseline > $OUT/bench_$name.json \
+    env "$@" timeout -k 10 400 python3 -u bench.py --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/bench_$name.json \
         2> $OUT/bench_$name.err || { echo "bench $name failed $?"; tail -5 $OUT/bench_$name.err; exit 1; }
     python3 tools/bench_summary.py $OUT/bench_$name.json > $OUT/bench_$name.txt
     echo "$name: $(head -1 $OUT/bench_$name.txt)"
@@ -78,6 +79,13 @@ for STEP in "$@"; do
     ab:*)
         LIB=${STEP#ab:}
         bench_line B1 FLSIM_LIB=$LIB; bench_line A1; bench_line B2 FLSIM_LIB=$LIB; bench_line A2 ;;
+    c1abenv:*)
+        KV=${STEP#c1abenv:}
+        timeout -k 10 120 python -u tools/warm_start_file.py --out $OUT/warm_start.pt > $OUT/c1_warm.log 2>&1 \
+            || { echo "warm start failed"; exit 1; }
+        BENCH_ARGS="--n_workers 10 --delay 50 --model_file $OUT/warm_start.pt --steps 200 --warmup 10"
+        bench_line c1E1 $KV; bench_line c1A1; bench_line c1E2 $KV; bench_line c1A2
+        BENCH_ARGS="" ;;
     abenv:*)
         KV=${STEP#abenv:}
         bench_line E1 $KV; bench_line A1; bench_line E2 $KV; bench_line A2 ;;
