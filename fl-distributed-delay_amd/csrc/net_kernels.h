@@ -761,15 +761,18 @@ static int conv_pool_direct(const float* X, int S, const float* Wpk, int KP, flo
 }
 
 // Small chunks (configs[1]: 5 workers = 640 samples per epoch) leave the 256-row direct tiles with
-// a few rounds of blocks on 256 CUs, so the last, partial round costs up to 15-25 % on the
-// conv5/conv6 passes; chunks of at most small_chunk_samples() samples run the same GEMMs with
-// 128-row tiles (FM halved).  The k order per output is unchanged, so the results are
-// bit-identical.  FLSIM_SMALL_S overrides the threshold (0: never).
+// a few rounds of blocks on 256 CUs; chunks of at most small_chunk_samples() samples can run the
+// same GEMMs with half-height tiles (FM halved, and the weight gradients' small tiles).  The k
+// order per output is unchanged, so the results are bit-identical.  Round 3 measured them faster
+// up to 2048 samples; on round 5's kernels they lose at configs[1]'s 640 samples (993 against 1038
+// worker-steps/s, profiles/r05/ab/c1_small_tiles_off.txt) and still win on the facade's 128-sample
+// calls (713-722 against 677, ab/facade_small_tiles.txt): threshold 256 samples.  FLSIM_SMALL_S
+// sets it.
 static int small_chunk_samples() {
     static int s = -1;
     if (s < 0) {
         const char* e = getenv("FLSIM_SMALL_S");
-        s = e ? atoi(e) : 2048;
+        s = e ? atoi(e) : 256;
     }
     return s;
 }

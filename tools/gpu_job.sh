@@ -17,6 +17,7 @@
 #   forcedist         torchrun --nproc-per-node 1 bench.py --force-dist (RCCL at world size 1)
 #   sizes             the per-rank loads of an N-GPU job on one GPU: n = 128 / 256 / 512
 #   aggceil           tools/agg_ceiling.py (torch streams at the aggregation paths' sizes)
+#   facadeab:<VAR=VAL> the facade loop with one environment setting, E A E A
 #   facade            tools/facade_bench.py (the FL.agents reference loop, n = 1024)
 #   configs           tools/gpu_configs_all.sh (the other BASELINE configs)
 #   lab:<bin>[:<arg>] a lab binary from tools/lab (built beforehand on the CPU)
@@ -164,6 +165,14 @@ for STEP in "$@"; do
         D=$(dirname $(find $OUT/c1trace -name "run_kernel_trace.csv" | head -1))
         cp $D/run_kernel_stats.csv $OUT/c1_kernel_stats.csv
         python3 tools/trace_gaps.py $D 0.5 > $OUT/c1_gaps.txt && head -30 $OUT/c1_gaps.txt ;;
+    facadeab:*)
+        KV=${STEP#facadeab:}
+        for R in E1 A1 E2 A2; do
+            if [ ${R:0:1} = E ]; then ENVS="$KV"; else ENVS="FLSIM_NOOP=1"; fi
+            env $ENVS timeout -k 10 300 python3 -u tools/facade_bench.py --epochs 4 > $OUT/facade_$R.json \
+                2> $OUT/facade_$R.err || { echo "facade $R failed $?"; tail -5 $OUT/facade_$R.err; exit 1; }
+            echo "$R $(cut -c1-120 $OUT/facade_$R.json)"
+        done ;;
     facadetrace)
         timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/ftrace -o run \
             -- python3 tools/facade_bench.py --epochs 2 > $OUT/facade_trace.log 2>&1 \
