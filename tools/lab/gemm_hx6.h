@@ -134,8 +134,8 @@ struct HaloA {
 
 // Block = WAVES waves stacked along M (each 16*FM rows) x all BN = 16*FN columns of its n-tile.
 // ksteps = 9 * CS.
-template <int FM, int FN, int WAVES, class HA, class BL, class EPI>
-__global__ void __launch_bounds__(64 * WAVES)
+template <int FM, int FN, int WAVES, class HA, class BL, class EPI, int MINW = 1>
+__global__ void __launch_bounds__(64 * WAVES, MINW)
 gemm_hx6_kernel(HA ha, BL bl, EPI epi, int tiles_m, int tiles_n) {
     constexpr int NT = 64 * WAVES;
     constexpr int BM = 16 * FM * WAVES;

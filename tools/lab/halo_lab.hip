@@ -99,7 +99,7 @@ static int max_patch_rows(int M, int BM) {
     return mx;
 }
 
-template <int IH, int CI, int CO, bool WIN, int FM, int FN, int WAVES, int KB, int NRP>
+template <int IH, int CI, int CO, bool WIN, int FM, int FN, int WAVES, int KB, int NRP, int MINW = 1>
 static void shape(const char* tag, const Xs& Xsm, const Xs& Wx, const float* b, float* Y0,
                   float* Y1, int S) {
     constexpr int PAD = 2, NT = 64 * WAVES, BM = 16 * FM * WAVES, BN = 16 * FN;
@@ -132,13 +132,14 @@ static void shape(const char* tag, const Xs& Xsm, const Xs& Wx, const float* b, 
     const double flops = 2.0 * M * CO * KP;
     auto tf = [&](double t) { return flops / (t * 1e-3) / 1e12; };
     auto kd = gemm_dx6_kernel<FM, FN, WAVES, KB, 2, AD, BD, EpiBiasRelu>;
-    auto kh = gemm_hx6_kernel<FM, FN, WAVES, HA, BD, EpiBiasRelu>;
+    auto kh = gemm_hx6_kernel<FM, FN, WAVES, HA, BD, EpiBiasRelu, MINW>;
     double t[2][2];
     for (int r = 0; r < 2; ++r) {
         t[r][0] = timeit(kd, g, NT, ad, bd, EpiBiasRelu{Y0, b, M, CO}, KP / GK, tm, tn);
         t[r][1] = timeit(kh, g, NT, ha, bd, EpiBiasRelu{Y1, b, M, CO}, tm, tn);
     }
     const size_t d = ndiff(Y0, Y1, (size_t)M * CO);
+    printf("[waves per EU >= %d] ", MINW);
     printf("%-6s %3dx%3d %d waves  product dx6 %7.3f %7.3f ms %6.1f TF/s | halo (patch %d rows, "
            "%.1f KB) %7.3f %7.3f ms %6.1f TF/s (x%.3f) | differ %zu of %zu\n",
            tag, BM, BN, WAVES, t[0][0], t[1][0], tf(t[1][0]), need,
@@ -178,18 +179,25 @@ int main(int argc, char** argv) {
     if (want("fwd2")) {
         const Xs x = sm(34 * 34, 48);
         shape<34, 48, 48, true, 4, 3, 4, 3, 14>("fwd2", x, Wx, b, Y0, Y1, S);
+        shape<34, 48, 48, true, 4, 3, 4, 3, 14, 2>("fwd2", x, Wx, b, Y0, Y1, S);
+        shape<34, 48, 48, true, 4, 3, 8, 3, 22, 2>("fwd2", x, Wx, b, Y0, Y1, S);
+        shape<34, 48, 48, true, 2, 3, 8, 3, 14, 2>("fwd2", x, Wx, b, Y0, Y1, S);
+        shape<34, 48, 48, true, 2, 3, 8, 3, 14, 3>("fwd2", x, Wx, b, Y0, Y1, S);
         CK(hipFree(x.hm));
         CK(hipFree(x.l));
     }
     if (want("fwd3")) {
         const Xs x = sm(18 * 18, 48);
         shape<18, 48, 96, false, 2, 6, 8, 3, 18>("fwd3", x, Wx, b, Y0, Y1, S);
+        shape<18, 48, 96, false, 4, 6, 4, 3, 18, 2>("fwd3", x, Wx, b, Y0, Y1, S);
         CK(hipFree(x.hm));
         CK(hipFree(x.l));
     }
     if (want("fwd4")) {
         const Xs x = sm(20 * 20, 96);
         shape<20, 96, 96, true, 2, 6, 8, 3, 20>("fwd4", x, Wx, b, Y0, Y1, S);
+        shape<20, 96, 96, true, 2, 6, 8, 3, 20, 3>("fwd4", x, Wx, b, Y0, Y1, S);
+        shape<20, 96, 96, true, 4, 6, 4, 3, 20, 2>("fwd4", x, Wx, b, Y0, Y1, S);
         CK(hipFree(x.hm));
         CK(hipFree(x.l));
     }
