@@ -78,6 +78,17 @@ constexpr bool x6_fresh(bool kc) {
 }
 constexpr bool x6_fresh_bias() { return FLSIM_X6_FRESH >= 2; }
 
+// Main-loop schedule (-DFLSIM_X6_PP_V=V -DFLSIM_X6_PP_W=W -DFLSIM_X6_PP_L=L; V = 0: the
+// compiler's order): the
+// staging of the next k-step interleaved with the current k-step's MFMAs, per MFMA V VALU, an LDS
+// store every W MFMAs, a global load every L (tools/lab/pp_lab.hip)
+#ifndef FLSIM_X6_PP_V
+#define FLSIM_X6_PP_V 0
+#define FLSIM_X6_PP_W 2
+#define FLSIM_X6_PP_L 4
+#endif
+constexpr int X6_PP_V = FLSIM_X6_PP_V, X6_PP_W = FLSIM_X6_PP_W, X6_PP_L = FLSIM_X6_PP_L;
+
 typedef short s16x4v __attribute__((ext_vector_type(4)));
 
 // 4 consecutive k of one tile row from a k-major bf16 plane [16][LD] (ds_read_b64_tr_b16)
@@ -300,7 +311,15 @@ gemm_x6_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, in
     auto main_loop = [&](auto with_sum) {
         constexpr bool WS = decltype(with_sum)::value;
         for (int ks = ks0; ks < ks1; ++ks) {
-            if (ks + 1 < ks1) {
+            if constexpr (X6_PP_V > 0) {
+                // branch-free (one basic block, so the staging can be interleaved with the
+                // MFMAs, below): the last k-step stages into the buffer nobody reads again, and
+                // the loads past the split re-read its last k-step
+                stage(lds + (cur ^ 1) * BUF);
+                const int kl = ks + 2 < ks1 ? ks + 2 : ks1 - 1;
+                al.load(kl, ra);
+                bl.load(kl, rb);
+            } else if (ks + 1 < ks1) {
                 stage(lds + (cur ^ 1) * BUF);
                 if (ks + 2 < ks1) {
                     al.load(ks + 2, ra);
@@ -334,6 +353,18 @@ gemm_x6_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, in
                 for (int j = 0; j < FN; ++j) {
                     acc[i][j] = x6_step<FRESH>(acc[i][j], af.x0, af.x1, bf[j].x0, bf[j].x1,
                                                bf[j].x2);
+                }
+            }
+            if constexpr (X6_PP_V > 0) {
+                // per MFMA X6_PP_V VALU (the staging's split and address arithmetic), an LDS
+                // store every X6_PP_W MFMAs and a global load every X6_PP_L
+#pragma unroll
+                for (int n = 0; n < 3 * FM * FN; ++n) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, X6_PP_V, 0);
+                    if (n % X6_PP_W == 0) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+                    if (n % X6_PP_L == 1 % X6_PP_L)
+                        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
                 }
             }
             __syncthreads();

@@ -1,13 +1,18 @@
 // Lab variant of gemm_x6_kernel (development tool, not part of libflsim.so): where the next
 // k-step's LDS stores and global loads sit in the main loop.  MODE 0: first (the product's
-// order); 1: after the first A fragment's MFMAs; 2: after half of them.  A fragments are read
-// one ahead.  Fresh accumulation off (the product's default level).
+// order); 1: after the first A fragment's MFMAs; 2: after half of them; 3: first, with the loop
+// body branch-free (one basic block: the product's `if (ks + 1 < ks1)` around the staging splits
+// the staging VALU and the MFMAs into separate blocks); 4: 3 plus sched_group_barrier
+// interleaving (one MFMA, two VALU, every other MFMA one LDS store); 5: per MFMA V VALU, an LDS
+// store every W, a global load every L, an LDS read every R MFMAs (template parameters).  A fragments are read one ahead.  Fresh accumulation off (the product's
+// default level).
 #pragma once
 #include "gemm_x6.h"
 
 namespace flsim {
 
-template <int MODE, int FM, int FN, int WAVES_M, int WAVES_N, class AL, class BL, class EPI>
+template <int MODE, int FM, int FN, int WAVES_M, int WAVES_N, class AL, class BL, class EPI,
+          int V = 3, int W = 2, int LG = 4, int R = 0>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N)
 gemm_x6pp_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, int tiles_m,
                int tiles_n) {
@@ -96,7 +101,14 @@ gemm_x6pp_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, 
         for (int ks = ks0; ks < ks1; ++ks) {
             const bool more = ks + 1 < ks1;
             auto next = [&]() {
-                if (more) {
+                if constexpr (MODE >= 3) {
+                    // branch-free: the last k-step stages into the buffer nobody reads again and
+                    // the loads past the split re-read its last k-step
+                    stage(lds + (cur ^ 1) * BUF);
+                    const int kl = ks + 2 < ks1 ? ks + 2 : ks1 - 1;
+                    al.load(kl, ra);
+                    bl.load(kl, rb);
+                } else if (more) {
                     stage(lds + (cur ^ 1) * BUF);
                     if (ks + 2 < ks1) {
                         al.load(ks + 2, ra);
@@ -104,7 +116,7 @@ gemm_x6pp_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, 
                     }
                 }
             };
-            if constexpr (MODE == 0) next();
+            if constexpr (MODE == 0 || MODE >= 3) next();
             const float* A = lds + cur * BUF;
             const float* B = A + TA::FL;
             if constexpr (WS && !AMF) {
@@ -140,6 +152,29 @@ gemm_x6pp_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, 
                     }
                 }
                 if (i + 1 < FM) af = an;
+            }
+            if constexpr (MODE == 4) {
+                // interleave: one MFMA, two VALU, and every other MFMA one LDS store
+#pragma unroll
+                for (int n = 0; n < 3 * FM * FN; ++n) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+                    if (n % 2 == 0) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+                }
+            }
+            if constexpr (MODE == 5) {
+                // per MFMA: V VALU; every W-th MFMA one LDS store, every L-th one global load,
+                // every R-th one LDS read (R = 0: LDS reads unconstrained)
+#pragma unroll
+                for (int n = 0; n < 3 * FM * FN; ++n) {
+                    if constexpr (R > 0) {
+                        if (n % R == 0) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    }
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, V, 0);
+                    if (n % W == 0) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+                    if (n % LG == 1 % LG) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+                }
             }
             __syncthreads();
             cur ^= 1;

@@ -82,25 +82,32 @@ static void conv(const char* tag, const Xs& Xx, const Xs& Wx, const float* b, fl
     const dim3 g(tm * tn);
     auto tf = [&](double t) { return flops / (t * 1e-3) / 1e12; };
     auto prod = gemm_x6_kernel<FM, FN, WM, WN, AL, BL, EpiBiasRelu>;
-    auto m0 = gemm_x6pp_kernel<0, FM, FN, WM, WN, AL, BL, EpiBiasRelu>;
-    auto m1 = gemm_x6pp_kernel<1, FM, FN, WM, WN, AL, BL, EpiBiasRelu>;
-    auto m2 = gemm_x6pp_kernel<2, FM, FN, WM, WN, AL, BL, EpiBiasRelu>;
     const size_t n = (size_t)M * CO;
-    double t[2][4];
-    size_t d[3];
-    for (int r = 0; r < 2; ++r) {
-        t[r][0] = timeit(prod, g, NT, al, bl, EpiBiasRelu{Y0, b, M, CO}, KP / GK, KP / GK, tm, tn);
-        t[r][1] = timeit(m0, g, NT, al, bl, EpiBiasRelu{Y1, b, M, CO}, KP / GK, KP / GK, tm, tn);
-        if (r == 0) d[0] = ndiff(Y0, Y1, n);
-        t[r][2] = timeit(m1, g, NT, al, bl, EpiBiasRelu{Y1, b, M, CO}, KP / GK, KP / GK, tm, tn);
-        if (r == 0) d[1] = ndiff(Y0, Y1, n);
-        t[r][3] = timeit(m2, g, NT, al, bl, EpiBiasRelu{Y1, b, M, CO}, KP / GK, KP / GK, tm, tn);
-        if (r == 0) d[2] = ndiff(Y0, Y1, n);
+    EpiBiasRelu e0{Y0, b, M, CO}, e1{Y1, b, M, CO};
+    auto run = [&](auto k, const EpiBiasRelu& e) {
+        return timeit(k, g, NT, al, bl, e, KP / GK, KP / GK, tm, tn);
+    };
+    std::vector<void*> ks = {
+        (void*)gemm_x6pp_kernel<5, FM, FN, WM, WN, AL, BL, EpiBiasRelu, 3, 2, 4, 0>,
+        (void*)gemm_x6pp_kernel<5, FM, FN, WM, WN, AL, BL, EpiBiasRelu, 4, 2, 4, 0>,
+        (void*)gemm_x6pp_kernel<5, FM, FN, WM, WN, AL, BL, EpiBiasRelu, 2, 3, 3, 0>,
+        (void*)gemm_x6pp_kernel<5, FM, FN, WM, WN, AL, BL, EpiBiasRelu, 3, 2, 2, 0>,
+        (void*)gemm_x6pp_kernel<5, FM, FN, WM, WN, AL, BL, EpiBiasRelu, 3, 1, 4, 0>,
+        (void*)gemm_x6pp_kernel<5, FM, FN, WM, WN, AL, BL, EpiBiasRelu, 3, 2, 4, 2>};
+    const char* names[] = {"V3W2L4", "V4W2L4", "V2W3L3", "V3W2L2", "V3W1L4", "V3W2L4R2"};
+    double tp[2];
+    for (int r = 0; r < 2; ++r) tp[r] = run(prod, e0);
+    printf("%-6s %3dx%3d product %7.3f %7.3f ms %6.1f TF/s\n", tag, BM, BN, tp[0], tp[1], tf(tp[1]));
+    for (size_t v = 0; v < ks.size(); ++v) {
+        using KT = decltype(prod);
+        const KT kv = reinterpret_cast<KT>(ks[v]);
+        const double a = run(kv, e1);
+        const size_t d = ndiff(Y0, Y1, n);
+        const double p = run(prod, e0), c = run(kv, e1);
+        printf("%-6s   %-9s %7.3f %7.3f ms %6.1f TF/s (x%.3f against the product's %7.3f %7.3f) "
+               "differ %zu\n", tag, names[v], a, c, tf(c), (tp[1] + p) / (a + c), tp[1], p, d);
+        tp[1] = p;
     }
-    printf("%-6s %3dx%3d product %7.3f %7.3f ms %6.1f | pp0 %7.3f %7.3f %6.1f | pp1 %7.3f %7.3f "
-           "%6.1f | pp2 %7.3f %7.3f %6.1f TF/s | differ %zu %zu %zu\n",
-           tag, BM, BN, t[0][0], t[1][0], tf(t[1][0]), t[0][1], t[1][1], tf(t[1][1]), t[0][2],
-           t[1][2], tf(t[1][2]), t[0][3], t[1][3], tf(t[1][3]), d[0], d[1], d[2]);
     fflush(stdout);
 }
 
@@ -132,25 +139,30 @@ static void wgrad(const char* tag, const float* dz, const Xs& Xx, float* S0, flo
     auto tf = [&](double t) { return flops / (t * 1e-3) / 1e12; };
     EpiSlabAcc e0{S0, CO, KP, (long)CO * KP, B0, 0}, e1{S1, CO, KP, (long)CO * KP, B1, 0};
     auto prod = gemm_x6_kernel<FM, FN, WM, WN, AL, BL, EpiSlabAcc>;
-    auto m0 = gemm_x6pp_kernel<0, FM, FN, WM, WN, AL, BL, EpiSlabAcc>;
-    auto m1 = gemm_x6pp_kernel<1, FM, FN, WM, WN, AL, BL, EpiSlabAcc>;
-    auto m2 = gemm_x6pp_kernel<2, FM, FN, WM, WN, AL, BL, EpiSlabAcc>;
     const size_t n = (size_t)Z * CO * KP, nb = (size_t)Z * CO;
-    double t[2][4];
-    size_t d[3];
-    for (int r = 0; r < 2; ++r) {
-        t[r][0] = timeit(prod, g, NT, al, bl, e0, ks, per, tm, tn);
-        t[r][1] = timeit(m0, g, NT, al, bl, e1, ks, per, tm, tn);
-        if (r == 0) d[0] = ndiff(S0, S1, n) + ndiff(B0, B1, nb);
-        t[r][2] = timeit(m1, g, NT, al, bl, e1, ks, per, tm, tn);
-        if (r == 0) d[1] = ndiff(S0, S1, n) + ndiff(B0, B1, nb);
-        t[r][3] = timeit(m2, g, NT, al, bl, e1, ks, per, tm, tn);
-        if (r == 0) d[2] = ndiff(S0, S1, n) + ndiff(B0, B1, nb);
+    auto run = [&](auto k, const EpiSlabAcc& e) { return timeit(k, g, NT, al, bl, e, ks, per, tm, tn); };
+    std::vector<void*> kv_ = {
+        (void*)gemm_x6pp_kernel<5, FM, FN, WM, WN, AL, BL, EpiSlabAcc, 3, 2, 4, 0>,
+        (void*)gemm_x6pp_kernel<5, FM, FN, WM, WN, AL, BL, EpiSlabAcc, 4, 2, 4, 0>,
+        (void*)gemm_x6pp_kernel<5, FM, FN, WM, WN, AL, BL, EpiSlabAcc, 2, 3, 3, 0>,
+        (void*)gemm_x6pp_kernel<5, FM, FN, WM, WN, AL, BL, EpiSlabAcc, 3, 2, 2, 0>,
+        (void*)gemm_x6pp_kernel<5, FM, FN, WM, WN, AL, BL, EpiSlabAcc, 3, 1, 4, 0>,
+        (void*)gemm_x6pp_kernel<5, FM, FN, WM, WN, AL, BL, EpiSlabAcc, 3, 2, 4, 2>};
+    const char* names[] = {"V3W2L4", "V4W2L4", "V2W3L3", "V3W2L2", "V3W1L4", "V3W2L4R2"};
+    double tp[2];
+    for (int r = 0; r < 2; ++r) tp[r] = run(prod, e0);
+    printf("%-6s %3dx%3d Z %4d product %7.3f %7.3f ms %6.1f TF/s\n", tag, BM, BN, Z, tp[0], tp[1],
+           tf(tp[1]));
+    for (size_t v = 0; v < kv_.size(); ++v) {
+        using KT = decltype(prod);
+        const KT kv = reinterpret_cast<KT>(kv_[v]);
+        const double a = run(kv, e1);
+        const size_t d = ndiff(S0, S1, n) + ndiff(B0, B1, nb);
+        const double p = run(prod, e0), c = run(kv, e1);
+        printf("%-6s   %-9s %7.3f %7.3f ms %6.1f TF/s (x%.3f against the product's %7.3f %7.3f) "
+               "differ %zu\n", tag, names[v], a, c, tf(c), (tp[1] + p) / (a + c), tp[1], p, d);
+        tp[1] = p;
     }
-    printf("%-6s %3dx%3d Z %4d product %7.3f %7.3f ms %6.1f | pp0 %7.3f %7.3f %6.1f | pp1 %7.3f "
-           "%7.3f %6.1f | pp2 %7.3f %7.3f %6.1f TF/s | differ %zu %zu %zu\n",
-           tag, BM, BN, Z, t[0][0], t[1][0], tf(t[1][0]), t[0][1], t[1][1], tf(t[1][1]), t[0][2],
-           t[1][2], tf(t[1][2]), t[0][3], t[1][3], tf(t[1][3]), d[0], d[1], d[2]);
     fflush(stdout);
 }
 
