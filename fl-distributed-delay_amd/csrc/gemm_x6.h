@@ -78,12 +78,16 @@ constexpr bool x6_fresh(bool kc) {
 }
 constexpr bool x6_fresh_bias() { return FLSIM_X6_FRESH >= 2; }
 
-// Main-loop schedule (-DFLSIM_X6_PP_V=V -DFLSIM_X6_PP_W=W -DFLSIM_X6_PP_L=L; V = 0: the
-// compiler's order): the
-// staging of the next k-step interleaved with the current k-step's MFMAs, per MFMA V VALU, an LDS
-// store every W MFMAs, a global load every L (tools/lab/pp_lab.hip)
+// Main-loop schedule of the k-contiguous GEMMs (both tiles KC: the staged forwards): the staging
+// of the next k-step interleaved with the current k-step's MFMAs by sched_group_barrier, per MFMA
+// V VALU, an LDS store every W MFMAs, a global load every L, in a branch-free loop body.  Lab
+// (tools/lab/pp_lab.hip, profiles/r05/lab_x6_interleave.txt): conv5 forward 1.06-1.10x, conv6
+// forward 1.01-1.04x, bit-identical; the k-major weight gradients lose up to 6 %, so they keep
+// the compiler's order, and so does linear1's fresh-accumulating forward (+3 % with it).  In the
+// product (A B A B, profiles/r05/ab/x6_interleave_kc.txt): conv6 forward 9.22-9.28 -> 9.01-9.07
+// ms, conv5 unchanged, the headline +0.2 %.  -DFLSIM_X6_PP_V=0 turns it off.
 #ifndef FLSIM_X6_PP_V
-#define FLSIM_X6_PP_V 0
+#define FLSIM_X6_PP_V 3
 #define FLSIM_X6_PP_W 2
 #define FLSIM_X6_PP_L 4
 #endif
@@ -308,10 +312,11 @@ gemm_x6_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, in
     // (conv6 9.76 against 8.93 ms, profiles/r04/r04h/lab_wg.txt); chosen per wave and taken on the
     // MFMA (AsumMfma) they run within 1.3 % of that, or faster (profiles/r04/r04i/lab_wg.txt)
     int cur = 0;
+    constexpr bool PP = X6_PP_V > 0 && AL::KC && BL::KC && !X6Fresh<EPI>::value;
     auto main_loop = [&](auto with_sum) {
         constexpr bool WS = decltype(with_sum)::value;
         for (int ks = ks0; ks < ks1; ++ks) {
-            if constexpr (X6_PP_V > 0) {
+            if constexpr (PP) {
                 // branch-free (one basic block, so the staging can be interleaved with the
                 // MFMAs, below): the last k-step stages into the buffer nobody reads again, and
                 // the loads past the split re-read its last k-step
@@ -355,7 +360,7 @@ gemm_x6_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, in
                                                bf[j].x2);
                 }
             }
-            if constexpr (X6_PP_V > 0) {
+            if constexpr (PP) {
                 // per MFMA X6_PP_V VALU (the staging's split and address arithmetic), an LDS
                 // store every X6_PP_W MFMAs and a global load every X6_PP_L
 #pragma unroll
