@@ -83,9 +83,11 @@ constexpr bool x6_fresh_bias() { return FLSIM_X6_FRESH >= 2; }
 // V VALU, an LDS store every W MFMAs, a global load every L, in a branch-free loop body.  Lab
 // (tools/lab/pp_lab.hip, profiles/r05/lab_x6_interleave.txt): conv5 forward 1.06-1.10x, conv6
 // forward 1.01-1.04x, bit-identical; the k-major weight gradients lose up to 6 %, so they keep
-// the compiler's order, and so does linear1's fresh-accumulating forward (+3 % with it).  In the
-// product (A B A B, profiles/r05/ab/x6_interleave_kc.txt): conv6 forward 9.22-9.28 -> 9.01-9.07
-// ms, conv5 unchanged, the headline +0.2 %.  -DFLSIM_X6_PP_V=0 turns it off.
+// the compiler's order, and so do the GEMMs that split an fp32 operand while staging it (linear1's
+// forward +3 %, VGG-11's forwards: configs[4] 1369 -> 1346 worker-steps/s with it,
+// profiles/r05/ab/vgg_x6_interleave.txt).  So it runs where both operands arrive split, PN1's
+// conv5 / conv6 forwards (A B A B, profiles/r05/ab/x6_interleave_kc.txt): conv6 forward
+// 9.22-9.28 -> 9.01-9.07 ms, conv5 unchanged, the headline +0.2 %.  -DFLSIM_X6_PP_V=0: off.
 #ifndef FLSIM_X6_PP_V
 #define FLSIM_X6_PP_V 3
 #define FLSIM_X6_PP_W 2
@@ -312,7 +314,9 @@ gemm_x6_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, in
     // (conv6 9.76 against 8.93 ms, profiles/r04/r04h/lab_wg.txt); chosen per wave and taken on the
     // MFMA (AsumMfma) they run within 1.3 % of that, or faster (profiles/r04/r04i/lab_wg.txt)
     int cur = 0;
-    constexpr bool PP = X6_PP_V > 0 && AL::KC && BL::KC && !X6Fresh<EPI>::value;
+    constexpr bool PP = X6_PP_V > 0 && AL::KC && BL::KC && !X6Fresh<EPI>::value &&
+                        std::is_same_v<typename AL::Unit, XsUnit> &&
+                        std::is_same_v<typename BL::Unit, XsUnit>;
     auto main_loop = [&](auto with_sum) {
         constexpr bool WS = decltype(with_sum)::value;
         for (int ks = ks0; ks < ks1; ++ks) {

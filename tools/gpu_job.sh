@@ -7,6 +7,7 @@
 #   bench             the default bench line (with its CPU baseline) + tools/bench_summary.py
 #   benchq            the default bench line without the CPU baseline
 #   ab:<lib>          bench line of an alternative libflsim.so (FLSIM_LIB=<lib>) beside benchq
+#   abvgg:<lib>       configs[4] (vgg11, n = 4096, d = 1000) with an alternative libflsim.so, B A B A
 #   abenv:<VAR=VAL>   bench line with one environment setting beside benchq (E1 A1 E2 A2)
 #   c1abenv:<VAR=VAL> the same on configs[1] (n = 10, d = 50, the warm start)
 #   trace             rocprofv3 --kernel-trace --stats of a short bench (kernel_stats.csv)
@@ -86,6 +87,11 @@ for STEP in "$@"; do
             || { echo "warm start failed"; exit 1; }
         BENCH_ARGS="--n_workers 10 --delay 50 --model_file $OUT/warm_start.pt --steps 200 --warmup 10"
         bench_line c1E1 $KV; bench_line c1A1; bench_line c1E2 $KV; bench_line c1A2
+        BENCH_ARGS="" ;;
+    abvgg:*)
+        LIB=${STEP#abvgg:}
+        BENCH_ARGS="--model vgg11 --n_workers 4096 --delay 1000 --steps 4 --warmup 1"
+        bench_line vB1 FLSIM_LIB=$LIB; bench_line vA1; bench_line vB2 FLSIM_LIB=$LIB; bench_line vA2
         BENCH_ARGS="" ;;
     abenv:*)
         KV=${STEP#abenv:}
