@@ -17,6 +17,12 @@
 
 namespace flsim {
 
+// Scheduling fences around each k-step's MFMAs (measurement override -DFLSIM_DIRECT_FENCES=<0|1>)
+#ifndef FLSIM_DIRECT_FENCES
+#define FLSIM_DIRECT_FENCES 1
+#endif
+constexpr bool DIRECT_FENCES = FLSIM_DIRECT_FENCES;
+
 // A operand of a 3x3 / stride-1 convolution (forward, or data gradient as a valid convolution of
 // dZ with the flipped weights) loaded per wave into MFMA fragments.  Same K order and the same
 // geometry options (WIN: pool-window row order; OHX: explicit output size) as Im2colKC with
@@ -206,7 +212,7 @@ gemm_direct_kernel(AD ad, BL bl, EPI epi, int ksteps, int tiles_m, int tiles_n) 
             if (kk > 0) bl.store(Bn + (kk - 1) * BFL, rb);
             bl.load(kn + kk, rb);
             ad.load(ks + DEPTH, ra[(kk + DEPTH) % R]);
-            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (DIRECT_FENCES) __builtin_amdgcn_sched_barrier(0);
             f32x4 bf[FN];
 #pragma unroll
             for (int j = 0; j < FN; ++j) bf[j] = read_frag<true, BN>(Bs + kk * BFL, 16 * j, lane);
@@ -217,7 +223,7 @@ gemm_direct_kernel(AD ad, BL bl, EPI epi, int ksteps, int tiles_m, int tiles_n) 
 #pragma unroll
                     for (int j = 0; j < FN; ++j)
                         acc[i][j] = mfma16(ra[kk % R][i][kq], bf[j][kq], acc[i][j]);
-            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (DIRECT_FENCES) __builtin_amdgcn_sched_barrier(0);
         }
         bl.store(Bn + (KB - 1) * BFL, rb);
         __syncthreads();

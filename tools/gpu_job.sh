@@ -188,6 +188,11 @@ for STEP in "$@"; do
         python3 tools/trace_gaps.py $D 0.5 > $OUT/facade_gaps.txt && head -30 $OUT/facade_gaps.txt ;;
     configs)
         bash tools/gpu_configs_all.sh $TAG || exit 1 ;;
+    labenv:*)      # labenv:<VAR=VAL>:<bin>[:<arg>]
+        SPEC=${STEP#labenv:}; KV=${SPEC%%:*}; SPEC=${SPEC#*:}; BIN=${SPEC%%:*}; ARG=${SPEC#$BIN}; ARG=${ARG#:}
+        env $KV timeout -k 10 300 tools/lab/$BIN $ARG > $OUT/lab_$BIN.txt 2>&1 \
+            || { echo "lab $BIN failed $?"; tail -5 $OUT/lab_$BIN.txt; exit 1; }
+        cat $OUT/lab_$BIN.txt ;;
     lab:*)
         SPEC=${STEP#lab:}; BIN=${SPEC%%:*}; ARG=${SPEC#$BIN}; ARG=${ARG#:}
         timeout -k 10 300 tools/lab/$BIN $ARG > $OUT/lab_$BIN${ARG:+_$ARG}.txt 2>&1 \

@@ -1,86 +1,18 @@
-// Direct-A split-bf16 GEMM for the convolutions' forward and data-gradient passes (gfx950).
-//
-// The operands arrive in the split form (split.h): every activation / dZ tensor is stored by its
-// producer as HM + L parts, and the packed weights likewise, once per epoch.  So nothing is split
-// in the GEMM.  As in gemm_direct.h, each wave owns 16*FM rows of the block tile and loads its A
-// fragments straight from memory into registers, DEPTH k-steps ahead: lane l of the 16x16x32 bf16
-// MFMA holds row (l & 15), k slots 8(l >> 4) .. +7 = the [h|m] unit of four consecutive input
-// channels of one pixel (one 16-B load at the fp32 tensor's own byte offset), and [h|l] takes two
-// dwords of the L unit (one 8-B load).  No LDS and no barrier for A.  Only B (the block's BN packed
-// weight columns) goes through LDS, KB k-steps per stage, planes [h|m] and [l|h] ([m|h] too when
-// NPLB = 3), each laid out like the fp32 KC tile.
-//
-// Per accumulator the MFMA sequence (k ascending; per k-step A[h|l] x B[l|h], A[h|m] x B[m|h],
-// A[h|m] x B[h|m]) is gemm_x6_kernel's, and the parts are the same RNE split, so the results are
-// bit-identical to gemm_x6_kernel over the fp32 operands.
+// Lab variant of gemm_dx6_kernel (development tool, not part of libflsim.so): the direct-A
+// split-bf16 forward with its per-k-step scheduling fences replaced.  MODE 0: the product's
+// fences; 1: no fences (the compiler's order); 2: sched_group_barrier interleave (per MFMA: an
+// LDS read every 2nd, a global load every 4th, an LDS store every 4th, one VALU); 3: LDS reads in
+// pairs every 3rd MFMA, loads / stores every 6th, two VALU.  Fresh accumulation off (the
+// product's default level).
 #pragma once
-#include "gemm_direct.h"
-#include "gemm_x6.h"
+#include "gemm_dx6.h"
 
 namespace flsim {
 
-// Scheduling fences around each k-step's MFMAs (measurement override -DFLSIM_DX6_FENCES=<0|1>)
-#ifndef FLSIM_DX6_FENCES
-#define FLSIM_DX6_FENCES 1
-#endif
-constexpr bool DX6_FENCES = FLSIM_DX6_FENCES;
-
-// B staging for gemm_dx6_kernel: rows [n0, n0 + ROWS) of a row-major [NR][ld] matrix in the split
-// form, one 16-deep k-step per load / store.  Per k-step the LDS holds NPL planes of KCTile<ROWS>
-// (plane 0 [h|m], plane 1 [l|h], plane 2 [m|h]) and one spare 16-B chunk that takes the stores of
-// units past the tile (rows >= NR read as zeros through the buffer bound).
-template <int TR, int NT, int NPL>
-struct RowsKCStageXs {
-    using Unit = XsUnit;
-    static constexpr int ROWS = TR;
-    static constexpr bool KC = true;
-    static constexpr int TOTAL = ROWS * 4;
-    static constexpr int UNITS = (TOTAL + NT - 1) / NT;
-    static constexpr int PLANE = KCTile<ROWS>::FLOATS;
-    static constexpr int SPARE = NPL * PLANE;
-    static constexpr int FLOATS = NPL * PLANE + 4;
-    static_assert(NPL == 2 || NPL == 3, "");
-    const float* P;
-    const float* PL;
-    long ld;
-    int NR;
-    unsigned rowb[UNITS];
-    int dst[UNITS];            // LDS float offset of the unit in plane 0, -1 for a surplus unit
-    XsSrc buf;
-    __device__ void setup(int r0, int tid) {
-        buf.init(P, PL, (unsigned long)NR * ld * 4);
-#pragma unroll
-        for (int j = 0; j < UNITS; ++j) {
-            const int u0 = tid + j * NT;
-            const bool real = u0 < TOTAL;
-            const int u = real ? u0 : u0 % TOTAL;
-            const int r = u >> 2, q = u & 3;
-            rowb[j] = r0 + r < NR ? (unsigned)(((long)(r0 + r) * ld + 4 * q) * 4) : BUF_OOB;
-            dst[j] = real ? KCTile<ROWS>::chunk_off(r, q) : -1;
-        }
-    }
-    __device__ void load(int ks, Unit (&r)[UNITS]) const {
-#pragma unroll
-        for (int j = 0; j < UNITS; ++j)
-            r[j] = buf.ld(rowb[j] == BUF_OOB ? BUF_OOB : rowb[j] + (unsigned)(ks * GK * 4));
-    }
-    __device__ void store(float* lds, const Unit (&r)[UNITS]) const {
-#pragma unroll
-        for (int j = 0; j < UNITS; ++j) {
-            const bool real = TOTAL % NT == 0 || dst[j] >= 0;
-            *reinterpret_cast<f32x4*>(lds + (real ? dst[j] : SPARE)) = r[j].hm;
-            *reinterpret_cast<f32x4*>(lds + (real ? dst[j] + PLANE : SPARE)) = xs_lh(r[j]);
-            if constexpr (NPL == 3)
-                *reinterpret_cast<f32x4*>(lds + (real ? dst[j] + 2 * PLANE : SPARE)) =
-                    f32x4{r[j].hm.z, r[j].hm.w, r[j].hm.x, r[j].hm.y};
-        }
-    }
-};
-
 // Block = WAVES waves stacked along M (each 16*FM rows) x all BN = 16*FN columns of its n-tile.
-template <int FM, int FN, int WAVES, int KB, int DEPTH, class AD, class BL, class EPI>
+template <int MODE, int FM, int FN, int WAVES, int KB, int DEPTH, class AD, class BL, class EPI>
 __global__ void __launch_bounds__(64 * WAVES)
-gemm_dx6_kernel(AD ad, BL bl, EPI epi, int ksteps, int tiles_m, int tiles_n) {
+gemm_dx6pp_kernel(AD ad, BL bl, EPI epi, int ksteps, int tiles_m, int tiles_n) {
     constexpr int BM = 16 * FM * WAVES;
     constexpr int BN = 16 * FN;
     static_assert(BL::ROWS == BN && BL::KC, "B loader: k-contiguous tile of BN rows");
@@ -147,7 +79,7 @@ gemm_dx6_kernel(AD ad, BL bl, EPI epi, int ksteps, int tiles_m, int tiles_n) {
             if (kk > 0) bl.store(Bn + (kk - 1) * BFL, rb);
             bl.load(kn + kk, rb);
             ad.load(ks + DEPTH, ra[(kk + DEPTH) % R]);
-            if constexpr (DX6_FENCES) __builtin_amdgcn_sched_barrier(0);
+            if constexpr (MODE == 0) __builtin_amdgcn_sched_barrier(0);
             const float* Bk = Bs + kk * BFL;
             f32x4 a0[FM], a1[FM];
 #pragma unroll
@@ -166,10 +98,30 @@ gemm_dx6_kernel(AD ad, BL bl, EPI epi, int ksteps, int tiles_m, int tiles_n) {
                     x1 = f32x4{x0.z, x0.w, x0.x, x0.y};
 #pragma unroll
                 for (int i = 0; i < FM; ++i) {
-                    acc[i][j] = x6_step<x6_fresh(true)>(acc[i][j], a0[i], a1[i], x0, x1, x2);
+                    acc[i][j] = x6_step<false>(acc[i][j], a0[i], a1[i], x0, x1, x2);
                 }
             }
-            if constexpr (DX6_FENCES) __builtin_amdgcn_sched_barrier(0);
+            if constexpr (MODE == 2) {
+#pragma unroll
+                for (int n = 0; n < 3 * FM * FN; ++n) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    if (n % 2 == 0) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    if (n % 4 == 1) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+                    if (n % 4 == 3) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+                }
+            }
+            if constexpr (MODE == 3) {
+#pragma unroll
+                for (int n = 0; n < 3 * FM * FN; ++n) {
+                    if (n % 3 == 0) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    if (n % 6 == 1) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+                    if (n % 6 == 4) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+                }
+            }
+            if constexpr (MODE == 0) __builtin_amdgcn_sched_barrier(0);
         }
         bl.store(Bn + (KB - 1) * BFL, rb);
         __syncthreads();

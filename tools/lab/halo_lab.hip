@@ -8,6 +8,7 @@
 #include <string>
 
 #include "gemm_hx6.h"
+#include "gemm_dx6pp.h"
 #include "lab_common.h"
 
 static __global__ void k_to_xs(const float* x, float* hm, float* l, long units) {
@@ -140,6 +141,25 @@ static void shape(const char* tag, const Xs& Xsm, const Xs& Wx, const float* b, 
     }
     const size_t d = ndiff(Y0, Y1, (size_t)M * CO);
     printf("[waves per EU >= %d] ", MINW);
+    if (getenv("LAB_DX6PP") && MINW == 1) {       // the direct kernel's scheduling variants
+        auto k1 = gemm_dx6pp_kernel<1, FM, FN, WAVES, KB, 2, AD, BD, EpiBiasRelu>;
+        auto k2 = gemm_dx6pp_kernel<2, FM, FN, WAVES, KB, 2, AD, BD, EpiBiasRelu>;
+        auto k3 = gemm_dx6pp_kernel<3, FM, FN, WAVES, KB, 2, AD, BD, EpiBiasRelu>;
+        double u[2][4];
+        size_t dd[3];
+        for (int r = 0; r < 2; ++r) {
+            u[r][0] = timeit(kd, g, NT, ad, bd, EpiBiasRelu{Y0, b, M, CO}, KP / GK, tm, tn);
+            u[r][1] = timeit(k1, g, NT, ad, bd, EpiBiasRelu{Y1, b, M, CO}, KP / GK, tm, tn);
+            if (r == 0) dd[0] = ndiff(Y0, Y1, (size_t)M * CO);
+            u[r][2] = timeit(k2, g, NT, ad, bd, EpiBiasRelu{Y1, b, M, CO}, KP / GK, tm, tn);
+            if (r == 0) dd[1] = ndiff(Y0, Y1, (size_t)M * CO);
+            u[r][3] = timeit(k3, g, NT, ad, bd, EpiBiasRelu{Y1, b, M, CO}, KP / GK, tm, tn);
+            if (r == 0) dd[2] = ndiff(Y0, Y1, (size_t)M * CO);
+        }
+        printf("\n%-6s dx6 product %7.3f %7.3f | no fences %7.3f %7.3f | interleave2 %7.3f %7.3f | "
+               "interleave3 %7.3f %7.3f ms | differ %zu %zu %zu\n", tag, u[0][0], u[1][0], u[0][1],
+               u[1][1], u[0][2], u[1][2], u[0][3], u[1][3], dd[0], dd[1], dd[2]);
+    }
     printf("%-6s %3dx%3d %d waves  product dx6 %7.3f %7.3f ms %6.1f TF/s | halo (patch %d rows, "
            "%.1f KB) %7.3f %7.3f ms %6.1f TF/s (x%.3f) | differ %zu of %zu\n",
            tag, BM, BN, WAVES, t[0][0], t[1][0], tf(t[1][0]), need,
