@@ -142,13 +142,13 @@ static void wgrad(const char* tag, const float* dz, const Xs& Xx, float* S0, flo
     const size_t n = (size_t)Z * CO * KP, nb = (size_t)Z * CO;
     auto run = [&](auto k, const EpiSlabAcc& e) { return timeit(k, g, NT, al, bl, e, ks, per, tm, tn); };
     std::vector<void*> kv_ = {
-        (void*)gemm_x6pp_kernel<5, FM, FN, WM, WN, AL, BL, EpiSlabAcc, 3, 2, 4, 0>,
-        (void*)gemm_x6pp_kernel<5, FM, FN, WM, WN, AL, BL, EpiSlabAcc, 4, 2, 4, 0>,
+        (void*)gemm_x6pp_kernel<3, FM, FN, WM, WN, AL, BL, EpiSlabAcc, 3, 2, 4, 0>,
+        (void*)gemm_x6pp_kernel<5, FM, FN, WM, WN, AL, BL, EpiSlabAcc, 1, 3, 4, 0>,
         (void*)gemm_x6pp_kernel<5, FM, FN, WM, WN, AL, BL, EpiSlabAcc, 2, 3, 3, 0>,
-        (void*)gemm_x6pp_kernel<5, FM, FN, WM, WN, AL, BL, EpiSlabAcc, 3, 2, 2, 0>,
-        (void*)gemm_x6pp_kernel<5, FM, FN, WM, WN, AL, BL, EpiSlabAcc, 3, 1, 4, 0>,
-        (void*)gemm_x6pp_kernel<5, FM, FN, WM, WN, AL, BL, EpiSlabAcc, 3, 2, 4, 2>};
-    const char* names[] = {"V3W2L4", "V4W2L4", "V2W3L3", "V3W2L2", "V3W1L4", "V3W2L4R2"};
+        (void*)gemm_x6pp_kernel<5, FM, FN, WM, WN, AL, BL, EpiSlabAcc, 2, 4, 6, 0>,
+        (void*)gemm_x6pp_kernel<5, FM, FN, WM, WN, AL, BL, EpiSlabAcc, 6, 3, 4, 0>,
+        (void*)gemm_x6pp_kernel<5, FM, FN, WM, WN, AL, BL, EpiSlabAcc, 2, 3, 3, 3>};
+    const char* names[] = {"branchfree", "V1W3L4", "V2W3L3", "V2W4L6", "V6W3L4", "V2W3L3R3"};
     double tp[2];
     for (int r = 0; r < 2; ++r) tp[r] = run(prod, e0);
     printf("%-6s %3dx%3d Z %4d product %7.3f %7.3f ms %6.1f TF/s\n", tag, BM, BN, Z, tp[0], tp[1],
