@@ -94,6 +94,10 @@ constexpr bool x6_fresh_bias() { return FLSIM_X6_FRESH >= 2; }
 #define FLSIM_X6_PP_L 4
 #endif
 constexpr int X6_PP_V = FLSIM_X6_PP_V, X6_PP_W = FLSIM_X6_PP_W, X6_PP_L = FLSIM_X6_PP_L;
+#ifndef FLSIM_X6_PP_KM
+#define FLSIM_X6_PP_KM 0
+#endif
+constexpr bool X6_PP_KM = FLSIM_X6_PP_KM;
 
 typedef short s16x4v __attribute__((ext_vector_type(4)));
 
@@ -314,9 +318,16 @@ gemm_x6_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, in
     // (conv6 9.76 against 8.93 ms, profiles/r04/r04h/lab_wg.txt); chosen per wave and taken on the
     // MFMA (AsumMfma) they run within 1.3 % of that, or faster (profiles/r04/r04i/lab_wg.txt)
     int cur = 0;
-    constexpr bool PP = X6_PP_V > 0 && AL::KC && BL::KC && !X6Fresh<EPI>::value &&
-                        std::is_same_v<typename AL::Unit, XsUnit> &&
-                        std::is_same_v<typename BL::Unit, XsUnit>;
+    constexpr bool PP_KC = X6_PP_V > 0 && AL::KC && BL::KC && !X6Fresh<EPI>::value &&
+                           std::is_same_v<typename AL::Unit, XsUnit> &&
+                           std::is_same_v<typename BL::Unit, XsUnit>;
+    // (measurement, -DFLSIM_X6_PP_KM=1) the 192-row k-major weight-gradient tiles of PN1's conv5 /
+    // conv6 interleaved too, two VALU per MFMA, a store and a load every third: +2.7 % / +0.8 % in
+    // the lab (profiles/r05/lab_x6_interleave_wgrad.txt) but 5-6 % slower in the product
+    // (profiles/r05/ab/x6_interleave_km.txt), so off
+    constexpr bool PP_KM = X6_PP_KM && !AL::KC && !BL::KC && FM == 6 && WAVES_M * WAVES_N == 4;
+    constexpr bool PP = PP_KC || PP_KM;
+    constexpr int PV = PP_KM ? 2 : X6_PP_V, PW = PP_KM ? 3 : X6_PP_W, PL = PP_KM ? 3 : X6_PP_L;
     auto main_loop = [&](auto with_sum) {
         constexpr bool WS = decltype(with_sum)::value;
         for (int ks = ks0; ks < ks1; ++ks) {
@@ -370,10 +381,9 @@ gemm_x6_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, in
 #pragma unroll
                 for (int n = 0; n < 3 * FM * FN; ++n) {
                     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x002, X6_PP_V, 0);
-                    if (n % X6_PP_W == 0) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
-                    if (n % X6_PP_L == 1 % X6_PP_L)
-                        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, PV, 0);
+                    if (n % PW == 0) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+                    if (n % PL == 1 % PL) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
                 }
             }
             __syncthreads();
