@@ -197,6 +197,34 @@ def test_chunk_of_workers_sums_gradients(pool):
     assert _rel_l2(S.cpu().numpy().astype(np.float64), g64) <= 1e-2
 
 
+def test_small_chunk_tiles_bit_identical(pool):
+    """Chunks of at most small_chunk_samples() (256) samples run the GEMMs on half-height tiles
+    (net_kernels.h): the k order per output is the large tiles', so the forward -- and
+    with it every worker's loss -- must be bit-identical.  Two workers (256 samples, small tiles)
+    against the same two inside a three-worker chunk (384 samples, large tiles)."""
+    import torch as T
+    from flsim.data import DevicePool
+    from flsim.engine import PN1Engine, worker_table
+    from oracle import model_ref as MR
+    sim = MR.OracleSim(4, delay=2, pool=pool)
+    items = [(3, 0, 1), (3, 2, 3), (3, 3, 0)]
+    eng = PN1Engine(DEV, chunk_workers=3)
+    dpool = DevicePool(DEV, 0, pool)
+    theta = T.from_numpy(sim.theta.copy()).to(DEV)
+    eng.begin_epoch(theta)
+    small = T.zeros(2, device=DEV)
+    large = T.zeros(3, device=DEV)
+    eng.run_chunk(theta, dpool, worker_table(items[:2], DEV), 2, 4, 0, True, small)
+    eng.run_chunk(theta, dpool, worker_table(items, DEV), 3, 4, 0, True, large)
+    S = T.zeros(eng.P, device=DEV)
+    eng.end_epoch(S)
+    T.cuda.synchronize()
+    a = small.cpu().numpy()
+    b = large[:2].cpu().numpy()
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), (a, b)
+    assert np.all(np.isfinite(S.cpu().numpy()))
+
+
 def test_conv1_wgrad_fused_into_conv2_dgrad(pool, monkeypatch):
     """FLSIM_C1_FUSE=1 (c1fuse.h, off by default: measured slower): conv1's weight and
     bias gradients computed inside conv2's data-gradient launch.  Two chunks (the second
