@@ -138,7 +138,26 @@ class _ModelContext:
             p.data = view                       # parameters alias the flat buffer
         self.m = torch.zeros_like(self.theta)
         self.v = torch.zeros_like(self.theta)
-        self.engine = self.engine_cls(dev, chunk_workers=1)
+        self.params = list(model.parameters())
+        # Deferred backward (PerformantNet1): every fwd_bkwd call of an epoch runs on theta_t, so
+        # a call runs only its forward + loss (what agents.py:40 returns) into the next rows of a
+        # chunk workspace, and the backward of up to `defer_rows` samples of calls runs as ONE
+        # worker-batched pass (flsim_pn1_bwd_rows) when the chunk is full or the gradient is
+        # needed (a .grad view is touched, update_model, evaluation, a parameter change).
+        # FLSIM_FACADE_CHUNK = workers (128-sample groups) per deferred backward at most; 0: a
+        # backward per call.  The chunk workspace starts at 8 workers and grows between epochs to
+        # what an epoch used (so a 4-worker loop holds 1.6 GB, a 1024-worker one 2 x 26 GB).
+        cw = int(os.environ.get("FLSIM_FACADE_CHUNK", "128"))
+        self.defer_max = 0
+        if self.engine_cls.PREFIX == "pn1" and cw > 0:
+            self.defer_max = min(cw, MAX_BATCH // 128) * 128
+        self.engine = self.engine_cls(dev, chunk_workers=min(self.defer_max // 128, 8) or 1)
+        self.defer_rows = self.engine.max_samples if self.defer_max else 0
+        self.epoch_rows = 0          # rows forwarded this epoch
+        self.pending = 0             # rows forwarded whose backward is not queued yet
+        self.pending_dropout = None  # their dropout flag (one per backward pass)
+        self.theta_run = None        # the theta this epoch's packed weights / rows were run with
+        self.version = None          # parameter versions when theta_run was taken
         self.bn_stats = None
         self.bns = []
         if self.engine.STATS_PER_WORKER:
@@ -159,6 +178,9 @@ class _ModelContext:
         self.loss_buf = torch.zeros(64, device=dev)
         self.stager = ProgramStager(dev)
         self.users = {}          # Worker.index -> id(Worker) of this epoch's fwd_bkwd calls
+        self.views = None        # the epoch's .grad views of G
+        self.rec_table = None    # device WorkerRec rows (t, i) of epoch rec_t
+        self.rec_t = -1
 
     def _alias_buffers(self, model):
         """BatchNorm running buffers become views of the engine's device buffer (loaded from the
@@ -194,8 +216,24 @@ class _ModelContext:
                 self.engine.running = old.running
                 self.engine.num_batches_tracked = old.num_batches_tracked
             self.packed = False
+            if self.defer_rows:
+                self.defer_rows = self.engine.max_samples
+                self.defer_max = max(self.defer_max, self.defer_rows)
         if cw > self.loss_buf.numel():
             self.loss_buf = torch.zeros(cw, device=self.device)
+
+    def worker_rec(self, index, groups):
+        """Device WorkerRec rows (epoch t, index + b * 2^20) of a call: one-group calls slice a
+        table of the epoch's records uploaded once (grown by doubling), not one upload each."""
+        if groups != 1:
+            return worker_table([(self.t, index + b * GROUP_KEY_STRIDE, 0)
+                                 for b in range(groups)], self.device)
+        tab = self.rec_table
+        if tab is None or self.rec_t != self.t or index >= tab.shape[0]:
+            size = max(64, 2 * (index + 1), 0 if tab is None else tab.shape[0])
+            tab = worker_table([(self.t, i, 0) for i in range(size)], self.device)
+            self.rec_table, self.rec_t = tab, self.t
+        return tab[index:index + 1]
 
     def claim(self, worker):
         """Dropout keys are (epoch, Worker.index): two different Worker objects computing with
@@ -208,11 +246,43 @@ class _ModelContext:
                              "indices restart at 0 when a Central is built: build the Central "
                              "first, then the workers, as main.py:110-113 does)")
 
+    def _param_version(self):
+        return sum(p._version for p in self.params)
+
+    def prepare_rows(self):
+        """theta_run for this call's forward rows.  The first call of an epoch packs theta_t
+        (begin_epoch).  A parameter written in place since then (load_state_dict, an in-place op
+        under no_grad) is seen by the reference's next forward: the pending rows' backward runs
+        first with the theta their forwards used, the epoch's gradient so far is carried, and
+        the new theta is packed."""
+        v = self._param_version()
+        if self.packed and v == self.version:
+            return self.theta_run
+        if self.theta_run is None:
+            self.theta_run = torch.empty_like(self.theta)
+        if self.packed:
+            self.flush()
+            self.carry = self.G.clone()
+        self.theta_run.copy_(self.theta)
+        self.engine.begin_epoch(self.theta_run)
+        self.packed = True
+        self.version = v
+        return self.theta_run
+
+    def flush_backward(self):
+        """Queue the backward of the pending forward rows (one worker-batched pass)."""
+        if self.pending:
+            self.engine.backward_rows(self.theta_run, self.pending, self.pending_dropout,
+                                      self.slot)
+            self.slot ^= 1               # the next rows go to the other workspace
+            self.pending = 0
+
     def flush(self, touched=False):
         """G = the epoch's gradient so far: the slab reduction fwd_bkwd left pending.  touched:
         user code read or wrote a .grad view, so from now on G (not the slabs) is the epoch's
         gradient for update_model (an in-place change of a .grad is seen)."""
         self.touched = self.touched or touched
+        self.flush_backward()
         if not self.dirty:
             return
         self.dirty = False
@@ -221,9 +291,18 @@ class _ModelContext:
             self.G.add_(self.carry)
 
     def new_epoch(self):
+        if self.defer_rows and self.defer_rows < min(self.epoch_rows, self.defer_max):
+            # the last epoch's calls did not fit one deferred chunk: a larger workspace (the
+            # epoch's gradient is consumed, nothing is pending)
+            cw = -(-min(self.epoch_rows, self.defer_max) // 128)
+            self.engine = self.engine_cls(self.device, chunk_workers=cw)
+            self.defer_rows = self.engine.max_samples
+            self.slot = 0
+        self.epoch_rows = 0
         self.t += 1
         self.users = {}
         self.G = None
+        self.views = None
         self.dirty = False
         self.touched = False
         self.carry = None
@@ -316,6 +395,7 @@ class Central:
                 not ctx.touched and hasattr(eng, "server_step"):
             # fused: this epoch's slabs -> S_t (also written into G, which the FIFO entries of
             # main.py:156,161 alias) -> rule() + Adam, one pass
+            ctx.flush_backward()
             eng.server_step(ctx.G, r, ctx.theta, ctx.m, ctx.v, ctx.step, **hp)
             ctx.dirty = False
         else:
@@ -362,14 +442,19 @@ class Worker:
         ctx.ensure_capacity(n)
         eng = ctx.engine
         theta = ctx.theta
-        if not ctx.packed:
+        defer = ctx.defer_rows and ctx.bn_stats is None
+        if defer:
+            theta = ctx.prepare_rows()
+        elif not ctx.packed:
             eng.begin_epoch(theta)
             ctx.packed = True
         if ctx.G is None:
             ctx.G = torch.zeros(padded(ctx.P), device=ctx.device)
+            # the epoch's .grad views: every call returns the same tensors (agents.py:37-39 hands
+            # out the parameters' own .grad, the same objects for every worker of the epoch)
+            ctx.views = _lazy_views(ctx.G[:ctx.P], ctx.shapes, ctx)
         groups = -(-n // 128)
-        recs = [(ctx.t, self.index + b * GROUP_KEY_STRIDE, 0) for b in range(groups)]
-        wt = worker_table(recs, ctx.device)
+        wt = ctx.worker_rec(self.index, groups)
         lb = ctx.loss_buf[:groups]
         kw = {}
         if ctx.bn_stats is not None:
@@ -378,7 +463,20 @@ class Worker:
                                           "on 128-sample batches (main.py:43-44, 132)")
             kw = {"stats_out": ctx.bn_stats}
         x = inp.to(ctx.device, torch.float32)
-        if ctx.bn_stats is None and getattr(eng, "PIPELINE", False) and ctx.pipeline:
+        if defer:
+            # this call's forward + loss into the chunk's next rows; the backward waits for the
+            # chunk (one batched pass, flush_backward)
+            training = bool(self.model.training)
+            rows = groups * 128
+            if ctx.pending and (ctx.pending + rows > ctx.defer_rows or
+                                training != ctx.pending_dropout):
+                ctx.flush_backward()
+            eng.forward_rows(theta, x, outp.to(ctx.device), wt, ctx.seed, training, lb,
+                             ctx.pending, ctx.slot)
+            ctx.pending += rows
+            ctx.epoch_rows += rows
+            ctx.pending_dropout = training
+        elif ctx.bn_stats is None and getattr(eng, "PIPELINE", False) and ctx.pipeline:
             # the backward overlaps the next call's forward (the loss below needs only this
             # forward); the .grad views join it on first use, update_model in its server step
             ctx.slot ^= 1
@@ -392,11 +490,13 @@ class Worker:
             for mod in ctx.bns:
                 mod.num_batches_tracked.fill_(eng.num_batches_tracked)
         ctx.dirty = True                         # G = the running sum on first read (flush)
-        grads = _lazy_views(ctx.G[:ctx.P], ctx.shapes, ctx)
-        for p, gv in zip(self.model.parameters(), grads):
-            p.grad = gv                          # agents.py:35: accumulated in place
+        grads = ctx.views
+        for p, gv in zip(ctx.params, grads):
+            if p.grad is not gv:
+                p.grad = gv                      # agents.py:35: accumulated in place
         # CrossEntropyLoss(mean) over the n samples: group sums / n (padding contributes 0)
-        lossval = np.float32(float(lb.double().sum().cpu()) * 128.0 / n)
+        tot = lb.item() if groups == 1 else float(lb.double().sum().cpu())
+        lossval = np.float32(tot * 128.0 / n)
         return list(grads), np.asarray(lossval, np.float32)
 
 

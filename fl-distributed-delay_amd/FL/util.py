@@ -51,6 +51,7 @@ def print_test_accuracy(model, testloader):
         raise NotImplementedError("print_test_accuracy on the HIP engine evaluates in eval mode: "
                                   "call model.eval() first (main.py:190)")
     ctx = _context(model)
+    ctx.flush_backward()       # the evaluation reuses the workspace of deferred fwd_bkwd rows
     correct = 0
     total = 0
     with torch.no_grad():

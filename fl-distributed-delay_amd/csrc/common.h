@@ -2,8 +2,22 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #define FLSIM_WAVE 64
+
+// ---- measurement switches ------------------------------------------------------------------
+// The A/B switches behind the measurements DESIGN.md cites -- compile-time -DFLSIM_<X> overrides
+// and the FLSIM_<X> environment overrides read through lab_env() -- act only in a lab build
+// (make LAB=1 -> -DFLSIM_LAB).  The product build compiles their measured defaults, so its
+// behaviour depends on no environment variable (FLSIM_DEBUG_BWD_STOP, the tests' stop of the
+// backward pass after a given layer, excepted).
+#if !defined(FLSIM_LAB) &&                                                                  \
+    (defined(FLSIM_X6_FRESH) || defined(FLSIM_X6_PP_V) || defined(FLSIM_DG_FMS) ||          \
+     defined(FLSIM_DIRECT_FENCES) || defined(FLSIM_DX6_FENCES) || defined(FLSIM_BUFLOAD) ||  \
+     defined(FLSIM_SEQ_EARLY_EXIT))
+#error "FLSIM_* measurement overrides need a lab build (make LAB=1)"
+#endif
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -32,6 +46,16 @@ const char* last_error();
     } while (0)
 
 #define RC(x) do { int _r = (x); if (_r) return _r; } while (0)
+
+// a measurement override from the environment (lab builds only; see the top of this file)
+inline const char* lab_env(const char* name) {
+#ifdef FLSIM_LAB
+    return getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
 
 #define FLSIM_LAUNCH_CHECK()                                                            \
     do {                                                                                \

@@ -21,11 +21,6 @@
 
 namespace flsim {
 
-#ifndef FLSIM_CORE_PP
-#define FLSIM_CORE_PP 0
-#endif
-constexpr bool CORE_PP = FLSIM_CORE_PP;
-
 constexpr int GK = 16;  // K depth per LDS stage
 
 __device__ __forceinline__ int kc_swz(int row) { return (4 - ((row >> 2) & 3)) & 3; }
@@ -220,18 +215,11 @@ gemm_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, int t
         if (wave >= 4) __builtin_amdgcn_s_setprio(1);
     }
     int cur = 0;
-    // (measurement, -DFLSIM_CORE_PP=1) the k-contiguous GEMMs with a branch-free body whose
-    // staging is interleaved with the MFMAs (gemm_x6.h X6_PP): an LDS store every second MFMA, a
-    // global load every fourth
-    constexpr bool PP = CORE_PP && AL::KC && BL::KC;
+    // (the staging interleaved with the MFMAs in a branch-free body, as gemm_x6.h's X6_PP does
+    // for the split forwards, made conv3's data gradient 3 % slower here and left VGG-11's fp32
+    // data gradients unchanged, profiles/r05/ab/core_interleave.txt: removed)
     for (int ks = ks0; ks < ks1; ++ks) {
-        if constexpr (PP) {
-            al.store(lds + (cur ^ 1) * BUF, ra);
-            bl.store(lds + (cur ^ 1) * BUF + A_FL, rb);
-            const int kl = ks + 2 < ks1 ? ks + 2 : ks1 - 1;
-            al.load(kl, ra);
-            bl.load(kl, rb);
-        } else if (ks + 1 < ks1) {
+        if (ks + 1 < ks1) {
             al.store(lds + (cur ^ 1) * BUF, ra);
             bl.store(lds + (cur ^ 1) * BUF + A_FL, rb);
             if (ks + 2 < ks1) {
@@ -261,15 +249,6 @@ gemm_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, int t
             for (int i = 0; i < FM; ++i)
 #pragma unroll
                 for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(af[i][kk], bf[j][kk], acc[i][j]);
-        if constexpr (PP) {
-#pragma unroll
-            for (int n = 0; n < 4 * FM * FN; ++n) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
-                if (n % 2 == 0) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
-                if (n % 4 == 1) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-            }
-        }
         __syncthreads();
         cur ^= 1;
     }

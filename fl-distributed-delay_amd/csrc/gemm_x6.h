@@ -74,7 +74,8 @@ __device__ __forceinline__ f32x4 x6_step(f32x4 acc, f32x4 a0, f32x4 a1, f32x4 b0
 #define FLSIM_X6_FRESH 0
 #endif
 constexpr bool x6_fresh(bool kc) {
-    return FLSIM_X6_FRESH == 1 || FLSIM_X6_FRESH == 3 || (FLSIM_X6_FRESH == 2 && kc);
+    return FLSIM_X6_FRESH == 1 || FLSIM_X6_FRESH == 3 || (FLSIM_X6_FRESH == 2 && kc) ||
+           (FLSIM_X6_FRESH == 4 && !kc);
 }
 constexpr bool x6_fresh_bias() { return FLSIM_X6_FRESH >= 2; }
 
@@ -94,10 +95,6 @@ constexpr bool x6_fresh_bias() { return FLSIM_X6_FRESH >= 2; }
 #define FLSIM_X6_PP_L 4
 #endif
 constexpr int X6_PP_V = FLSIM_X6_PP_V, X6_PP_W = FLSIM_X6_PP_W, X6_PP_L = FLSIM_X6_PP_L;
-#ifndef FLSIM_X6_PP_KM
-#define FLSIM_X6_PP_KM 0
-#endif
-constexpr bool X6_PP_KM = FLSIM_X6_PP_KM;
 
 typedef short s16x4v __attribute__((ext_vector_type(4)));
 
@@ -321,13 +318,12 @@ gemm_x6_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, in
     constexpr bool PP_KC = X6_PP_V > 0 && AL::KC && BL::KC && !X6Fresh<EPI>::value &&
                            std::is_same_v<typename AL::Unit, XsUnit> &&
                            std::is_same_v<typename BL::Unit, XsUnit>;
-    // (measurement, -DFLSIM_X6_PP_KM=1) the 192-row k-major weight-gradient tiles of PN1's conv5 /
-    // conv6 interleaved too, two VALU per MFMA, a store and a load every third: +2.7 % / +0.8 % in
-    // the lab (profiles/r05/lab_x6_interleave_wgrad.txt) but 5-6 % slower in the product
-    // (profiles/r05/ab/x6_interleave_km.txt), so off
-    constexpr bool PP_KM = X6_PP_KM && !AL::KC && !BL::KC && FM == 6 && WAVES_M * WAVES_N == 4;
-    constexpr bool PP = PP_KC || PP_KM;
-    constexpr int PV = PP_KM ? 2 : X6_PP_V, PW = PP_KM ? 3 : X6_PP_W, PL = PP_KM ? 3 : X6_PP_L;
+    // (the 192-row k-major weight-gradient tiles of PN1's conv5 / conv6 interleaved too, two
+    // VALU per MFMA, a store and a load every third: +2.7 % / +0.8 % in the lab,
+    // profiles/r05/lab_x6_interleave_wgrad.txt, but 5-6 % slower in the product,
+    // profiles/r05/ab/x6_interleave_km.txt: removed)
+    constexpr bool PP = PP_KC;
+    constexpr int PV = X6_PP_V, PW = X6_PP_W, PL = X6_PP_L;
     auto main_loop = [&](auto with_sum) {
         constexpr bool WS = decltype(with_sum)::value;
         for (int ks = ks0; ks < ks1; ++ks) {

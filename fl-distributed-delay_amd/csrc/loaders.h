@@ -85,6 +85,26 @@ struct XsSrcSM : XsSrc {
     static constexpr bool SM = true;
 };
 
+// A split tensor read back as fp32 for the fp32 GEMM (gemm_core.h): each unit's HM and L parts
+// loaded as by XsSrc and put back together, (h + m) + l, which is the fp32 value exactly
+// (split.h).  The PerformantNet1 conv2-6 weight gradients run on the fp32 MFMA this way over the
+// layer inputs their producers wrote split (summed over a 16,384-sample chunk, the
+// bf16 MFMA's truncating accumulation leaves a relative bias of 5e-7 .. 1e-6 in them, above
+// SURVEY 8(c)'s bound; the fp32 MFMA is an fmaf chain).
+struct XsF32Src : XsSrc {
+    using Unit = f32x4;
+    static constexpr bool SPLIT = false;
+    __device__ __forceinline__ f32x4 ld(unsigned byte_off) const {
+        return xs_value(XsSrc::ld(byte_off));
+    }
+    __device__ __forceinline__ f32x4 ld_or0(unsigned byte_off, bool ok) const {
+        return ld(ok ? byte_off : BUF_OOB);
+    }
+};
+struct XsF32SrcSM : XsF32Src {
+    static constexpr bool SM = true;
+};
+
 // r / D for 0 <= r < R by one 24-bit multiply and a shift (exact on that range, checked at
 // compile time): the per-unit pixel -> (row, column) split of the k-major loaders
 template <unsigned D, unsigned R>

@@ -771,7 +771,7 @@ static int conv_pool_direct(const float* X, int S, const float* Wpk, int KP, flo
 static int small_chunk_samples() {
     static int s = -1;
     if (s < 0) {
-        const char* e = getenv("FLSIM_SMALL_S");
+        const char* e = lab_env("FLSIM_SMALL_S");
         s = e ? atoi(e) : 256;
     }
     return s;
@@ -816,7 +816,7 @@ static int conv_pool_direct_sz(const float* X, int S, const float* Wpk, int KP, 
 static int wsplit(int ksteps, int Z, int tiles, int cap = 0) {
     static int kmin = -1;
     if (kmin < 0) {
-        const char* e = getenv("FLSIM_WSPLIT_KMIN");     // measurement override (0: always Z)
+        const char* e = lab_env("FLSIM_WSPLIT_KMIN");     // measurement override (0: always Z)
         kmin = e ? atoi(e) : 32;
     }
     if (kmin <= 0) return Z;
@@ -825,7 +825,7 @@ static int wsplit(int ksteps, int Z, int tiles, int cap = 0) {
     if (z < zb) z = zb;
     static int fill = -1;
     if (fill < 0) {
-        const char* e = getenv("FLSIM_WSPLIT_FILL");     // measurement override (1: on)
+        const char* e = lab_env("FLSIM_WSPLIT_FILL");     // measurement override (1: on)
         fill = e ? atoi(e) : 0;
     }
     if (fill && cap > 0 && z < Z) {

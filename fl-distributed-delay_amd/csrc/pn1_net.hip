@@ -20,7 +20,6 @@
 #include <mutex>
 #include <unordered_map>
 
-#include "c1fuse.h"
 #include "net_kernels.h"
 #include "slabstep.h"
 
@@ -160,23 +159,26 @@ struct WS {
     XsT x(float* hm, float* l) const { return XsT{hm, l}; }
 };
 
-static WS ws_layout(char* base, int S) {
+// row0 > 0: the same workspace seen from sample row row0 on (every tensor is sample-major,
+// [S][...]), so a pass over S' samples at row0 reads and writes rows [row0, row0 + S') of a
+// workspace laid out for S samples (the facade's deferred backward, flsim_pn1_fwd_rows)
+static WS ws_layout(char* base, int S, int row0 = 0) {
     WS w;
     long o = 0;
-    auto take = [&](long bytes) {
-        char* p = base ? base + o : nullptr;
-        o += (bytes + 255) / 256 * 256;
+    auto take_rows = [&](long per_bytes) {
+        char* p = base ? base + o + per_bytes * row0 : nullptr;
+        o += (per_bytes * S + 255) / 256 * 256;
         return p;
     };
-    auto tf = [&](long per) { return (float*)take(per * (long)S * 4); };
+    auto tf = [&](long per) { return (float*)take_rows(per * 4); };
     w.x0 = tf(4096); w.a1 = tf(55488); w.a2 = tf(62208); w.d1 = tf(15552);
     w.a3 = tf(38400); w.a4 = tf(46464); w.d2 = tf(11616); w.a5 = tf(32448);
     w.a6 = tf(43200); w.d3 = tf(9408); w.e1 = tf(512); w.e2 = tf(256);
     w.part = tf(512L * ZL1F); w.dh1 = tf(512); w.dh2 = tf(256);
     w.gx = tf(55488); w.gy = tf(15552); w.loss_s = tf(1); w.dlog = tf(16);
-    w.y = (int32_t*)take(4L * S);
-    w.i1 = (uint8_t*)take(15552L * S); w.i2 = (uint8_t*)take(11616L * S);
-    w.i3 = (uint8_t*)take(9408L * S);
+    w.y = (int32_t*)take_rows(4);
+    w.i1 = (uint8_t*)take_rows(15552); w.i2 = (uint8_t*)take_rows(11616);
+    w.i3 = (uint8_t*)take_rows(9408);
     w.a1l = tf(55488 / 2); w.d1l = tf(15552 / 2); w.a3l = tf(38400 / 2); w.d2l = tf(11616 / 2);
     w.a5l = tf(32448 / 2);
     w.a6l = tf(0); w.a4l = tf(0); w.a2l = tf(0); w.gxl = tf(0);   // (dZ is fp32: ids kept, no bytes)
@@ -523,17 +525,12 @@ static bool concurrent_backward(int S) {
     static int smax = -1;
     if (smax < 0) {
         // measurement override: the largest chunk (samples) that runs the two streams; 0: off
-        const char* e = getenv("FLSIM_CONCURRENT_BWD");
+        const char* e = lab_env("FLSIM_CONCURRENT_BWD");
         smax = e ? atoi(e) : 2048;
     }
     return S <= smax;
 }
 
-// debug / measurement: FLSIM_DEBUG_BWD_STOP=6 / 5 / 4 ends the backward pass after conv6's /
-// conv5's / conv4's data gradient (dz5 in gx, dz4 in a4, dz3 in gx; all fp32),
-// so each data-gradient GEMM can be checked on its own inputs (tools/gemm_diag.py); the weight
-// gradients that ran (conv6 .. conv<stop>, the linear layers) reach the epoch's slab sum, the
-// others stay zero
 // fragment rows per wave of the conv4-6 fp32 data gradients on chunks of at most
 // small_chunk_samples() samples: 2, the large-chunk tile (configs[1] 984 -> 995 worker-steps/s
 // against 1, A B A B, profiles/r05/c1_dg_fms.txt; measurement override -DFLSIM_DG_FMS=<1|2>)
@@ -542,22 +539,15 @@ static bool concurrent_backward(int S) {
 #endif
 constexpr int DG_FMS = FLSIM_DG_FMS;
 
+// debug / measurement: FLSIM_DEBUG_BWD_STOP=6 / 5 / 4 / 3 ends the backward pass after conv6's /
+// conv5's / conv4's / conv3's data gradient (dz5 in gx; dz4 in a4, dz5 in gx; dz3 in gx, dz4 in
+// a4; dz2 in a2, dz3 in gx; all fp32), so each GEMM can be checked on its own inputs
+// (tools/gemm_diag.py, tests/test_gpu_survey_chunk.py); the weight gradients that ran (conv6 ..
+// conv<stop>, the linear layers) reach the epoch's slab sum, the others stay zero.  Read per call
+// (tests switch it in-process).
 static int debug_stop() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("FLSIM_DEBUG_BWD_STOP");
-        v = e ? atoi(e) : 0;
-    }
-    return v;
-}
-
-// conv1's weight gradient inside conv2's data gradient (c1fuse.h) with FLSIM_C1_FUSE=1.  Not the
-// default: the fused launch took 7.27-7.29 ms against 6.14-6.17 + 0.87-0.88 ms for the two GEMMs
-// apart (headline 1331.8 / 1335.1 against 1342.7 / 1346.3 worker-steps/s, profiles/r04/r04n,
-// r04o): its epilogue holds the data gradient at two blocks per CU instead of three
-static bool fuse_conv1() {
-    const char* e = getenv("FLSIM_C1_FUSE");      // read per call: tests switch it in-process
-    return e && atoi(e) != 0;
+    const char* e = getenv("FLSIM_DEBUG_BWD_STOP");
+    return e ? atoi(e) : 0;
 }
 
 static int backward(const GradState& g, const WS& w, const float* theta, int S, int dropout,
@@ -624,7 +614,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     // (192 x 192 tiles of 8 waves ran 9.10-9.13 against 9.41 ms in the lab,
     // profiles/r04/r04l/lab_wg6v.txt, but 9.26-9.29 against 9.10-9.12 in the product, A B A B on
     // one box, profiles/r04/r04s: kept 192 x 96)
-    RC((conv_wgrad_sz<13, 13, 192, 2, 6, 3, 2, 2, 3, 3, 2, 2, 14, true, true, BufSrc, XsSrc>(
+    RC((conv_wgrad<13, 13, 192, 2, 6, 3, 2, 4, 14, true, false, BufSrc, XsF32Src>(
         dz6, w.a5, S, 192, 1728, g.sw[5], g.sb[5], GEO[5].ZW, sw, K_WG6, 1728, zi(5), &zu[5],
         nullptr, w.a5l)));
     // (every data gradient runs on the fp32 MFMA: the bf16 MFMA truncates small addends toward
@@ -636,7 +626,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     // ---- conv5: wgrad (input d2), bias, dgrad -> grad wrt d2 (dropout site 2), scattered through
     //      pool2 straight into dz4 (a4 buffer; no gy round trip) ----
     RC(fork());
-    RC((conv_wgrad_sz<11, 11, 96, 2, 6, 3, 2, 2, 3, 3, 2, 2, 0, false, true, BufSrc, XsSrc>(
+    RC((conv_wgrad<11, 11, 96, 2, 6, 3, 2, 2, 0, false, false, BufSrc, XsF32Src>(
         dz5, w.d2, S, 192, 864, g.sw[4], g.sb[4], GEO[4].ZW, sw, K_WG5, 864, zi(4), &zu[4],
         nullptr, w.d2l)));
     RC((conv_direct_sz<13, 13, 192, 0, 2, DG_FMS, 6, 8, 3, 2, false, 0>(dz5, S, g.wd[4], 96, 1728,
@@ -650,7 +640,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     // gradients split dZ while staging (split-bf16 kernel over an fp32 dZ and a split layer input)
     RC(join());                                   // conv5's wgrad reads gx = dz5: done first
     RC(fork());
-    RC((conv_wgrad<20, 20, 96, 2, 3, 3, 2, 2, 0, false, true, BufSrc, XsSrcSM>(
+    RC((conv_wgrad<20, 20, 96, 2, 3, 3, 2, 2, 0, false, false, BufSrc, XsF32SrcSM>(
         dz4, w.a3, S, 96, 864, g.sw[3], g.sb[3], GEO[3].ZW, sw, K_WG4, 864, zi(3), &zu[3],
         nullptr, w.a3l)));
     RC((conv_direct_sz<22, 22, 96, 0, 2, DG_FMS, 6, 8, 3, 2, false, 0>(dz4, S, g.wd[3], 96, 864,
@@ -661,34 +651,31 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     //      straight into dz2 (a2 buffer, fp32) ----
     RC(fork());
     // (96 x 96 tiles of 4 waves: 2.96 against 3.54 ms for 96 x 48 of 2, profiles/r04/r04j/lab_wg.txt)
-    RC((conv_wgrad_sz<18, 18, 48, 2, 3, 3, 2, 2, 3, 3, 2, 2, 0, false, true, BufSrc, XsSrcSM>(
+    RC((conv_wgrad<18, 18, 48, 2, 3, 3, 2, 1, 0, false, false, BufSrc, XsF32SrcSM>(
         dz3, w.d1, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW, sw, K_WG3, 432, zi(2), &zu[2],
         nullptr, w.d1l)));
     // (gemm_kernel: the direct-A form measured 3.87 vs 3.78 ms with this staged epilogue, r03b)
     RC((conv_like_sz<20, 20, 96, 0, 4, 2, 3, 4, 1>(dz3, S, g.wd[2], 48, 864,
         EpiDropScatterXs<18, 18, 48, false, true>{w.a2, nullptr, w.d1, w.i1, s25, S * 18 * 18}, st,
         K_DG3, 864)));
+    if (debug_stop() == 3) return finish();       // (debug: dz2 in a2, dz3 in gx)
     float* dz2 = w.a2;
     // ---- conv2: wgrad (input a1), bias, dgrad -> dz1 = . * (a1 > 0) into gx (fp32) ----
     RC(join());                                   // conv3's wgrad reads gx = dz3: done first
     RC(fork());
-    RC((conv_wgrad_sz<34, 34, 48, 2, 3, 3, 1, 3, 3, 3, 1, 3, 0, false, true, BufSrc, XsSrcSM>(
+    RC((conv_wgrad<34, 34, 48, 2, 3, 3, 1, 1, 0, false, false, BufSrc, XsF32SrcSM>(
         dz2, w.a1, S, 48, 432, g.sw[1], g.sb[1], GEO[1].ZW, sw, K_WG2, 432, zi(1), &zu[1],
         nullptr, w.a1l)));
-    if (fuse_conv1()) {
-        // ---- conv2's dgrad with conv1's wgrad + bias fused in (c1fuse.h): dz1 stays on chip ----
-        RC((conv2_dgrad_conv1_wgrad<2, 1, 3, 8, 3, 2>(dz2, S, g.wd[1], 432, w.a1, w.x0, g.sw[0],
-                                                       g.sb[0], GEO[0].ZW, 48, zi(0), &zu[0], st,
-                                                       K_DG2)));
-    } else {
-        RC((conv_direct_sz<36, 36, 48, 0, 2, 1, 3, 8, 3, 2, false, 0>(dz2, S, g.wd[1], 48, 432,
-            EpiMaskXs<48, false, true, 1156>{w.gx, nullptr, w.a1, S * 34 * 34}, st, K_DG2, 432)));
-        float* dz1 = w.gx;
-        // ---- conv1: wgrad (input x0), bias ----
-        // (3 waves of 16 rows each: 0.272 vs 0.325 ms for one 48x48 wave, profiles/r01c/lab_conv1.txt)
-        RC((conv_wgrad<32, 32, 4, 2, 1, 3, 3, 1>(dz1, w.x0, S, 48, 48, g.sw[0], g.sb[0], GEO[0].ZW,
-                                                st, K_WG1, 27, zi(0), &zu[0])));
-    }
+    RC((conv_direct_sz<36, 36, 48, 0, 2, 1, 3, 8, 3, 2, false, 0>(dz2, S, g.wd[1], 48, 432,
+        EpiMaskXs<48, false, true, 1156>{w.gx, nullptr, w.a1, S * 34 * 34}, st, K_DG2, 432)));
+    float* dz1 = w.gx;
+    // ---- conv1: wgrad (input x0), bias ----
+    // (3 waves of 16 rows each: 0.272 vs 0.325 ms for one 48x48 wave, profiles/r01c/lab_conv1.txt;
+    // fusing it into conv2's data gradient measured slower: 7.27 ms against 6.14 + 0.87 ms for
+    // the two launches, the fused epilogue's registers cost the data gradient a third of its
+    // occupancy, profiles/r04/r04n)
+    RC((conv_wgrad<32, 32, 4, 2, 1, 3, 3, 1>(dz1, w.x0, S, 48, 48, g.sw[0], g.sb[0], GEO[0].ZW,
+                                            st, K_WG1, 27, zi(0), &zu[0])));
     return finish();                              // (the next chunk's forward rewrites a1, a2)
 }
 
@@ -811,30 +798,53 @@ int flsim_pn1_fwd_bwd_chunk(void* gradstate, void* workspace, int max_samples, c
 
 // one pipelined pass: `front` (batch fill, forward, loss) on `stream`, then the backward on the
 // gradstate's backward stream; a forward waits for the backward that last read its workspace
-template <class Front>
-static int run_pipelined(void* gradstate, void* workspace, int max_samples, const float* theta,
-                         int S, int dropout, hipStream_t stream, Front&& front) {
-    EpochRows* er = epoch_rows(gradstate);
-    FLSIM_REQUIRE(er, "backward pass without flsim_pn1_begin_epoch on this gradstate");
-    std::lock_guard<std::mutex> lk(g_pipe_mu);
+// (g_pipe_mu held) the gradstate's pipe, its stream and events created on first use
+static int pipe_of(void* gradstate, Pipe** out) {
     Pipe& p = g_pipes[gradstate];
     if (!p.bs) {
-        FLSIM_CHECK_HIP(hipStreamCreateWithFlags(&p.bs, hipStreamNonBlocking));
+        // the lowest priority: the caller's forwards (the facade's per-call forward, whose loss
+        // the caller waits for) get the CUs first as the backward's blocks retire
+        int least = 0, greatest = 0;
+        FLSIM_CHECK_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        FLSIM_CHECK_HIP(hipStreamCreateWithPriority(&p.bs, hipStreamNonBlocking, least));
         FLSIM_CHECK_HIP(hipEventCreateWithFlags(&p.fwd_done, hipEventDisableTiming));
         FLSIM_CHECK_HIP(hipEventCreateWithFlags(&p.bwd_tail, hipEventDisableTiming));
     }
-    hipEvent_t& ws_ev = p.ws_free[workspace];
-    if (!ws_ev) FLSIM_CHECK_HIP(hipEventCreateWithFlags(&ws_ev, hipEventDisableTiming));
-    else FLSIM_CHECK_HIP(hipStreamWaitEvent(stream, ws_ev, 0));   // its last backward is done
+    *out = &p;
+    return 0;
+}
+
+// (g_pipe_mu held) the backward of workspace rows [0, S) on the gradstate's backward stream,
+// after everything queued on `stream` so far; the workspace's event marks its end
+static int queue_backward(void* gradstate, Pipe& p, hipEvent_t& ws_ev, void* workspace,
+                          int max_samples, const float* theta, int S, int dropout,
+                          hipStream_t stream, EpochRows* er) {
     WS w = ws_layout((char*)workspace, max_samples);
     GradState g = gs_layout((float*)gradstate);
-    RC(front(g, w));
     FLSIM_CHECK_HIP(hipEventRecord(p.fwd_done, stream));
     FLSIM_CHECK_HIP(hipStreamWaitEvent(p.bs, p.fwd_done, 0));
     RC(backward(g, w, theta, S, dropout, p.bs, er));
     FLSIM_CHECK_HIP(hipEventRecord(ws_ev, p.bs));
     p.pending = true;
     return 0;
+}
+
+template <class Front>
+static int run_pipelined(void* gradstate, void* workspace, int max_samples, const float* theta,
+                         int S, int dropout, hipStream_t stream, Front&& front) {
+    EpochRows* er = epoch_rows(gradstate);
+    FLSIM_REQUIRE(er, "backward pass without flsim_pn1_begin_epoch on this gradstate");
+    std::lock_guard<std::mutex> lk(g_pipe_mu);
+    Pipe* p = nullptr;
+    RC(pipe_of(gradstate, &p));
+    hipEvent_t& ws_ev = p->ws_free[workspace];
+    if (!ws_ev) FLSIM_CHECK_HIP(hipEventCreateWithFlags(&ws_ev, hipEventDisableTiming));
+    else FLSIM_CHECK_HIP(hipStreamWaitEvent(stream, ws_ev, 0));   // its last backward is done
+    WS w = ws_layout((char*)workspace, max_samples);
+    GradState g = gs_layout((float*)gradstate);
+    RC(front(g, w));
+    return queue_backward(gradstate, *p, ws_ev, workspace, max_samples, theta, S, dropout, stream,
+                          er);
 }
 
 extern "C" {
@@ -887,6 +897,67 @@ int flsim_pn1_fwd_bwd_input_async(void* gradstate, void* workspace, int max_samp
                                   w.dlog, w.dh2, S, 1, dropout ? SCALE_P50 : 1.f,
                                   1.f / (float)n_samples, worker_loss, stream, workers);
     });
+}
+
+// The facade's deferred backward (Worker.fwd_bkwd, agents.py:32-40, with the backward of up to a
+// chunk of calls batched into one pass): every fwd_bkwd call of an epoch runs on the same theta_t
+// (main.py:154,159,169), so each call's forward + loss runs alone -- the loss is all the call
+// must return now (agents.py:40) -- into workspace rows [row0, row0 + S) (ws_layout's row view),
+// and one backward over rows [0, n_rows) later adds the whole chunk's gradient to the slabs, at
+// the batched engine's rates.  The forward kernels are the per-call facade's (bit-identical
+// losses); the backward is FLSimulation's over the same rows.
+int flsim_pn1_fwd_rows(void* gradstate, void* workspace, int max_samples, int row0,
+                       const float* theta, const float* x, const int64_t* y, int n_samples,
+                       const WorkerRec* workers, uint64_t seed, int dropout, float* worker_loss,
+                       hipStream_t stream) {
+    FLSIM_REQUIRE(gradstate && workspace && theta && x && y && workers && worker_loss,
+                  "null pointer");
+    FLSIM_REQUIRE(n_samples > 0, "empty batch");
+    FLSIM_REQUIRE(row0 >= 0 && row0 % SAMPLES_PER_WORKER == 0,
+                  "row0 %d is not a multiple of %d", row0, SAMPLES_PER_WORKER);
+    const int S = ceil_div(n_samples, SAMPLES_PER_WORKER) * SAMPLES_PER_WORKER;
+    FLSIM_REQUIRE((long)row0 + S <= max_samples, "rows [%d, %d) exceed workspace (%d)", row0,
+                  row0 + S, max_samples);
+    FLSIM_REQUIRE(max_samples <= 16384, "workspace of %d samples exceeds the 32-bit index budget",
+                  max_samples);
+    FLSIM_REQUIRE(epoch_rows(gradstate), "forward rows without flsim_pn1_begin_epoch");
+    {   // rows a queued backward still reads are not overwritten
+        std::lock_guard<std::mutex> lk(g_pipe_mu);
+        auto it = g_pipes.find(gradstate);
+        if (it != g_pipes.end()) {
+            auto e = it->second.ws_free.find(workspace);
+            if (e != it->second.ws_free.end() && e->second)
+                FLSIM_CHECK_HIP(hipStreamWaitEvent(stream, e->second, 0));
+        }
+    }
+    WS w = ws_layout((char*)workspace, max_samples, row0);
+    GradState g = gs_layout((float*)gradstate);
+    hipLaunchKernelGGL(k_load_input, dim3(S), dim3(256), 0, stream, x, y, n_samples, w.x0, w.y);
+    FLSIM_LAUNCH_CHECK();
+    RC(forward(g, w, theta, S, workers, seed, dropout, stream));
+    return head_and_loss<256>(w.e2, theta + P_OFF[16], theta + P_OFF[17], w.y, w.loss_s, w.dlog,
+                              w.dh2, S, 1, dropout ? SCALE_P50 : 1.f, 1.f / (float)n_samples,
+                              worker_loss, stream, workers);
+}
+
+// the backward of rows [0, n_rows) written by flsim_pn1_fwd_rows with this theta and dropout
+// flag, on the gradstate's backward stream after everything queued on `stream` (so the next
+// chunk's forwards -- into another workspace -- overlap it); every other entry point on the
+// gradstate joins it first (pipe_join)
+int flsim_pn1_bwd_rows(void* gradstate, void* workspace, int max_samples, int n_rows,
+                       const float* theta, int dropout, hipStream_t stream) {
+    FLSIM_REQUIRE(gradstate && workspace && theta, "null pointer");
+    FLSIM_REQUIRE(n_rows > 0 && n_rows % SAMPLES_PER_WORKER == 0 && n_rows <= max_samples &&
+                  n_rows <= 16384, "bad row count %d (workspace %d)", n_rows, max_samples);
+    EpochRows* er = epoch_rows(gradstate);
+    FLSIM_REQUIRE(er, "backward pass without flsim_pn1_begin_epoch on this gradstate");
+    std::lock_guard<std::mutex> lk(g_pipe_mu);
+    Pipe* p = nullptr;
+    RC(pipe_of(gradstate, &p));
+    hipEvent_t& ws_ev = p->ws_free[workspace];
+    if (!ws_ev) FLSIM_CHECK_HIP(hipEventCreateWithFlags(&ws_ev, hipEventDisableTiming));
+    return queue_backward(gradstate, *p, ws_ev, workspace, max_samples, theta, n_rows, dropout,
+                          stream, er);
 }
 
 // explicit batch (the Worker.fwd_bkwd(inp, outp) facade, agents.py:32-35): x NCHW fp32, y int64,

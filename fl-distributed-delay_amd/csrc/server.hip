@@ -884,7 +884,7 @@ int slab_step_launch(float* gradstate, const StepPlan& plan, long cnt_off, long 
     A.il_lo = plan.u_wide;
     A.il_w = plan.u_conv - plan.u_wide;
     A.il_n = (rule && rule->prog != nullptr) ? plan.units - plan.u_wide : 0;
-    if (const char* env = getenv("FLSIM_STEP_UNITS")) {
+    if (const char* env = lab_env("FLSIM_STEP_UNITS")) {
         int lo = 0, hi = 0;
         if (sscanf(env, "%d,%d", &lo, &hi) == 2 && 0 <= lo && lo < hi && hi <= plan.units) {
             A.u_lo = lo;
@@ -892,7 +892,7 @@ int slab_step_launch(float* gradstate, const StepPlan& plan, long cnt_off, long 
             A.il_n = 0;             // measurement of a unit range: plan order, no interleave
         }
     }
-    if (const char* env = getenv("FLSIM_STEP_NO_INTERLEAVE"))
+    if (const char* env = lab_env("FLSIM_STEP_NO_INTERLEAVE"))
         if (atoi(env)) A.il_n = 0;
     const unsigned nblk = (unsigned)(u_hi - A.u_lo);
     // algorithmic HBM bytes: every slab byte once; S_out written; p, m, v read + written; each
@@ -957,7 +957,7 @@ int flsim_aggregate_adam_rule_push(const float* S, float* S_out, const flsim_rul
     // 28.2 vs 28.4 us for k = 512; 32.0 vs 33.1 us for k = 513 with the stale S_{t-d});
     // FLSIM_AGG_G = 1 / 2 forces a form, 0 the LDS-staged k_agg_stream (measurement only)
     int agg_g = A.R.narr == 0 ? 2 : 1;
-    if (const char* e = getenv("FLSIM_AGG_G")) agg_g = atoi(e);
+    if (const char* e = lab_env("FLSIM_AGG_G")) agg_g = atoi(e);
     if (agg_g < 0 || agg_g > AGG_GMAX) agg_g = 1;
     const bool reg = A.R.prog == nullptr && A.R.narr <= 2 && agg_g > 0;
     const int G = reg ? agg_g : 1;

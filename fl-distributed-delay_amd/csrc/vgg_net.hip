@@ -352,12 +352,14 @@ static int vbackward(const VGrad& g, const VWS& w, const float* th, const VOff& 
     RC(head_wgrad<VFEAT>(w.dlog, w.e2, g.l3w, g.l3b, S, VZH, st));
     // Linear2: wgrad (input e1), dgrad through Dropout + ReLU of Linear1 (e1 is the dropped output)
     RC((linear_wgrad<4, 4, 2, 2, true>(w.dh2, w.e1, g.l2w, g.l2b, S, VFEAT, VFEAT, VZL, st, K_VL2W)));
-    RC((linear_dgrad<4, 4, 2, 2, true>(w.dh2, th + o.l2w, w.dh1, w.e1, s50, S, VFEAT, VFEAT, st,
+    // (every data gradient on the fp32 MFMA, the classifier's too: the bf16 MFMA's truncating
+    // sum biases per-channel sums)
+    RC((linear_dgrad<4, 4, 2, 2>(w.dh2, th + o.l2w, w.dh1, w.e1, s50, S, VFEAT, VFEAT, st,
                                  K_VL2D)));
     // Linear1: wgrad (input f0 = dropped features), dgrad through the first Dropout and conv8's
     // pooled ReLU (f0 > 0), then the pool scatter -> dz8
     RC((linear_wgrad<4, 4, 2, 2, true>(w.dh1, w.f0, g.l1w, g.l1b, S, VFEAT, VFEAT, VZL, st, K_VL1W)));
-    RC((linear_dgrad<4, 4, 2, 2, true>(w.dh1, th + o.l1w, w.gy, w.f0, s50, S, VFEAT, VFEAT, st,
+    RC((linear_dgrad<4, 4, 2, 2>(w.dh1, th + o.l1w, w.gy, w.f0, s50, S, VFEAT, VFEAT, st,
                                  K_VL1D)));
     RC((pool_scatter<2, 2, 512, false>(w.gy, w.i8, w.ga, S, st)));
     RC((vbn_back<BN, 2, 512>(g, w, th, o, 7, w.ga, S, st)));

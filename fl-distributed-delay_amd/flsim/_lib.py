@@ -35,8 +35,11 @@ EXPORTS = [
     "flsim_probe_enable", "flsim_probe_read", "flsim_probe_disable",
     "flsim_probe_kernel_count", "flsim_probe_kernel_name", "flsim_pn1_release",
     "flsim_pn1_fwd_bwd_chunk_async", "flsim_pn1_fwd_bwd_input_async",
-    "flsim_aggregate_adam_rule_push",
+    "flsim_aggregate_adam_rule_push", "flsim_pn1_fwd_rows", "flsim_pn1_bwd_rows",
+    "flsim_comm_unique_id", "flsim_comm_create", "flsim_comm_size", "flsim_comm_rank",
+    "flsim_allreduce_sum", "flsim_comm_destroy",
 ]
+COMM_ID_BYTES = 128      # FLSIM_COMM_ID_BYTES
 
 
 class FLSimError(RuntimeError):
@@ -109,6 +112,16 @@ def lib():
         ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_int, vp, vp]
     L.flsim_pn1_fwd_bwd_input_async.argtypes = [
         vp, vp, ctypes.c_int, vp, vp, vp, ctypes.c_int, vp, ctypes.c_uint64, ctypes.c_int, vp, vp]
+    L.flsim_pn1_fwd_rows.argtypes = [
+        vp, vp, ctypes.c_int, ctypes.c_int, vp, vp, vp, ctypes.c_int, vp, ctypes.c_uint64,
+        ctypes.c_int, vp, vp]
+    L.flsim_pn1_bwd_rows.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, vp]
+    L.flsim_comm_unique_id.argtypes = [vp]
+    L.flsim_comm_create.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp]
+    L.flsim_comm_size.argtypes = [vp]
+    L.flsim_comm_rank.argtypes = [vp]
+    L.flsim_allreduce_sum.argtypes = [vp, vp, ctypes.c_size_t, vp]
+    L.flsim_comm_destroy.argtypes = [vp]
     L.flsim_aggregate_adam.argtypes = [
         vp, ctypes.c_int, vp, ctypes.c_int, vp, vp, vp, ctypes.c_long, vp, ctypes.c_int,
         ctypes.c_long, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp]

@@ -165,6 +165,31 @@ class NetEngine:
             int(x.shape[0]), ptr(workers_dev), ctypes.c_uint64(seed), int(bool(dropout)),
             ptr(loss_out), stream_ptr()))
 
+    def _slot_workspace(self, slot):
+        if getattr(self, "workspace2", None) is None:
+            self.workspace2 = torch.empty_like(self.workspace)
+        return self.workspace if slot % 2 == 0 else self.workspace2
+
+    def forward_rows(self, theta, x, y, workers_dev, seed, dropout, loss_out, row0, slot):
+        """The facade's deferred backward (PN1Engine): forward + loss of an explicit batch into
+        workspace rows [row0, row0 + ceil(n/128)*128) of workspace `slot`; the loss is ready on
+        the current stream.  backward_rows() later runs the backward of all rows at once."""
+        ws = self._slot_workspace(slot)
+        self.last_workspace = ws
+        x = x.contiguous()
+        y = y.to(torch.int64).contiguous()
+        check(lib().flsim_pn1_fwd_rows(
+            ptr(self.gradstate), ptr(ws), self.max_samples, int(row0), ptr(theta), ptr(x), ptr(y),
+            int(x.shape[0]), ptr(workers_dev), ctypes.c_uint64(seed), int(bool(dropout)),
+            ptr(loss_out), stream_ptr()))
+
+    def backward_rows(self, theta, n_rows, dropout, slot):
+        """The backward of rows [0, n_rows) of workspace `slot` (forward_rows) into the epoch's
+        slabs, on the library's backward stream (the next slot's forwards overlap it)."""
+        check(lib().flsim_pn1_bwd_rows(ptr(self.gradstate), ptr(self._slot_workspace(slot)),
+                                       self.max_samples, int(n_rows), ptr(theta),
+                                       int(bool(dropout)), stream_ptr()))
+
     def evaluate_input(self, theta, x):
         """Predictions for an explicit NCHW fp32 batch (util.py:31-45's model(images) in eval
         mode): device int32 tensor of argmax indices."""

@@ -60,7 +60,8 @@ class FLSimulation:
                  semantics="reference", dropout=True, chunk_workers=128, device=None, theta0=None,
                  group=None, max_throttle=32, pool=None, betas=(0.9, 0.999), eps=1e-8,
                  engine=None, device_pool=None, test_pool=None, model="PerformantNet1",
-                 fused=True, keep_S=False, batch_size=128, distributed=None):
+                 fused=True, keep_S=False, batch_size=128, distributed=None,
+                 collective="torch"):
         if semantics not in SEMANTICS:
             raise NotImplementedError(f"semantics {semantics!r} (supported: {SEMANTICS})")
         self.n = int(n_workers)
@@ -104,6 +105,25 @@ class FLSimulation:
         self.distributed = self.world > 1 if distributed is None else bool(distributed)
         if self.distributed and not (dist.is_available() and dist.is_initialized()):
             raise RuntimeError("distributed=True needs an initialised torch.distributed group")
+        # the epoch's one all-reduce: "torch" = torch.distributed (RCCL with the nccl backend);
+        # "flsim" = the C-ABI's flsim_allreduce_sum over RCCL (include/flsim.h), its unique id
+        # shipped over the process group; "flsim-local" (world 1) = the C-ABI's one-rank
+        # communicator, which never touches RCCL
+        if collective not in ("torch", "flsim", "flsim-local"):
+            raise ValueError(f"collective {collective!r}")
+        if collective == "flsim-local" and self.world != 1:
+            raise ValueError("collective='flsim-local' is the one-rank communicator")
+        self.collective = collective
+        self._comm = None
+        if self.distributed and collective != "torch":
+            from .comm import Comm
+            if collective == "flsim":
+                box = [Comm.unique_id() if self.rank == 0 else None]
+                dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0)
+                                           if group is not None else 0, group=group)
+                self._comm = Comm(self.world, self.rank, box[0])
+            else:
+                self._comm = Comm()
         self.device = torch.device(device) if device is not None else \
             torch.device("cuda", torch.cuda.current_device())
         # engine / device_pool are injectable only so tests can drive the sharding and
@@ -199,16 +219,22 @@ class FLSimulation:
             self._wt_ev[j] = ev
         return dev
 
+    def _reduce(self, buf):
+        if self._comm is not None:
+            self._comm.all_reduce_sum(buf)          # flsim_allreduce_sum (C-ABI, RCCL)
+        else:
+            torch.distributed.all_reduce(buf, group=self.group)
+
     def _all_reduce(self, buf):
-        """The epoch's one collective (RCCL over xGMI with the nccl backend)."""
+        """The epoch's one collective (RCCL over xGMI: the nccl backend or the C-ABI's)."""
         if self.time_collective and self.device.type == "cuda":
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            torch.distributed.all_reduce(buf, group=self.group)
+            self._reduce(buf)
             e1.record()
             self.coll_events.append((e0, e1))
         else:
-            torch.distributed.all_reduce(buf, group=self.group)
+            self._reduce(buf)
 
     def collective_ms(self):
         """Per-epoch collective times (ms) recorded since the last call (synchronises)."""

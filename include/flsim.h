@@ -38,6 +38,28 @@ typedef struct WorkerRec {
 const char* flsim_last_error(void);
 
 /* ---------------------------------------------------------------------------------------------
+ * The one collective of a sharded server step: each rank computes its contiguous
+ * block of the epoch's workers (main.py:137-178 split across GPUs) into a partial
+ * [S_t | losses]; one all-reduce (sum, fp32, in place) over RCCL / xGMI then gives every rank the
+ * sum that rule() (main.py:184) and Adam (main.py:188) consume, replicated.  The reference has no
+ * collective (one process, main.py:137); this is its replacement for a caller that does not use
+ * torch.distributed.  RCCL is bound at run time: the copy already loaded in the process (e.g.
+ * torch's), else $FLSIM_RCCL_LIB, else librccl.so.1.
+ *   flsim_comm_unique_id: rank 0 makes the id (ncclGetUniqueId) and ships it to the others;
+ *   flsim_comm_create(nranks, rank, id): ncclCommInitRank; nranks = 1 with id = NULL is a local
+ *     communicator that never touches RCCL (its all-reduce is the identity);
+ *   flsim_allreduce_sum: ncclAllReduce(buf, buf, count, float32, sum) on `stream`.
+ * ------------------------------------------------------------------------------------------- */
+#define FLSIM_COMM_ID_BYTES 128
+typedef struct flsim_comm flsim_comm;
+int flsim_comm_unique_id(unsigned char* id /* FLSIM_COMM_ID_BYTES */);
+int flsim_comm_create(int nranks, int rank, const unsigned char* id, flsim_comm** out);
+int flsim_comm_size(const flsim_comm* comm);
+int flsim_comm_rank(const flsim_comm* comm);
+int flsim_allreduce_sum(flsim_comm* comm, float* buf, size_t count, flsim_stream_t stream);
+int flsim_comm_destroy(flsim_comm* comm);
+
+/* ---------------------------------------------------------------------------------------------
  * Schedule (host): replaces the integer scan of main.py:119-123 (state), :150-166 (slow worker
  * + pesky_worker_grads FIFO), :167-178 (fast worker + throttle), :180-181 (window decrement).
  * delays[i] != 0 marks a slow worker (reference: only i = n-1, delay = --delay);
@@ -105,6 +127,22 @@ int flsim_pn1_fwd_bwd_input_async(void* gradstate, void* workspace, int max_samp
                                   const float* theta, const float* x, const int64_t* y,
                                   int n_samples, const WorkerRec* workers, uint64_t seed,
                                   int dropout, float* worker_loss, flsim_stream_t stream);
+/* The facade's deferred backward: Worker.fwd_bkwd (agents.py:32-40) with the backward of up to
+ * 16,384 samples of calls batched into one pass.  All calls of an epoch use theta_t
+ * (main.py:154,159,169), so a call runs only its forward + CrossEntropyLoss now (the loss is what
+ * agents.py:40 returns) into workspace rows [row0, row0 + ceil(n/128)*128); x, y, workers and
+ * worker_loss as for flsim_pn1_fwd_bwd_input.  row0 is a multiple of 128; max_samples <= 16384. */
+int flsim_pn1_fwd_rows(void* gradstate, void* workspace, int max_samples, int row0,
+                       const float* theta, const float* x, const int64_t* y, int n_samples,
+                       const WorkerRec* workers, uint64_t seed, int dropout, float* worker_loss,
+                       flsim_stream_t stream);
+/* ...then one backward over rows [0, n_rows) (the same theta and dropout flag as their forwards)
+ * adds every call's gradient to the epoch's slabs (agents.py:35 accumulation).  It runs on the
+ * gradstate's backward stream after everything queued on `stream`, so the next chunk's forwards
+ * (into a second workspace) overlap it; every other flsim_pn1_* entry point joins it first, and a
+ * flsim_pn1_fwd_rows into the same workspace waits for it. */
+int flsim_pn1_bwd_rows(void* gradstate, void* workspace, int max_samples, int n_rows,
+                       const float* theta, int dropout, flsim_stream_t stream);
 /* explicit batch variant (Worker.fwd_bkwd(inp, outp), agents.py:32): x NCHW fp32 [n][3][32][32],
  * y int64 [n], any n >= 1 (main.py:43-44 --batch_size; at most 16384): padded to whole groups of
  * 128 samples that add nothing; the gradient is CrossEntropyLoss's mean over the n samples

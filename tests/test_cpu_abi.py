@@ -114,3 +114,34 @@ def test_schedule_empty_epoch_raises_like_rule():
     s = Schedule(1, np.array([5], np.int32), False)
     with pytest.raises(IndexError):
         s.next_epoch()      # t=0: slow worker computes and pushes, nothing appended
+
+
+def test_comm_abi_one_rank_local():
+    """flsim_comm_* / flsim_allreduce_sum through the C-ABI: the one-rank local
+    communicator (no unique id, never touches RCCL) reduces in place to the identity; bad ranks,
+    a multi-rank communicator without a unique id and a null communicator are refused like the
+    other entry points (status 1 + flsim_last_error)."""
+    import ctypes
+
+    import torch
+    from flsim import _lib
+    from flsim.comm import Comm
+    L = _lib.lib()
+    c = Comm()
+    assert (c.size, c.rank) == (1, 0)
+    buf = torch.arange(7, dtype=torch.float32)
+    ref = buf.clone()
+    c.all_reduce_sum(buf)
+    assert torch.equal(buf, ref)
+    c.all_reduce_sum(torch.zeros(0))              # empty buffer: nothing to do
+    c.close()
+    h = ctypes.c_void_p()
+    for nranks, rank in ((1, 1), (0, 0), (2, -1), (2, 0)):   # (2, 0): no unique id
+        assert L.flsim_comm_create(nranks, rank, None, ctypes.byref(h)) == 1
+        assert not h.value
+        assert L.flsim_last_error()
+    assert L.flsim_allreduce_sum(None, None, 4, None) == 1
+    assert b"null communicator" in L.flsim_last_error()
+    assert L.flsim_comm_destroy(None) == 0
+    with pytest.raises(ValueError):
+        Comm(2, 0, b"short")

@@ -60,7 +60,7 @@ class StandInEngine:
 
 
 def _run(rank, world, n, d, thr, epochs, out, port, delays=None, semantics="reference",
-         force=False):
+         force=False, collective="torch"):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, os.path.dirname(here))
@@ -72,18 +72,44 @@ def _run(rank, world, n, d, thr, epochs, out, port, delays=None, semantics="refe
     from flsim.sim import FLSimulation
     sim = FLSimulation(n, delay=d, delays=delays, throttle=thr, device="cpu", semantics=semantics,
                        engine=StandInEngine(), device_pool=object(), theta0=torch.zeros(P),
-                       distributed=True if force else None)
+                       distributed=True if force else None, collective=collective)
     calls = []
     if force:                    # count the epoch's collectives (events are CUDA-only)
         inner = sim._all_reduce
         sim._all_reduce = lambda buf: (calls.append(buf.numel()), inner(buf))
+    abi = []
+    if sim._comm is not None:    # ... and the C-ABI's flsim_allreduce_sum calls among them
+        inner_c = sim._comm.all_reduce_sum
+        sim._comm.all_reduce_sum = lambda buf: (abi.append(buf.numel()), inner_c(buf))
     losses = [sim.epoch() for _ in range(epochs)]
     res = dict(theta=sim.theta.numpy().copy(), losses=losses,
                trace=[(p.t, p.computes.tobytes(), p.stale) for p in sim.trace],
-               distributed=sim.distributed, collectives=len(calls))
+               distributed=sim.distributed, collectives=len(calls), abi_calls=len(abi))
     if world > 1 or force:
         dist.destroy_process_group()
     out[rank] = res
+
+
+def test_forced_distributed_world1_flsim_collective():
+    """The same one-rank N > 1 path with the epoch's all-reduce through the C-ABI
+    (collective="flsim-local": flsim_allreduce_sum on the one-rank communicator) instead of
+    torch.distributed: one ABI call per epoch, the single-process trace, losses and theta."""
+    n, d, epochs = 11, 3, 5
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
+    single = mgr.dict()
+    _run(0, 1, n, d, True, epochs, single, 0)
+    out = mgr.dict()
+    port = 29500 + (os.getpid() % 1000) + 31
+    p = ctx.Process(target=_run, args=(0, 1, n, d, True, epochs, out, port, None, "reference",
+                                       True, "flsim-local"))
+    p.start()
+    p.join(300)
+    assert p.exitcode == 0
+    assert out[0]["collectives"] == epochs and out[0]["abi_calls"] == epochs
+    assert out[0]["trace"] == single[0]["trace"]
+    np.testing.assert_array_equal(out[0]["losses"], single[0]["losses"])
+    np.testing.assert_array_equal(out[0]["theta"], single[0]["theta"])
 
 
 @pytest.mark.parametrize("thr,delays", [

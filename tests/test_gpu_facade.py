@@ -94,11 +94,13 @@ def test_worker_batch_sizes_match_oracle(pool, n):
     _check_facade_step(g, model, x, y, keys, theta, n)
 
 
-def test_mixed_batch_sizes_in_one_epoch(pool):
-    """A 128-sample then a 256-sample batch in the same epoch: the engine grows between the
-    calls and the epoch's gradient keeps both (agents.py:35 keeps accumulating into .grad)."""
+def test_mixed_batch_sizes_in_one_epoch(pool, monkeypatch):
+    """A 128-sample then a 256-sample batch in the same epoch: the engine (a deferred chunk of one
+    128-sample group, FLSIM_FACADE_CHUNK=1) grows between the calls and the epoch's gradient
+    keeps both (agents.py:35 keeps accumulating into .grad)."""
     from FL.agents import Worker
     from oracle import model_ref as MR
+    monkeypatch.setenv("FLSIM_FACADE_CHUNK", "1")
     model, central = _fresh_central()
     ws = [Worker(nn.CrossEntropyLoss()) for _ in range(2)]
     model.train()
@@ -118,11 +120,12 @@ def test_mixed_batch_sizes_in_one_epoch(pool):
     assert all(p.grad.data_ptr() == t.data_ptr() for p, t in zip(model.parameters(), grads))
 
 
-def test_mixed_batch_sizes_untouched_grads(pool):
+def test_mixed_batch_sizes_untouched_grads(pool, monkeypatch):
     """The same two calls with no .grad read in between: the engine grows while the
-    128-sample gradient still sits in the old engine's slabs.  The epoch's gradient read after the
-    second call equals the one read with a flush between the calls, bit for bit."""
+    128-sample call is still a deferred forward (its backward not run).  The epoch's gradient
+    read after the second call equals the one read with a flush between the calls, bit for bit."""
     from FL.agents import Worker
+    monkeypatch.setenv("FLSIM_FACADE_CHUNK", "1")
 
     def run(read_between):
         model, central = _fresh_central()
@@ -285,3 +288,36 @@ def test_cifar10_binary_pool_through_hip_path(pool, tmp_path):
         assert abs(sim.epoch() - o2.epoch()) <= (1e-4 if t == 0 else 1e-3)
     acc, per = sim.evaluate()
     assert 0.0 <= acc <= 100.0 and len(per) == 10
+
+
+@pytest.mark.parametrize("defer", ["0", "128"])
+def test_two_calls_teacher_forced(pool, monkeypatch, defer):
+    """Two 128-sample fwd_bkwd calls, then a .grad read (agents.py:35 accumulation of both): with
+    the deferred backward (FLSIM_FACADE_CHUNK=128: one 256-row backward pass) and with a backward
+    per call (0), the epoch's gradient meets the teacher-forced fp64 checks and SURVEY 8(c) per
+    tensor (tests/_flips.py) on the two calls' own forward decisions."""
+    import _flips
+    from FL.agents import Worker
+    from oracle import model_ref as MR
+    monkeypatch.setenv("FLSIM_FACADE_CHUNK", defer)
+    model, central = _fresh_central()
+    ws = [Worker(nn.CrossEntropyLoss()) for _ in range(2)]
+    model.train()
+    theta = MR.init_params(0)
+    xs, ys, dec = [], [], []
+    grads = None
+    for i, w in enumerate(ws):
+        x, y = _batch(pool, 128, 40 + i)
+        w.model = model
+        grads, _ = w.fwd_bkwd(x.to(DEV), y.to(DEV))
+        xs.append(x)
+        ys.append(y)
+        if defer == "0":      # per call: each call's forward decisions are in its own workspace
+            dec.append(_flips.gpu_decisions(central.ctx.engine, 128))
+    g = torch.cat([t.reshape(-1) for t in grads]).cpu().numpy().astype(np.float64)
+    x, y = torch.cat(xs), torch.cat(ys)
+    noise = _flips.noise_groups([(0, 0), (0, 1)], 256)
+    if defer == "0":
+        forced = {k: torch.cat([dec[0][k], dec[1][k]]) for k in dec[0]}
+        monkeypatch.setattr(_flips, "gpu_decisions", lambda eng, n, rows=None: forced)
+    _flips.check_worker_step(g, central.ctx.engine, theta, x, y, noise, 1.0 / 128)

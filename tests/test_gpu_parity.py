@@ -201,7 +201,11 @@ def test_small_chunk_tiles_bit_identical(pool):
     """Chunks of at most small_chunk_samples() (256) samples run the GEMMs on half-height tiles
     (net_kernels.h): the k order per output is the large tiles', so the forward -- and
     with it every worker's loss -- must be bit-identical.  Two workers (256 samples, small tiles)
-    against the same two inside a three-worker chunk (384 samples, large tiles)."""
+    against the same two inside a three-worker chunk (384 samples, large tiles).  Only the
+    forward is compared bit for bit: the weight gradients' split of the pixel range follows the
+    chunk size (wsplit), so a chunk's gradient bits depend on its size by design; its accuracy
+    is checked per tensor at every chunk size by the worker-step and chunk tests
+    (test_gpu_survey_chunk.py)."""
     import torch as T
     from flsim.data import DevicePool
     from flsim.engine import PN1Engine, worker_table
@@ -223,47 +227,6 @@ def test_small_chunk_tiles_bit_identical(pool):
     b = large[:2].cpu().numpy()
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), (a, b)
     assert np.all(np.isfinite(S.cpu().numpy()))
-
-
-def test_conv1_wgrad_fused_into_conv2_dgrad(pool, monkeypatch):
-    """FLSIM_C1_FUSE=1 (c1fuse.h, off by default: measured slower): conv1's weight and
-    bias gradients computed inside conv2's data-gradient launch.  Two chunks (the second
-    accumulates into the first's slab rows) against the unfused path: every other tensor of S_t
-    bit-identical, conv1's within 1e-5 rel-L2 (another summation order), and the fused first chunk
-    passes the teacher-forced check against fp64."""
-    import torch as T
-    from flsim.data import DevicePool
-    from flsim.engine import PN1Engine, worker_table
-    from oracle import model_ref as MR
-    import _flips
-    sim = MR.OracleSim(4, delay=2, pool=pool)
-    items = [(2, 0, 1), (2, 1, 3), (2, 3, 0)]
-    dpool = DevicePool(DEV, 0, pool)
-    theta = T.from_numpy(sim.theta.copy()).to(DEV)
-    out = {}
-    for fuse in ("0", "1"):
-        monkeypatch.setenv("FLSIM_C1_FUSE", fuse)
-        eng = PN1Engine(DEV, chunk_workers=2)
-        eng.begin_epoch(theta)
-        loss = T.zeros(3, device=DEV)
-        eng.run_chunk(theta, dpool, worker_table(items[:2], DEV), 2, 4, 0, True, loss[:2])
-        S1 = T.zeros(eng.P, device=DEV)
-        eng.end_epoch(S1)
-        if fuse == "1":          # teacher-forced against fp64, on this chunk's own activations
-            x, y, noise = _items_batch(sim, items[:2])
-            _flips.check_worker_step(S1.cpu().numpy().astype(np.float64), eng, sim.theta, x, y,
-                                     noise, 1.0 / 128)
-        eng.run_chunk(theta, dpool, worker_table(items[2:], DEV), 1, 4, 0, True, loss[2:])
-        S = T.zeros(eng.P, device=DEV)
-        eng.end_epoch(S)
-        T.cuda.synchronize()
-        out[fuse] = (S1.cpu().numpy(), S.cpu().numpy(), loss.cpu().numpy())
-    n1 = 48 * 3 * 9 + 48                                  # conv1.weight, conv1.bias come first
-    for a, b in ((out["0"][0], out["1"][0]), (out["0"][1], out["1"][1])):
-        assert np.array_equal(a[n1:].view(np.uint32), b[n1:].view(np.uint32))
-        assert _rel_l2(b[:n1 - 48].astype(np.float64), a[:n1 - 48].astype(np.float64)) <= 1e-5
-        assert _rel_l2(b[n1 - 48:n1].astype(np.float64), a[n1 - 48:n1].astype(np.float64)) <= 1e-5
-    assert np.array_equal(out["0"][2], out["1"][2])       # the forward is untouched
 
 
 @pytest.mark.parametrize("thr", [False, True])

@@ -5,7 +5,11 @@
     bit for bit, for small chunks (weight gradients also on the side stream) and 32-worker ones;
   * the FL.agents facade with the pipelined fwd_bkwd (flsim_pn1_fwd_bwd_input_async) against the
     synchronous one: the same per-call losses, the same .grad values read between calls (the lazy
-    views join the backward stream), the same parameters after update_model (main.py:126-188).
+    views join the backward stream), the same parameters after update_model (main.py:126-188);
+  * the facade's deferred backward (flsim_pn1_fwd_rows / bwd_rows: each call's forward alone,
+    one batched backward per chunk of calls) against the per-call backward -- the same per-call
+    losses bit for bit, parameters within fp32 tolerance -- and against FLSimulation running the
+    same epochs: bit for bit when an epoch's calls form one chunk in both.
 """
 import numpy as np
 import pytest
@@ -44,14 +48,24 @@ def test_pipelined_chunks_match_sync(pool, n, chunk):
     assert torch.equal(wa, wb)
 
 
-def _loop(pool, pipeline, epochs=2, n=4, read_grads=False):
-    """The reference's loop (main.py:126-188 without the slow worker) through FL.agents."""
+def _loop(pool, pipeline, epochs=2, n=4, read_grads=False, defer="0"):
+    """The reference's loop (main.py:126-188 without the slow worker) through FL.agents.
+    defer: FLSIM_FACADE_CHUNK ("0": a backward per call, pipelined or not)."""
+    import os
     from FL.agents import Agg, Central, Worker, rule
     from FL.models import PerformantNet1
     from oracle import oracle as O
     torch.manual_seed(0)
     model = PerformantNet1().to(DEV)
-    central = Central(model, torch.optim.Adam(model.parameters(), lr=0.001))
+    old = os.environ.get("FLSIM_FACADE_CHUNK")
+    os.environ["FLSIM_FACADE_CHUNK"] = defer
+    try:
+        central = Central(model, torch.optim.Adam(model.parameters(), lr=0.001))
+    finally:
+        if old is None:
+            del os.environ["FLSIM_FACADE_CHUNK"]
+        else:
+            os.environ["FLSIM_FACADE_CHUNK"] = old
     central.ctx.pipeline = pipeline
     workers = [Worker(nn.CrossEntropyLoss()) for _ in range(n)]
     agg = Agg(rule)
@@ -83,3 +97,84 @@ def test_facade_pipelined_matches_sync(pool, read_grads):
         assert torch.equal(x, y)
     for name in ("theta", "m", "v"):
         assert torch.equal(getattr(ca, name), getattr(cb, name)), name
+
+
+@pytest.mark.parametrize("read_grads", [False, True])
+def test_facade_deferred_backward(pool, read_grads):
+    """Deferred chunk backward vs a backward per call: the forwards are the same kernels on the
+    same rows (losses bit-identical); the gradient differs only in summation order."""
+    ca, la, ga = _loop(pool, True, read_grads=read_grads, defer="0")
+    cb, lb, gb = _loop(pool, True, read_grads=read_grads, defer="128")
+    assert la == lb
+    for t, (x, y) in enumerate(zip(ga, gb)):
+        x, y = x.double(), y.double()
+        # epoch 0: the same theta, only the summation order differs (arithmetic, ~1e-7);
+        # epoch 1: theta after one Adam step can differ by +-2 lr where a gradient component is
+        # ~0 (its sign decides), which moves the next gradient further (SURVEY 7)
+        assert float((x - y).norm() / y.norm()) < (1e-6 if t == 0 else 1e-3), t
+    a, b = ca.theta[:ca.P].double(), cb.theta[:cb.P].double()
+    # two Adam steps: a near-zero gradient component can move by ~2 lr either way (SURVEY 7)
+    assert float((a - b).abs().max()) <= 4.1e-3
+    assert float((a - b).norm() / b.norm()) < 1e-2
+
+
+def test_deferred_facade_equals_simulation(pool, monkeypatch):
+    """main.py:126-188 through FL.agents (deferred backward) and FLSimulation on the same data,
+    dropout keys and schedule (n = 6, d = 3, throttle, 5 epochs): every epoch's calls form one
+    deferred chunk and one FLSimulation chunk, so per-worker losses and theta / m / v after every
+    epoch agree bit for bit -- the drop-in API runs the batched engine's own arithmetic."""
+    from FL.agents import Agg, Central, Worker, rule
+    from FL.models import PerformantNet1
+    from flsim.sim import FLSimulation
+    from oracle import oracle as O
+    monkeypatch.setenv("FLSIM_FACADE_CHUNK", "8")
+    n, d, ep = 6, 3, 5
+    sim = FLSimulation(n, delay=d, throttle=True, device=DEV, pool=pool, chunk_workers=8)
+    torch.manual_seed(0)
+    model = PerformantNet1().to(DEV)
+    central = Central(model, torch.optim.Adam(model.parameters(), lr=0.001))
+    ctx = central.ctx
+    assert torch.equal(ctx.theta[:ctx.P], sim.theta[:sim.P])
+    workers = [Worker(nn.CrossEntropyLoss()) for _ in range(n)]
+    agg = Agg(rule)
+    rs = np.random.RandomState(0)
+    lists = O.class_lists(pool[1])
+    lut = O.normalize_lut()
+    pesky, window, gone = [], 0, False
+    for t in range(ep):
+        sim.epoch()
+        ks = rs.randint(0, n, size=n)
+        weight_ups, call_losses = [], []
+        model.train()
+        for i in range(n):
+            idx = O.batch_indices(0, t, i, int(ks[i]), n, lists)
+            x = torch.from_numpy(lut[pool[0][idx]]).to(DEV)
+            y = torch.from_numpy(pool[1][idx]).to(DEV)
+            if i == n - 1:
+                gone = False
+                ups = None
+                if t == 0 or t % d == 0:
+                    workers[i].model = central.model
+                    ups, lv = workers[i].fwd_bkwd(x, y)
+                    call_losses.append(lv)
+                    pesky.append(ups)
+                    ups = pesky.pop(0) if t > 0 else None
+                if ups is not None:
+                    weight_ups.append(ups)
+                    gone = True
+            elif window <= 0:
+                workers[i].model = central.model
+                ups, lv = workers[i].fwd_bkwd(x, y)
+                call_losses.append(lv)
+                weight_ups.append(ups)
+                window = 1 if gone else 2
+            if window > 0:
+                window -= 1
+        central.update_model(agg.rule(weight_ups))
+        got = np.asarray([float(v) for v in call_losses], np.float32)
+        ref = sim.comm[sim.Ppad:sim.Ppad + len(got)].cpu().numpy()
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), (t, got, ref)
+        for name in ("theta", "m", "v"):
+            a = getattr(ctx, name)[:ctx.P]
+            b = getattr(sim, name)[:sim.P]
+            assert torch.equal(a, b), (t, name, int((a != b).sum()))

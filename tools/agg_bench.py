@@ -4,6 +4,9 @@ from S_t in a buffer [+ the FIFO slot write]) at PerformantNet1's P, for the str
 thread).  Bytes are SURVEY 8(d)'s: 4P (1 + distinct stale + 3 + 3) [+ 4P for the slot write].
 
   python tools/agg_bench.py [--iters 50]
+
+FLSIM_AGG_G acts only in a lab build of the library (make LAB=1, csrc/common.h): point FLSIM_LIB at
+one to compare the variants; the product build runs its default stream.
 """
 import argparse
 import json

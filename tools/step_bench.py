@@ -4,6 +4,8 @@ the whole plan and each segment alone (FLSIM_STEP_UNITS), reduce-only and with r
   python tools/step_bench.py
 Prints per segment: units, slab MB, time (us), algorithmic GB/s.  Modes: ref (reference order,
 k = 513), seq (k = 8100 with 72 stale entries among 6 arrays), c3 [T] (configs[3]'s epoch T).
+The per-segment runs (FLSIM_STEP_UNITS, FLSIM_STEP_NO_INTERLEAVE) need a lab build of the library
+(make LAB=1, csrc/common.h) under FLSIM_LIB.
 """
 import os
 import sys
