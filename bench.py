@@ -35,10 +35,12 @@ MFMA_F32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: fp32 matrix (v_mfma_f32_
 # the split-bf16 GEMMs (gemm_x6.h) issue six bf16 products per fp32 product on the bf16 matrix
 # cores (~2.5 PF/s dense, MI355X_MICROARCH.md): their fp32-equivalent peak
 MFMA_X6_PEAK_TFLOPS = 2500.0 / 6
-# probe names of the GEMMs that run on gemm_x6_kernel (pn1_net.hip, vgg_net.hip)
-# (every data gradient runs on the fp32 MFMA since round 5: DESIGN 7)
-X6_KERNELS = {f"conv{i}_{p}" for i in range(2, 7) for p in ("fwd", "wgrad")} | \
-    {"linear1_fwd", "linear1_wgrad"}
+# probe names of the GEMMs that run on gemm_x6_kernel (pn1_net.hip, vgg_net.hip): the forwards
+# and the linear weight gradients.  Every data gradient runs on the fp32 MFMA since round 5, every
+# conv weight gradient since round 6
+X6_KERNELS = {f"conv{i}_fwd" for i in range(2, 7)} | {"linear1_fwd", "linear1_wgrad"}
+VGG_X6_KERNELS = {f"vgg_conv{i}_fwd" for i in range(1, 9)} | \
+    {f"vgg_linear{i}_{p}" for i in (1, 2) for p in ("fwd", "wgrad")}
 HBM_PEAK_GBPS = 8000.0           # MI355X_MICROARCH.md: HBM3E spec
 
 
@@ -338,7 +340,7 @@ def main():
         achieved = fl / cnt / avg_s / 1e12
         gemm_ms = sum(v[1] for v in kern.values())
         gemm_fl = sum(v[2] for v in kern.values())
-        x6 = name in X6_KERNELS or (name.startswith("vgg") and not name.endswith("_dgrad"))
+        x6 = name in X6_KERNELS or name in VGG_X6_KERNELS
         traffic = TRAFFIC.get(name) if args.model == "PerformantNet1" else None
         if traffic and x6 and traffic.get("math") != "bf16x6":
             traffic = None      # profiles/traffic.json was counted on the fp32 kernel
@@ -443,9 +445,10 @@ def main():
             # fp32 in, fp32 accumulate; the k-contiguous convolution GEMMs split each fp32 operand
             # into three bf16 parts and sum six exact partial products on the bf16 matrix cores
             # (gemm_x6.h): fp32 accuracy, not a reduced-precision mode
-            "math": "bf16x6 split of the fp32 operands, fp32 accumulate (conv2-6 forward and "
-                    "weight gradients, linear1 forward and weight gradient; VGG forward and weight "
-                    "gradients); fp32 MFMA for the rest, every data gradient included",
+            "math": "bf16x6 split of the fp32 operands, fp32 accumulate (conv2-6 forwards, "
+                    "linear1 forward and weight gradient; VGG forwards and linear weight "
+                    "gradients); fp32 MFMA for the rest: every data gradient and every conv "
+                    "weight gradient",
             "data": f"synthetic: seeded CIFAR-shaped u8 pool in HBM, "
                     + (f"{args.model} warm-started from {os.path.basename(args.model_file)}"
                        if args.model_file else f"models.py-init {args.model}")
