@@ -342,8 +342,8 @@ def main():
         gemm_fl = sum(v[2] for v in kern.values())
         x6 = name in X6_KERNELS or name in VGG_X6_KERNELS
         traffic = TRAFFIC.get(name) if args.model == "PerformantNet1" else None
-        if traffic and x6 and traffic.get("math") != "bf16x6":
-            traffic = None      # profiles/traffic.json was counted on the fp32 kernel
+        if traffic and traffic.get("math") != ("bf16x6" if x6 else "fp32"):
+            traffic = None      # profiles/traffic.json was counted on the other kernel
         peak = MFMA_X6_PEAK_TFLOPS if x6 else MFMA_F32_PEAK_TFLOPS
         roofline = dict(bound="mfma", kernel=name, achieved=round(achieved, 2),
                         peak=round(peak, 1), unit="TFLOP/s",
