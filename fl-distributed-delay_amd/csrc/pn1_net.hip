@@ -321,6 +321,10 @@ static int conv1_fwd(const float* x0, const float* W, const float* bias, XsT a1,
 // 7.24 ms for 32-row waves, 8 per block (profiles/r04/r04j/lab_fwd2.txt, "fwd2v e")
 constexpr int DX_FM = 2, DX_KB = 3, DX_DEPTH = 2, DX_NPL = 2;
 
+// (One-call passes, the facade's 128-sample forwards, on quarter-height 64-row blocks: bit-identical
+// and 8 % slower on the facade loop, 748 / 746 against 814 / 804 worker-steps/s, E A E A on one box,
+// profiles/r06/facade/facade_tiny_ab: more blocks each staging the same B panel.  Not kept.)
+
 template <int IH, int IW, int CI, int PAD, int FN, bool WIN, int OHX, int FM = DX_FM,
           int WAVES = 8, class EPI>
 static int dx6(XsT X, int S, XsT W, int N, int KP, const EPI& epi, hipStream_t st, int kid,

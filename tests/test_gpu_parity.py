@@ -200,8 +200,9 @@ def test_chunk_of_workers_sums_gradients(pool):
 def test_small_chunk_tiles_bit_identical(pool):
     """Chunks of at most small_chunk_samples() (256) samples run the GEMMs on half-height tiles
     (net_kernels.h): the k order per output is the large tiles', so the forward -- and
-    with it every worker's loss -- must be bit-identical.  Two workers (256 samples, small tiles)
-    against the same two inside a three-worker chunk (384 samples, large tiles).  Only the
+    with it every worker's loss -- must be bit-identical.  One worker (128 samples: the facade's
+    one-call forward, flsim_pn1_fwd_rows) and two workers (256 samples), both on the small tiles,
+    against the same workers inside a three-worker chunk (384 samples, large tiles).  Only the
     forward is compared bit for bit: the weight gradients' split of the pixel range follows the
     chunk size (wsplit), so a chunk's gradient bits depend on its size by design; its accuracy
     is checked per tensor at every chunk size by the worker-step and chunk tests
@@ -216,8 +217,10 @@ def test_small_chunk_tiles_bit_identical(pool):
     dpool = DevicePool(DEV, 0, pool)
     theta = T.from_numpy(sim.theta.copy()).to(DEV)
     eng.begin_epoch(theta)
+    tiny = T.zeros(1, device=DEV)
     small = T.zeros(2, device=DEV)
     large = T.zeros(3, device=DEV)
+    eng.run_chunk(theta, dpool, worker_table(items[:1], DEV), 1, 4, 0, True, tiny)
     eng.run_chunk(theta, dpool, worker_table(items[:2], DEV), 2, 4, 0, True, small)
     eng.run_chunk(theta, dpool, worker_table(items, DEV), 3, 4, 0, True, large)
     S = T.zeros(eng.P, device=DEV)
@@ -225,7 +228,9 @@ def test_small_chunk_tiles_bit_identical(pool):
     T.cuda.synchronize()
     a = small.cpu().numpy()
     b = large[:2].cpu().numpy()
+    c = tiny.cpu().numpy()
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), (a, b)
+    assert np.array_equal(c.view(np.uint32), b[:1].view(np.uint32)), (c, b)
     assert np.all(np.isfinite(S.cpu().numpy()))
 
 

@@ -205,13 +205,13 @@ def test_vgg11_oracle_trajectory(golden):
     sim = MR.OracleSim(3, delay=2, throttle=True, pool=(imgs, labels), model="vgg11")
     for t, ref in enumerate(g["train_losses"]):
         loss = sim.epoch()
-        # host-CPU fp32 drift after the first Adam steps, as in test_training_trajectory: exact
-        # at epochs 0-1, 2.1e-5 at epoch 2 on one build host; other EPYC hosts drift further
-        # (PerformantNet1: 1.2e-4 by epoch 4, running_mean 8e-4 / 1.6e-3 below), so the bound
-        # follows that cross-host spread, not one host's figure
+        # host-CPU fp32 drift after the first Adam steps (the fixture was made on a Xeon host):
+        # exact at epoch 0, <= 2.4e-7 at epoch 1, 5.94e-5 at epoch 2 measured on both EPYC hosts
+        # this test runs on (this container and the GPU box, profiles/r06/r06f/cpu_drift.txt);
+        # bound 1.5 x that
         print("MEASURED", json.dumps(dict(test="vgg11_oracle_trajectory", epoch=t,
                                           loss_drift=abs(loss - float(ref)))))
-        assert abs(loss - ref) <= (1e-5 if t < 2 else 5e-4), (t, loss, ref)
+        assert abs(loss - ref) <= (1e-5 if t < 2 else 9e-5), (t, loss, ref)
         np.testing.assert_allclose(
             [float((a.astype(np.float64) ** 2).sum()) for a in MR.split_flat(sim.theta, "vgg11")],
             g[f"train_theta{t}_stats"][:, 1], rtol=1e-3)
@@ -264,13 +264,12 @@ def test_vgg11_bn_oracle_trajectory_and_eval(golden):
     sim = MR.OracleSim(3, delay=2, throttle=True, pool=(imgs, labels), model="vgg11_bn")
     for t, ref in enumerate(g["train_losses"]):
         loss = sim.epoch()
-        # host-CPU fp32 drift after the first Adam steps, as in test_training_trajectory: exact
-        # at epochs 0-1, 2.1e-5 at epoch 2 on one build host; other EPYC hosts drift further
-        # (PerformantNet1: 1.2e-4 by epoch 4, running_mean 8e-4 / 1.6e-3 below), so the bound
-        # follows that cross-host spread, not one host's figure
+        # host-CPU fp32 drift after the first Adam steps: exact at epochs 0-1, 2.09e-5 at epoch 2
+        # on both EPYC hosts this test runs on (2.1e-5 on the Xeon host that made the fixture,
+        # profiles/r06/r06f/cpu_drift.txt); bound 1.5 x that
         print("MEASURED", json.dumps(dict(test="vgg11_bn_oracle_trajectory", epoch=t,
                                           loss_drift=abs(loss - float(ref)))))
-        assert abs(loss - ref) <= (1e-5 if t < 2 else 5e-4), (t, loss, ref)
+        assert abs(loss - ref) <= (1e-5 if t < 2 else 3.2e-5), (t, loss, ref)
         np.testing.assert_allclose(
             [float((a.astype(np.float64) ** 2).sum())
              for a in MR.split_flat(sim.theta, "vgg11_bn")][2::4],     # BatchNorm weights
