@@ -34,7 +34,7 @@
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int K = 1728, N = 192, KB = K / 64;
-constexpr int BROWS = 64, BCOLS = 64;          // block tile; 4 waves of 16 rows x 64 columns
+constexpr int BROWS = 64, BCOLS = 64;          // block tile per row fragment: 4 waves x 16 rows
 constexpr int LDB = 64 + 16;                   // LDS row stride (bytes) of a B slice plane
 
 // per-row exponents: e = ilogb(max |x|) + 2 (0 for an all-zero row)
@@ -59,21 +59,23 @@ __global__ void k_slice(const float* X, int rows, const int* e, int S, signed ch
     }
 }
 
-// C[M][N] = A[M][K] B[N][K]^T from the slices; grid (M / 64) x (N / 64), 256 threads
-template <int S>
+// C[M][N] = A[M][K] B[N][K]^T from the slices; 4 waves, each RF x 16 rows x 64 columns (RF row
+// fragments share each B fragment read from LDS); grid (M / (64 RF)) x (N / 64)
+template <int S, int RF>
 __global__ void __launch_bounds__(256) k_gemm(const signed char* qa, const signed char* qb,
                                               const int* ea, const int* eb, float* C, int M) {
     constexpr int NCLS = S;                    // classes c = i + j = 2 .. S + 1
     __shared__ __attribute__((aligned(16))) signed char sb[2][S][BCOLS * LDB];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int m0 = blockIdx.x * BROWS, n0 = blockIdx.y * BCOLS;
+    const int m0 = blockIdx.x * BROWS * RF, n0 = blockIdx.y * BCOLS;
     const int i = lane & 15, g = lane >> 4;
-    const int row = m0 + 16 * wave + i;
-    i32x4 acc[NCLS][4];
+    i32x4 acc[NCLS][RF][4];
 #pragma unroll
     for (int c = 0; c < NCLS; ++c)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[c][j] = i32x4{0, 0, 0, 0};
+        for (int f = 0; f < RF; ++f)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[c][f][j] = i32x4{0, 0, 0, 0};
     // B staging: 64 columns x 64 k bytes per slice = 256 x 16 B: thread -> (column, 16-B chunk)
     const int scol = tid >> 2, sch = tid & 3;
     auto stage = [&](int kb, int buf) {
@@ -84,16 +86,33 @@ __global__ void __launch_bounds__(256) k_gemm(const signed char* qa, const signe
             *reinterpret_cast<i32x4*>(&sb[buf][t][scol * LDB + 16 * sch]) = v;
         }
     };
+    // A's slices come straight from global memory (each lane 16 B per slice: one row, 16 k),
+    // loaded one k-block ahead so their latency hides behind the current block's MFMAs
+    auto load_a = [&](int kb, i32x4 (&a)[RF][S]) {
+#pragma unroll
+        for (int f = 0; f < RF; ++f) {
+            const int row = m0 + (wave * RF + f) * 16 + i;
+#pragma unroll
+            for (int t = 0; t < S; ++t)
+                a[f][t] = *reinterpret_cast<const i32x4*>(qa + (long)t * M * K + (long)row * K +
+                                                           kb * 64 + 16 * g);
+        }
+    };
+    i32x4 an[RF][S];
+    load_a(0, an);
     stage(0, 0);
     __syncthreads();
     for (int kb = 0; kb < KB; ++kb) {
         const int cur = kb & 1;
-        if (kb + 1 < KB) stage(kb + 1, cur ^ 1);
-        i32x4 a[S];
+        i32x4 a[RF][S];
 #pragma unroll
-        for (int t = 0; t < S; ++t)
-            a[t] = *reinterpret_cast<const i32x4*>(qa + (long)t * M * K + (long)row * K + kb * 64 +
-                                                    16 * g);
+        for (int f = 0; f < RF; ++f)
+#pragma unroll
+            for (int t = 0; t < S; ++t) a[f][t] = an[f][t];
+        if (kb + 1 < KB) {
+            load_a(kb + 1, an);
+            stage(kb + 1, cur ^ 1);
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             i32x4 b[S];
@@ -101,30 +120,34 @@ __global__ void __launch_bounds__(256) k_gemm(const signed char* qa, const signe
             for (int t = 0; t < S; ++t)
                 b[t] = *reinterpret_cast<const i32x4*>(&sb[cur][t][(16 * j + i) * LDB + 16 * g]);
 #pragma unroll
-            for (int ti = 0; ti < S; ++ti)
+            for (int f = 0; f < RF; ++f)
 #pragma unroll
-                for (int tj = 0; tj < S; ++tj)
-                    if (ti + tj <= S - 1)      // slices 1-based: (ti+1) + (tj+1) <= S + 1
-                        acc[ti + tj][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(
-                            a[ti], b[tj], acc[ti + tj][j], 0, 0, 0);
+                for (int ti = 0; ti < S; ++ti)
+#pragma unroll
+                    for (int tj = 0; tj < S; ++tj)
+                        if (ti + tj <= S - 1)  // slices 1-based: (ti+1) + (tj+1) <= S + 1
+                            acc[ti + tj][f][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(
+                                a[f][ti], b[tj], acc[ti + tj][f][j], 0, 0, 0);
         }
         __syncthreads();
     }
     // C = 2^(eA + eB) sum_c 2^-7(c+2) acc_c; output layout: col = lane & 15, row = 4 g + r
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int col = n0 + 16 * j + i;
-        const int ecol = eb[col];
+    for (int f = 0; f < RF; ++f)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int orow = m0 + 16 * wave + 4 * g + r;
-            float v = 0.f;
+        for (int j = 0; j < 4; ++j) {
+            const int col = n0 + 16 * j + i;
+            const int ecol = eb[col];
 #pragma unroll
-            for (int c = NCLS - 1; c >= 0; --c)      // smallest terms first
-                v += ldexpf((float)acc[c][j][r], -7 * (c + 2));
-            C[(long)orow * N + col] = ldexpf(v, ea[orow] + ecol);
+            for (int r = 0; r < 4; ++r) {
+                const int orow = m0 + (wave * RF + f) * 16 + 4 * g + r;
+                float v = 0.f;
+#pragma unroll
+                for (int c = NCLS - 1; c >= 0; --c)      // smallest terms first
+                    v += ldexpf((float)acc[c][f][j][r], -7 * (c + 2));
+                C[(long)orow * N + col] = ldexpf(v, ea[orow] + ecol);
+            }
         }
-    }
 }
 
 // references on the first R rows: fp64 dot, and a sequential fp32 fmaf chain
@@ -156,7 +179,7 @@ static Err err_of(const float* c, const double* r, int R) {
     return Err{sqrt(e2 / r2), er / r2, sqrt(ce / cr)};
 }
 
-template <int S>
+template <int S, int RF>
 static void run(int M, const float* dA, const float* dB, const int* ea, const int* eb,
                 const double* r64, const std::vector<float>& h32, int R) {
     signed char *qa, *qb;
@@ -167,15 +190,15 @@ static void run(int M, const float* dA, const float* dB, const int* ea, const in
     k_slice<<<(unsigned)(((long)M * K + 255) / 256), 256>>>(dA, M, ea, S, qa);
     k_slice<<<(N * K + 255) / 256, 256>>>(dB, N, eb, S, qb);
     CK(hipDeviceSynchronize());
-    const dim3 grid(M / BROWS, N / BCOLS);
-    k_gemm<S><<<grid, 256>>>(qa, qb, ea, eb, C, M);     // warm-up
+    const dim3 grid(M / (BROWS * RF), N / BCOLS);
+    k_gemm<S, RF><<<grid, 256>>>(qa, qb, ea, eb, C, M);     // warm-up
     CK(hipDeviceSynchronize());
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     const int it = 10;
     CK(hipEventRecord(e0));
-    for (int r = 0; r < it; ++r) k_gemm<S><<<grid, 256>>>(qa, qb, ea, eb, C, M);
+    for (int r = 0; r < it; ++r) k_gemm<S, RF><<<grid, 256>>>(qa, qb, ea, eb, C, M);
     CK(hipEventRecord(e1));
     CK(hipEventSynchronize(e1));
     float ms = 0;
@@ -187,10 +210,10 @@ static void run(int M, const float* dA, const float* dB, const int* ea, const in
     CK(hipMemcpy(hr.data(), r64, hr.size() * 8, hipMemcpyDeviceToHost));
     const Err e = err_of(hc.data(), hr.data(), R), f = err_of(h32.data(), hr.data(), R);
     const double tf = 2.0 * M * N * K / (ms * 1e-3) / 1e12;
-    printf("S=%d  products %2d  issue-bound peak %6.0f TF/s | %8.3f ms  %6.1f TF/s  (x %.1f to a "
+    printf("S=%d RF=%d  products %2d  issue-bound peak %6.0f TF/s | %8.3f ms  %6.1f TF/s  (x %.1f to a "
            "16,384-sample conv6 launch: %.2f ms) | rel %.2e alpha %+.1e colsum %.2e  [fp32 chain: "
            "rel %.2e alpha %+.1e colsum %.2e]\n",
-           S, S * (S + 1) / 2, 5000.0 / (S * (S + 1) / 2), ms, tf, 16384.0 * 169 / M,
+           S, RF, S * (S + 1) / 2, 5000.0 / (S * (S + 1) / 2), ms, tf, 16384.0 * 169 / M,
            ms * 16384.0 * 169 / M, e.rel, e.alpha, e.colsum, f.rel, f.alpha, f.colsum);
     CK(hipFree(qa));
     CK(hipFree(qb));
@@ -232,9 +255,12 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(h32.data(), r32, h32.size() * 4, hipMemcpyDeviceToHost));
     printf("M = %d rows, N = %d, K = %d (conv6 data gradient; the product's fp32 direct kernel: "
            "12.7 ms per 16,384-sample launch, 140 TF/s)\n", M, N, K);
-    run<3>(M, dA, dB, ea, eb, r64, h32, R);
-    run<4>(M, dA, dB, ea, eb, r64, h32, R);
-    run<5>(M, dA, dB, ea, eb, r64, h32, R);
-    run<6>(M, dA, dB, ea, eb, r64, h32, R);
+    run<3, 1>(M, dA, dB, ea, eb, r64, h32, R);
+    run<3, 2>(M, dA, dB, ea, eb, r64, h32, R);
+    run<4, 1>(M, dA, dB, ea, eb, r64, h32, R);
+    run<4, 2>(M, dA, dB, ea, eb, r64, h32, R);
+    run<5, 1>(M, dA, dB, ea, eb, r64, h32, R);
+    run<5, 2>(M, dA, dB, ea, eb, r64, h32, R);
+    run<6, 1>(M, dA, dB, ea, eb, r64, h32, R);
     return 0;
 }
