@@ -79,6 +79,15 @@ constexpr bool x6_fresh(bool kc) {
 }
 constexpr bool x6_fresh_bias() { return FLSIM_X6_FRESH >= 2; }
 
+// The k-major GEMMs (weight gradients: K = the chunk's pixels, up to 3.2M) flush their running
+// MFMA sums into an fp32 total every X6_FLUSH k-steps (and restart them from zero), so the bf16
+// MFMA's truncation only ever acts against a 16 * X6_FLUSH-pixel partial sum: the bias it leaves
+// stays at the short chain's (tools/lab/wg_numerics.hip: 1.5e-7 rel-L2 for 512-pixel chains
+// against 1.6e-6 for 16,384-pixel ones) instead of growing with K.  0: no flush.
+#ifndef FLSIM_X6_FLUSH
+#define FLSIM_X6_FLUSH 0
+#endif
+
 // Main-loop schedule of the k-contiguous GEMMs (both tiles KC: the staged forwards): the staging
 // of the next k-step interleaved with the current k-step's MFMAs by sched_group_barrier, per MFMA
 // V VALU, an LDS store every W MFMAs, a global load every L, in a branch-free loop body.  Lab
@@ -324,6 +333,17 @@ gemm_x6_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, in
     // profiles/r05/ab/x6_interleave_km.txt: removed)
     constexpr bool PP = PP_KC;
     constexpr int PV = X6_PP_V, PW = X6_PP_W, PL = X6_PP_L;
+    constexpr int FLUSH = AL::KC ? 0 : FLSIM_X6_FLUSH;
+    f32x4 tot[FLUSH ? FM : 1][FLUSH ? FN : 1];
+    f32x4 btot[FLUSH && AMF ? FM : 1];
+    if constexpr (FLUSH > 0) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+#pragma unroll
+            for (int j = 0; j < FN; ++j) tot[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if constexpr (AMF) btot[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
     auto main_loop = [&](auto with_sum) {
         constexpr bool WS = decltype(with_sum)::value;
         for (int ks = ks0; ks < ks1; ++ks) {
@@ -382,6 +402,22 @@ gemm_x6_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, in
                     if (n % PL == 1 % PL) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
                 }
             }
+            if constexpr (FLUSH > 0) {
+                if ((ks - ks0) % FLUSH == FLUSH - 1) {        // block-uniform
+#pragma unroll
+                    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+                        for (int j = 0; j < FN; ++j) {
+                            tot[i][j] += acc[i][j];
+                            acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+                        }
+                        if constexpr (WS && AMF) {
+                            btot[i] += bacc[i];
+                            bacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+                        }
+                    }
+                }
+            }
             __syncthreads();
             cur ^= 1;
         }
@@ -395,6 +431,14 @@ gemm_x6_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, in
     else if constexpr (EPI::ASUM) sum_wave = tn == 0 && wave * 64 < BM;
     if (sum_wave) main_loop(std::true_type{});
     else main_loop(std::false_type{});
+    if constexpr (FLUSH > 0) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+#pragma unroll
+            for (int j = 0; j < FN; ++j) acc[i][j] = tot[i][j] + acc[i][j];
+            if constexpr (AMF) bacc[i] = btot[i] + bacc[i];
+        }
+    }
 
     if constexpr (AMF) {
         // every column of the ones product is the row sum: lanes of column 0 store it

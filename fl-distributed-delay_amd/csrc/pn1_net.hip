@@ -543,6 +543,12 @@ static bool concurrent_backward(int S) {
 #endif
 constexpr int DG_FMS = FLSIM_DG_FMS;
 
+// conv2-6 weight gradients on the split-bf16 GEMM (1) or the fp32 one (0); the split form needs
+// the flushed accumulation (gemm_x6.h FLSIM_X6_FLUSH) to meet SURVEY 8(c) at the chunk's K
+#ifndef FLSIM_WGRAD_X6
+#define FLSIM_WGRAD_X6 0
+#endif
+
 // debug / measurement: FLSIM_DEBUG_BWD_STOP=6 / 5 / 4 / 3 ends the backward pass after conv6's /
 // conv5's / conv4's / conv3's data gradient (dz5 in gx; dz4 in a4, dz5 in gx; dz3 in gx, dz4 in
 // a4; dz2 in a2, dz3 in gx; all fp32), so each GEMM can be checked on its own inputs
@@ -618,9 +624,15 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     // (192 x 192 tiles of 8 waves ran 9.10-9.13 against 9.41 ms in the lab,
     // profiles/r04/r04l/lab_wg6v.txt, but 9.26-9.29 against 9.10-9.12 in the product, A B A B on
     // one box, profiles/r04/r04s: kept 192 x 96)
+#if FLSIM_WGRAD_X6
+    RC((conv_wgrad_sz<13, 13, 192, 2, 6, 3, 2, 2, 3, 3, 2, 2, 14, true, true, BufSrc, XsSrc>(
+        dz6, w.a5, S, 192, 1728, g.sw[5], g.sb[5], GEO[5].ZW, sw, K_WG6, 1728, zi(5), &zu[5],
+        nullptr, w.a5l)));
+#else
     RC((conv_wgrad<13, 13, 192, 2, 6, 3, 2, 4, 14, true, false, BufSrc, XsF32Src>(
         dz6, w.a5, S, 192, 1728, g.sw[5], g.sb[5], GEO[5].ZW, sw, K_WG6, 1728, zi(5), &zu[5],
         nullptr, w.a5l)));
+#endif
     // (every data gradient runs on the fp32 MFMA: the bf16 MFMA truncates small addends toward
     // zero, which biases the per-channel sums of its outputs 30-100x beyond the CPU fp32 port's
     // and failed SURVEY 8(c) on conv1-4, conv6's alone too (tools/gemm_diag.py))
@@ -630,9 +642,15 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     // ---- conv5: wgrad (input d2), bias, dgrad -> grad wrt d2 (dropout site 2), scattered through
     //      pool2 straight into dz4 (a4 buffer; no gy round trip) ----
     RC(fork());
+#if FLSIM_WGRAD_X6
+    RC((conv_wgrad_sz<11, 11, 96, 2, 6, 3, 2, 2, 3, 3, 2, 2, 0, false, true, BufSrc, XsSrc>(
+        dz5, w.d2, S, 192, 864, g.sw[4], g.sb[4], GEO[4].ZW, sw, K_WG5, 864, zi(4), &zu[4],
+        nullptr, w.d2l)));
+#else
     RC((conv_wgrad<11, 11, 96, 2, 6, 3, 2, 2, 0, false, false, BufSrc, XsF32Src>(
         dz5, w.d2, S, 192, 864, g.sw[4], g.sb[4], GEO[4].ZW, sw, K_WG5, 864, zi(4), &zu[4],
         nullptr, w.d2l)));
+#endif
     RC((conv_direct_sz<13, 13, 192, 0, 2, DG_FMS, 6, 8, 3, 2, false, 0>(dz5, S, g.wd[4], 96, 1728,
         EpiDropScatterXs<11, 11, 96, false>{dz4, nullptr, w.d2, w.i2, s25, S * 11 * 11}, st,
         K_DG5, 1728)));
@@ -644,7 +662,8 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     // gradients split dZ while staging (split-bf16 kernel over an fp32 dZ and a split layer input)
     RC(join());                                   // conv5's wgrad reads gx = dz5: done first
     RC(fork());
-    RC((conv_wgrad<20, 20, 96, 2, 3, 3, 2, 2, 0, false, false, BufSrc, XsF32SrcSM>(
+    RC((conv_wgrad<20, 20, 96, 2, 3, 3, 2, 2, 0, false, FLSIM_WGRAD_X6, BufSrc,
+                   std::conditional_t<FLSIM_WGRAD_X6, XsSrcSM, XsF32SrcSM>>(
         dz4, w.a3, S, 96, 864, g.sw[3], g.sb[3], GEO[3].ZW, sw, K_WG4, 864, zi(3), &zu[3],
         nullptr, w.a3l)));
     RC((conv_direct_sz<22, 22, 96, 0, 2, DG_FMS, 6, 8, 3, 2, false, 0>(dz4, S, g.wd[3], 96, 864,
@@ -655,9 +674,15 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     //      straight into dz2 (a2 buffer, fp32) ----
     RC(fork());
     // (96 x 96 tiles of 4 waves: 2.96 against 3.54 ms for 96 x 48 of 2, profiles/r04/r04j/lab_wg.txt)
+#if FLSIM_WGRAD_X6
+    RC((conv_wgrad_sz<18, 18, 48, 2, 3, 3, 2, 2, 3, 3, 2, 2, 0, false, true, BufSrc, XsSrcSM>(
+        dz3, w.d1, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW, sw, K_WG3, 432, zi(2), &zu[2],
+        nullptr, w.d1l)));
+#else
     RC((conv_wgrad<18, 18, 48, 2, 3, 3, 2, 1, 0, false, false, BufSrc, XsF32SrcSM>(
         dz3, w.d1, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW, sw, K_WG3, 432, zi(2), &zu[2],
         nullptr, w.d1l)));
+#endif
     // (gemm_kernel: the direct-A form measured 3.87 vs 3.78 ms with this staged epilogue, r03b)
     RC((conv_like_sz<20, 20, 96, 0, 4, 2, 3, 4, 1>(dz3, S, g.wd[2], 48, 864,
         EpiDropScatterXs<18, 18, 48, false, true>{w.a2, nullptr, w.d1, w.i1, s25, S * 18 * 18}, st,
@@ -667,9 +692,15 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     // ---- conv2: wgrad (input a1), bias, dgrad -> dz1 = . * (a1 > 0) into gx (fp32) ----
     RC(join());                                   // conv3's wgrad reads gx = dz3: done first
     RC(fork());
+#if FLSIM_WGRAD_X6
+    RC((conv_wgrad_sz<34, 34, 48, 2, 3, 3, 1, 3, 3, 3, 1, 3, 0, false, true, BufSrc, XsSrcSM>(
+        dz2, w.a1, S, 48, 432, g.sw[1], g.sb[1], GEO[1].ZW, sw, K_WG2, 432, zi(1), &zu[1],
+        nullptr, w.a1l)));
+#else
     RC((conv_wgrad<34, 34, 48, 2, 3, 3, 1, 1, 0, false, false, BufSrc, XsF32SrcSM>(
         dz2, w.a1, S, 48, 432, g.sw[1], g.sb[1], GEO[1].ZW, sw, K_WG2, 432, zi(1), &zu[1],
         nullptr, w.a1l)));
+#endif
     RC((conv_direct_sz<36, 36, 48, 0, 2, 1, 3, 8, 3, 2, false, 0>(dz2, S, g.wd[1], 48, 432,
         EpiMaskXs<48, false, true, 1156>{w.gx, nullptr, w.a1, S * 34 * 34}, st, K_DG2, 432)));
     float* dz1 = w.gx;

@@ -8,6 +8,8 @@
 #   benchq            the default bench line without the CPU baseline
 #   ab:<lib>          bench line of an alternative libflsim.so (FLSIM_LIB=<lib>) beside benchq
 #   abvgg:<lib>       configs[4] (vgg11, n = 4096, d = 1000) with an alternative libflsim.so, B A B A
+#   bl:<name>:<lib>  one bench line on another libflsim.so build (FLSIM_LIB)
+#   ltests:<lib>:<k> pytest -m gpu -k <k> on another build (tol_<build>.jsonl)
 #   abenv:<VAR=VAL>   bench line with one environment setting beside benchq (E1 A1 E2 A2)
 #   c1abenv:<VAR=VAL> the same on configs[1] (n = 10, d = 50, the warm start)
 #   trace             rocprofv3 --kernel-trace --stats of a short bench (kernel_stats.csv)
@@ -17,6 +19,7 @@
 #   gloo2             2-rank gloo rehearsal of the N > 1 path through bench.py (n = 256)
 #   forcedist         torchrun --nproc-per-node 1 bench.py --force-dist (RCCL at world size 1)
 #   sizes             the per-rank loads of an N-GPU job on one GPU: n = 128 / 256 / 512
+#   fwd1              tools/fwd1_bench.py (the facade's one-call forward alone)
 #   aggceil           tools/agg_ceiling.py (torch streams at the aggregation paths' sizes)
 #   facadeab:<VAR=VAL> the facade loop with one environment setting, E A E A
 #   facade            tools/facade_bench.py (the FL.agents reference loop, n = 1024)
@@ -93,6 +96,16 @@ for STEP in "$@"; do
         BENCH_ARGS="--model vgg11 --n_workers 4096 --delay 1000 --steps 4 --warmup 1"
         bench_line vB1 FLSIM_LIB=$LIB; bench_line vA1; bench_line vB2 FLSIM_LIB=$LIB; bench_line vA2
         BENCH_ARGS="" ;;
+    bl:*)          # bl:<name>:<lib> one bench line on another build of libflsim.so
+        SPEC=${STEP#bl:}; bench_line ${SPEC%%:*} FLSIM_LIB=${SPEC#*:} ;;
+    ltests:*)      # ltests:<lib>:<k-expr> pytest -m gpu -k <k-expr> on another build
+        SPEC=${STEP#ltests:}; LIB=${SPEC%%:*}; K=${SPEC#*:}; N=$(basename $(dirname $LIB))
+        FLSIM_LIB=$LIB FLSIM_TOL_LOG=$OUT/tol_$N.jsonl timeout -k 10 1000 python3 -u \
+            -m pytest tests -m gpu -v -s --timeout 600 --timeout-method thread -k "$K" \
+            > $OUT/pytest_$N.txt 2>&1
+        rc=$?
+        tail -2 $OUT/pytest_$N.txt; grep -E "^FAILED" $OUT/pytest_$N.txt | head
+        [ $rc -le 1 ] || { echo "pytest rc $rc: stopping"; exit $rc; } ;;
     abenv:*)
         KV=${STEP#abenv:}
         bench_line E1 $KV; bench_line A1; bench_line E2 $KV; bench_line A2 ;;
@@ -146,6 +159,10 @@ for STEP in "$@"; do
             python3 tools/bench_summary.py $OUT/bench_n$N.json > $OUT/bench_n$N.txt
             echo "n=$N: $(head -1 $OUT/bench_n$N.txt)"
         done ;;
+    fwd1)
+        timeout -k 10 200 python3 -u tools/fwd1_bench.py > $OUT/fwd1.json 2> $OUT/fwd1.err \
+            || { echo "fwd1 failed $?"; tail -5 $OUT/fwd1.err; exit 1; }
+        cat $OUT/fwd1.json ;;
     aggceil)
         timeout -k 10 300 python3 -u tools/agg_ceiling.py > $OUT/agg_ceiling.txt 2>&1 \
             || { echo "agg ceiling failed $?"; tail -5 $OUT/agg_ceiling.txt; exit 1; }
