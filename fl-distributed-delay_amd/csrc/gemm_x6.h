@@ -69,15 +69,16 @@ __device__ __forceinline__ f32x4 x6_step(f32x4 acc, f32x4 a0, f32x4 a1, f32x4 b0
 
 // Which accumulations are fresh (measurement levels, FLSIM_X6_FRESH): 0 none; 1 every x6 main
 // accumulator (round 4's experiment); 2 the k-contiguous GEMMs (forward and data gradients:
-// gemm_x6 with a KC A tile, gemm_dx6) and the bias column sums; 3 everything.
+// gemm_x6 with a KC A tile, gemm_dx6) and the bias column sums; 3 everything; 4 the k-major
+// (weight-gradient) GEMMs and the bias column sums; 5 the k-major GEMMs' main accumulation only.
 #ifndef FLSIM_X6_FRESH
 #define FLSIM_X6_FRESH 0
 #endif
 constexpr bool x6_fresh(bool kc) {
     return FLSIM_X6_FRESH == 1 || FLSIM_X6_FRESH == 3 || (FLSIM_X6_FRESH == 2 && kc) ||
-           (FLSIM_X6_FRESH == 4 && !kc);
+           ((FLSIM_X6_FRESH == 4 || FLSIM_X6_FRESH == 5) && !kc);
 }
-constexpr bool x6_fresh_bias() { return FLSIM_X6_FRESH >= 2; }
+constexpr bool x6_fresh_bias() { return FLSIM_X6_FRESH >= 2 && FLSIM_X6_FRESH != 5; }
 
 // The k-major GEMMs (weight gradients: K = the chunk's pixels, up to 3.2M) flush their running
 // MFMA sums into an fp32 total every X6_FLUSH k-steps (and restart them from zero), so the bf16

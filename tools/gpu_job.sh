@@ -163,6 +163,13 @@ for STEP in "$@"; do
         timeout -k 10 200 python3 -u tools/fwd1_bench.py > $OUT/fwd1.json 2> $OUT/fwd1.err \
             || { echo "fwd1 failed $?"; tail -5 $OUT/fwd1.err; exit 1; }
         cat $OUT/fwd1.json ;;
+    fwd1trace)
+        timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/f1trace -o run \
+            -- python3 tools/fwd1_bench.py --calls 200 > $OUT/fwd1_trace.log 2>&1 \
+            || { echo "fwd1 trace failed $?"; tail -5 $OUT/fwd1_trace.log; exit 1; }
+        D=$(dirname $(find $OUT/f1trace -name "run_kernel_trace.csv" | head -1))
+        cp $D/run_kernel_stats.csv $OUT/fwd1_kernel_stats.csv
+        python3 tools/trace_gaps.py $D 0.5 > $OUT/fwd1_gaps.txt && head -40 $OUT/fwd1_gaps.txt ;;
     aggceil)
         timeout -k 10 300 python3 -u tools/agg_ceiling.py > $OUT/agg_ceiling.txt 2>&1 \
             || { echo "agg ceiling failed $?"; tail -5 $OUT/agg_ceiling.txt; exit 1; }
