@@ -58,7 +58,13 @@ static const long P_OFF[18] = {0,       1296,    1344,    22080,   22128,   6360
                                63696,   146640,  146736,  312624,  312816,  644592,
                                644784,  5461680, 5462192, 5593264, 5593520, 5596080};
 constexpr long P_TOTAL = 5596090;
-constexpr int ZL1F = 4;     // linear1 forward split-K
+// linear1 forward split-K: 16, for the facade's one-call forwards (128 samples: 32 tiles of 32 x
+// 64, so the split sets the block count), 0.447 -> 0.406 ms per call and facade 808 -> 834
+// worker-steps/s against 4, the batched chunk unchanged (1051.7 / 1054.3), profiles/r06/r06t
+#ifndef FLSIM_ZL1F
+#define FLSIM_ZL1F 16
+#endif
+constexpr int ZL1F = FLSIM_ZL1F;
 constexpr int ZL1W = 8;     // linear1 wgrad split
 constexpr int ZL2W = 64;    // linear2 wgrad split
 constexpr int ZH = 32;      // head wgrad split
