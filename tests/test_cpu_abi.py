@@ -145,3 +145,26 @@ def test_comm_abi_one_rank_local():
     assert L.flsim_comm_destroy(None) == 0
     with pytest.raises(ValueError):
         Comm(2, 0, b"short")
+
+
+@pytest.mark.parametrize("macro", ["FLSIM_X6_FRESH=5", "FLSIM_WGRAD_X6=1", "FLSIM_X6_FLUSH=16",
+                                   "FLSIM_ZL1F=4", "FLSIM_DG_FMS=1"])
+def test_measurement_overrides_need_a_lab_build(macro, tmp_path):
+    """csrc/common.h: a -DFLSIM_<X> measurement override compiles only with -DFLSIM_LAB (make
+    LAB=1), so the product library cannot be built off its measured defaults by accident."""
+    import shutil
+    import subprocess
+    cxx = shutil.which("g++") or shutil.which("c++")
+    if cxx is None:
+        pytest.skip("no host C++ compiler")
+    src = tmp_path / "t.cpp"
+    # common.h's own preprocessor check, with the HIP runtime header replaced by an empty one
+    (tmp_path / "hip").mkdir()
+    (tmp_path / "hip" / "hip_runtime.h").write_text("")
+    src.write_text('#include "common.h"\nint main() { return 0; }\n')
+    inc = ["-I", str(tmp_path), "-I", os.path.join(REPO, "fl-distributed-delay_amd", "csrc")]
+    cmd = [cxx, "-std=c++17", "-E", "-D" + macro] + inc + [str(src)]
+    bad = subprocess.run(cmd, capture_output=True, text=True)
+    assert bad.returncode != 0 and "need a lab build" in bad.stderr, bad.stderr[-400:]
+    ok = subprocess.run(cmd + ["-DFLSIM_LAB"], capture_output=True, text=True)
+    assert ok.returncode == 0, ok.stderr[-400:]
