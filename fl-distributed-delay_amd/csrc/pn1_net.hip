@@ -668,6 +668,7 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     // gradients split dZ while staging (split-bf16 kernel over an fp32 dZ and a split layer input)
     RC(join());                                   // conv5's wgrad reads gx = dz5: done first
     RC(fork());
+    // (fp32 tiles 96 x 144 of 6 waves: 15.2 against 11.0 ms, profiles/r06/r06r)
     RC((conv_wgrad<20, 20, 96, 2, 3, 3, 2, 2, 0, false, FLSIM_WGRAD_X6, BufSrc,
                    std::conditional_t<FLSIM_WGRAD_X6, XsSrcSM, XsF32SrcSM>>(
         dz4, w.a3, S, 96, 864, g.sw[3], g.sb[3], GEO[3].ZW, sw, K_WG4, 864, zi(3), &zu[3],
@@ -703,6 +704,9 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
         dz2, w.a1, S, 48, 432, g.sw[1], g.sb[1], GEO[1].ZW, sw, K_WG2, 432, zi(1), &zu[1],
         nullptr, w.a1l)));
 #else
+    // (one 48 x 48 wave per block; its tap tiles fetch dZ and the layer input once each, 53 GB
+    // per launch, profiles/traffic.json.  Blocks spanning 3 or 9 taps, 48 x 144 of 3 waves /
+    // 48 x 432 of 9, ran slower: 9.06 / 14.9 against 8.91 ms, profiles/r06/r06r)
     RC((conv_wgrad<34, 34, 48, 2, 3, 3, 1, 1, 0, false, false, BufSrc, XsF32SrcSM>(
         dz2, w.a1, S, 48, 432, g.sw[1], g.sb[1], GEO[1].ZW, sw, K_WG2, 432, zi(1), &zu[1],
         nullptr, w.a1l)));
