@@ -49,6 +49,7 @@ struct EpiBiasReluXs {
     float* Yl;
     const float* bias;
     int M;
+    float* Yf = nullptr;   // fp32 copy, same layout (split.h xs_store_f), or none
     __device__ float value(int, float v) const { return v; }
     __device__ void store_rows(const float* tile, int ld, int m0, int bm, int n0, int bn, int tid,
                                int nt) const {
@@ -60,7 +61,7 @@ struct EpiBiasReluXs {
             const f32x4 b = *reinterpret_cast<const f32x4*>(bias + n0 + 4 * c);
             const f32x4 v = {fmaxf(t.x + b.x, 0.f), fmaxf(t.y + b.y, 0.f), fmaxf(t.z + b.z, 0.f),
                              fmaxf(t.w + b.w, 0.f)};
-            xs_store(Yhm, Yl, xs_unit<NC, HW, SM>((unsigned)(m0 + r), n0 / 4 + c), v);
+            xs_store_f(Yhm, Yl, Yf, xs_unit<NC, HW, SM>((unsigned)(m0 + r), n0 / 4 + c), v);
         }
     }
 };
@@ -228,6 +229,7 @@ struct EpiPoolDropXs {
     float scale;
     int dropout;
     int M;
+    float* df = nullptr;   // fp32 copy of d, same layout (split.h xs_store_f), or none
     __device__ float value(int, float v) const { return v; }
     __device__ void store_rows(const float* tile, int ld, int m0, int bm, int tid, int nt) const {
         const int rows = M - m0 < bm ? M - m0 : bm;
@@ -269,7 +271,7 @@ struct EpiPoolDropXs {
             }
             const long eo = (long)q * C + 4 * c;
             *reinterpret_cast<uint32_t*>(idx + eo) = id;
-            xs_store(dhm, dl, xs_unit<C, PH * PW, SM>((unsigned)q, c), out);
+            xs_store_f(dhm, dl, df, xs_unit<C, PH * PW, SM>((unsigned)q, c), out);
         }
     }
 };

@@ -53,6 +53,10 @@ struct BufSrc {
         return ld(ok ? byte_off : BUF_OOB);
     }
 };
+// fp32, channel-slice-major ([img][C/16][H][W][16]; split.h xs_store_f's copies of a1, d1, a3)
+struct BufSrcSM : BufSrc {
+    static constexpr bool SM = true;
+};
 // The same over a tensor in the split-bf16 form (split.h): byte offsets are the fp32 tensor's; the
 // HM unit is read at that offset and the L unit at half of it.  A masked unit's BUF_OOB halves to
 // 0x7ffffff8, still past the end of the L buffer (< 2 GB: every split tensor here is; the fp32

@@ -161,6 +161,9 @@ struct WS {
     uint8_t* i1; uint8_t* i2; uint8_t* i3;
     float* a1l; float* d1l; float* a3l; float* d2l; float* a5l;     // forward split tensors
     float* a6l; float* a4l; float* a2l; float* gxl;                  // (unused: dZ is fp32)
+    // fp32 copies of the weight gradients' layer inputs (split.h xs_store_f; a1f, d1f, a3f
+    // channel-slice-major like their HM parts)
+    float* a1f; float* d1f; float* a3f; float* d2f; float* a5f;
     long bytes;
     XsT x(float* hm, float* l) const { return XsT{hm, l}; }
 };
@@ -188,6 +191,7 @@ static WS ws_layout(char* base, int S, int row0 = 0) {
     w.a1l = tf(55488 / 2); w.d1l = tf(15552 / 2); w.a3l = tf(38400 / 2); w.d2l = tf(11616 / 2);
     w.a5l = tf(32448 / 2);
     w.a6l = tf(0); w.a4l = tf(0); w.a2l = tf(0); w.gxl = tf(0);   // (dZ is fp32: ids kept, no bytes)
+    w.a1f = tf(55488); w.d1f = tf(15552); w.a3f = tf(38400); w.d2f = tf(11616); w.a5f = tf(32448);
     w.bytes = o;
     return w;
 }
@@ -222,7 +226,7 @@ static_assert(C1_ROWS == 32, "the a1 store loop maps 64 lanes to 16 rows x 4 uni
 constexpr int C1_LD = 52;       // staging row stride (floats): 16-B aligned, rows on different banks
 __global__ void __launch_bounds__(256)
 k_conv1_fwd(const float* __restrict__ x0, const float* __restrict__ W, const float* __restrict__ bias,
-            float* __restrict__ a1, float* __restrict__ a1l, long units) {
+            float* __restrict__ a1, float* __restrict__ a1l, float* __restrict__ a1f, long units) {
     __shared__ __attribute__((aligned(16))) float stage[4][C1_ROWS * C1_LD];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int i = lane & 15, g = lane >> 4;
@@ -298,15 +302,15 @@ k_conv1_fwd(const float* __restrict__ x0, const float* __restrict__ W, const flo
 #pragma unroll
         for (int q0 = 0; q0 < C1_ROWS * 12; q0 += 64) {
             const int q = q0 + lane, slice = q >> 7, row = (q & 127) >> 2, c4 = 4 * slice + (q & 3);
-            xs_store(a1, a1l, xs_unit<48, 1156, true>((unsigned)(u * C1_ROWS + row), c4),
-                     *reinterpret_cast<const f32x4*>(st + row * C1_LD + 4 * c4));
+            xs_store_f(a1, a1l, a1f, xs_unit<48, 1156, true>((unsigned)(u * C1_ROWS + row), c4),
+                       *reinterpret_cast<const f32x4*>(st + row * C1_LD + 4 * c4));
         }
         __builtin_amdgcn_wave_barrier();
     }
 }
 
-static int conv1_fwd(const float* x0, const float* W, const float* bias, XsT a1, int S,
-                     hipStream_t st) {
+static int conv1_fwd(const float* x0, const float* W, const float* bias, XsT a1, float* a1f,
+                     int S, hipStream_t st) {
     const long M = (long)S * 34 * 34;
     if (M % C1_ROWS) return 1;             // S is a multiple of 128 (whole sample groups)
     const long units = M / C1_ROWS;
@@ -315,7 +319,7 @@ static int conv1_fwd(const float* x0, const float* W, const float* bias, XsT a1,
     const int grid = (int)(units / 4 < 2048 ? (units + 3) / 4 : 2048);
     const ProbeSlot ps = probe_begin();
     hipExtLaunchKernelGGL(k_conv1_fwd, dim3(grid), dim3(256), 0, st, ps.start, ps.stop, 0, x0, W,
-                          bias, a1.hm, a1.l, units);
+                          bias, a1.hm, a1.l, a1f, units);
     FLSIM_LAUNCH_CHECK();
     return probe_end(ps, K_FWD1, 2.0 * M * 48 * 27);
 }
@@ -363,22 +367,24 @@ static int forward(const GradState& g, const WS& w, const float* theta, int S,
     const XsT a1 = w.x(w.a1, w.a1l), d1 = w.x(w.d1, w.d1l), a3 = w.x(w.a3, w.a3l);
     const XsT d2 = w.x(w.d2, w.d2l), a5 = w.x(w.a5, w.a5l);
     // conv1 + ReLU (models.py:29), a1 written split
-    RC(conv1_fwd(w.x0, theta + P_OFF[0], theta + P_OFF[1], a1, S, st));
+    RC(conv1_fwd(w.x0, theta + P_OFF[0], theta + P_OFF[1], a1, w.a1f, S, st));
     // conv2 + ReLU + pool1 + dropout1 (models.py:30-32), one fused launch -> d1 (split)
     RC((dx6<34, 34, 48, 2, 3, true, 0, 4, 4>(a1, S, g.wfx[1], 48, 432,
         EpiPoolDropXs<18, 18, 48, true>{d1.hm, d1.l, w.i1, theta + P_OFF[3], workers, seed, SITE_DROP1,
-                                  THR_P25, SCALE_P25, dropout, S * 18 * 18 * 4}, st, K_FWD2, 432)));
+                                  THR_P25, SCALE_P25, dropout, S * 18 * 18 * 4, w.d1f}, st,
+        K_FWD2, 432)));
     // conv3 + ReLU (models.py:33) -> a3 (split)
     RC((dx6<18, 18, 48, 2, 6, false, 0>(d1, S, g.wfx[2], 96, 432,
-        EpiBiasReluXs<96, true, 400>{a3.hm, a3.l, theta + P_OFF[5], S * 20 * 20}, st, K_FWD3,
+        EpiBiasReluXs<96, true, 400>{a3.hm, a3.l, theta + P_OFF[5], S * 20 * 20, w.a3f}, st, K_FWD3,
         432)));
     // conv4 + ReLU + pool2 + dropout1 (models.py:34-36) -> d2 (split)
     RC((dx6<20, 20, 96, 2, 6, true, 0>(a3, S, g.wfx[3], 96, 864,
         EpiPoolDropXs<11, 11, 96>{d2.hm, d2.l, w.i2, theta + P_OFF[7], workers, seed, SITE_DROP2,
-                                  THR_P25, SCALE_P25, dropout, S * 11 * 11 * 4}, st, K_FWD4, 864)));
+                                  THR_P25, SCALE_P25, dropout, S * 11 * 11 * 4, w.d2f}, st,
+        K_FWD4, 864)));
     // conv5 + ReLU (models.py:37) -> a5 (split)
     RC((xs<11, 11, 96, 2, 4, 6, 4, 2, false, 0>(d2, S, g.wfx[4], 192, 864,
-        EpiBiasReluXs<192>{a5.hm, a5.l, theta + P_OFF[9], S * 13 * 13}, st, K_FWD5, 864)));
+        EpiBiasReluXs<192>{a5.hm, a5.l, theta + P_OFF[9], S * 13 * 13, w.a5f}, st, K_FWD5, 864)));
     // conv6 + ReLU + pool3 + dropout1 (models.py:38-40), written fp32 in torch's flatten order
     // (models.py:41) so linear1 keeps the torch weight layout; the floor-mode border row/column
     // of the 15x15 output (dropped by the pool) is never computed
@@ -635,9 +641,8 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
         dz6, w.a5, S, 192, 1728, g.sw[5], g.sb[5], GEO[5].ZW, sw, K_WG6, 1728, zi(5), &zu[5],
         nullptr, w.a5l)));
 #else
-    RC((conv_wgrad<13, 13, 192, 2, 6, 3, 2, 4, 14, true, false, BufSrc, XsF32Src>(
-        dz6, w.a5, S, 192, 1728, g.sw[5], g.sb[5], GEO[5].ZW, sw, K_WG6, 1728, zi(5), &zu[5],
-        nullptr, w.a5l)));
+    RC((conv_wgrad<13, 13, 192, 2, 6, 3, 2, 4, 14, true, false, BufSrc, BufSrc>(
+        dz6, w.a5f, S, 192, 1728, g.sw[5], g.sb[5], GEO[5].ZW, sw, K_WG6, 1728, zi(5), &zu[5])));
 #endif
     // (every data gradient runs on the fp32 MFMA: the bf16 MFMA truncates small addends toward
     // zero, which biases the per-channel sums of its outputs 30-100x beyond the CPU fp32 port's
@@ -653,9 +658,8 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
         dz5, w.d2, S, 192, 864, g.sw[4], g.sb[4], GEO[4].ZW, sw, K_WG5, 864, zi(4), &zu[4],
         nullptr, w.d2l)));
 #else
-    RC((conv_wgrad<11, 11, 96, 2, 6, 3, 2, 2, 0, false, false, BufSrc, XsF32Src>(
-        dz5, w.d2, S, 192, 864, g.sw[4], g.sb[4], GEO[4].ZW, sw, K_WG5, 864, zi(4), &zu[4],
-        nullptr, w.d2l)));
+    RC((conv_wgrad<11, 11, 96, 2, 6, 3, 2, 2, 0, false, false, BufSrc, BufSrc>(
+        dz5, w.d2f, S, 192, 864, g.sw[4], g.sb[4], GEO[4].ZW, sw, K_WG5, 864, zi(4), &zu[4])));
 #endif
     RC((conv_direct_sz<13, 13, 192, 0, 2, DG_FMS, 6, 8, 3, 2, false, 0>(dz5, S, g.wd[4], 96, 1728,
         EpiDropScatterXs<11, 11, 96, false>{dz4, nullptr, w.d2, w.i2, s25, S * 11 * 11}, st,
@@ -669,10 +673,14 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     RC(join());                                   // conv5's wgrad reads gx = dz5: done first
     RC(fork());
     // (fp32 tiles 96 x 144 of 6 waves: 15.2 against 11.0 ms, profiles/r06/r06r)
-    RC((conv_wgrad<20, 20, 96, 2, 3, 3, 2, 2, 0, false, FLSIM_WGRAD_X6, BufSrc,
-                   std::conditional_t<FLSIM_WGRAD_X6, XsSrcSM, XsF32SrcSM>>(
+#if FLSIM_WGRAD_X6
+    RC((conv_wgrad<20, 20, 96, 2, 3, 3, 2, 2, 0, false, true, BufSrc, XsSrcSM>(
         dz4, w.a3, S, 96, 864, g.sw[3], g.sb[3], GEO[3].ZW, sw, K_WG4, 864, zi(3), &zu[3],
         nullptr, w.a3l)));
+#else
+    RC((conv_wgrad<20, 20, 96, 2, 3, 3, 2, 2, 0, false, false, BufSrc, BufSrcSM>(
+        dz4, w.a3f, S, 96, 864, g.sw[3], g.sb[3], GEO[3].ZW, sw, K_WG4, 864, zi(3), &zu[3])));
+#endif
     RC((conv_direct_sz<22, 22, 96, 0, 2, DG_FMS, 6, 8, 3, 2, false, 0>(dz4, S, g.wd[3], 96, 864,
         EpiMaskXs<96, false, true, 400>{w.gx, nullptr, w.a3, S * 20 * 20}, st, K_DG4, 864)));
     if (debug_stop() == 4) return finish();       // (debug: dz3 in gx, dz4 in a4)
@@ -686,9 +694,8 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
         dz3, w.d1, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW, sw, K_WG3, 432, zi(2), &zu[2],
         nullptr, w.d1l)));
 #else
-    RC((conv_wgrad<18, 18, 48, 2, 3, 3, 2, 1, 0, false, false, BufSrc, XsF32SrcSM>(
-        dz3, w.d1, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW, sw, K_WG3, 432, zi(2), &zu[2],
-        nullptr, w.d1l)));
+    RC((conv_wgrad<18, 18, 48, 2, 3, 3, 2, 1, 0, false, false, BufSrc, BufSrcSM>(
+        dz3, w.d1f, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW, sw, K_WG3, 432, zi(2), &zu[2])));
 #endif
     // (gemm_kernel: the direct-A form measured 3.87 vs 3.78 ms with this staged epilogue, r03b)
     RC((conv_like_sz<20, 20, 96, 0, 4, 2, 3, 4, 1>(dz3, S, g.wd[2], 48, 864,
@@ -707,9 +714,8 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
     // (one 48 x 48 wave per block; its tap tiles fetch dZ and the layer input once each, 53 GB
     // per launch, profiles/traffic.json.  Blocks spanning 3 or 9 taps, 48 x 144 of 3 waves /
     // 48 x 432 of 9, ran slower: 9.06 / 14.9 against 8.91 ms, profiles/r06/r06r)
-    RC((conv_wgrad<34, 34, 48, 2, 3, 3, 1, 1, 0, false, false, BufSrc, XsF32SrcSM>(
-        dz2, w.a1, S, 48, 432, g.sw[1], g.sb[1], GEO[1].ZW, sw, K_WG2, 432, zi(1), &zu[1],
-        nullptr, w.a1l)));
+    RC((conv_wgrad<34, 34, 48, 2, 3, 3, 1, 1, 0, false, false, BufSrc, BufSrcSM>(
+        dz2, w.a1f, S, 48, 432, g.sw[1], g.sb[1], GEO[1].ZW, sw, K_WG2, 432, zi(1), &zu[1])));
 #endif
     RC((conv_direct_sz<36, 36, 48, 0, 2, 1, 3, 8, 3, 2, false, 0>(dz2, S, g.wd[1], 48, 432,
         EpiMaskXs<48, false, true, 1156>{w.gx, nullptr, w.a1, S * 34 * 34}, st, K_DG2, 432)));
@@ -747,7 +753,8 @@ int flsim_pn1_workspace_offset(int which, int samples, long* offset_bytes) {
     const void* p[] = {w.x0, w.a1, w.a2, w.d1, w.a3, w.a4, w.d2, w.a5, w.a6, w.d3,
                        w.e1, w.e2, w.dh1, w.dh2, w.gx, w.gy, w.loss_s, w.dlog, w.y,
                        w.i1, w.i2, w.i3,
-                       w.a1l, w.d1l, w.a3l, w.d2l, w.a5l, w.a6l, w.a4l, w.a2l, w.gxl};
+                       w.a1l, w.d1l, w.a3l, w.d2l, w.a5l, w.a6l, w.a4l, w.a2l, w.gxl,
+                       w.a1f, w.d1f, w.a3f, w.d2f, w.a5f};
     FLSIM_REQUIRE(which >= 0 && which < (int)(sizeof(p) / sizeof(p[0])), "bad workspace id %d", which);
     *offset_bytes = (long)((const char*)p[which] - fake);
     return 0;

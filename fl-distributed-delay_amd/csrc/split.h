@@ -114,4 +114,14 @@ __device__ __forceinline__ void xs_store(float* hm, float* l, long u, f32x4 v) {
     }
 }
 
+// xs_store plus, when f is not null, the fp32 values themselves at the same unit index of f (a
+// tensor laid out like the HM part: 4 B per element).  The layer inputs of PerformantNet1's fp32
+// weight gradients (a1, d1, a3, d2, a5) get this copy: read as plain fp32 (BufSrc) it spares the
+// weight gradients the L loads and the (h + m) + l recombination, 1.05-1.2x on conv2-6's
+// (profiles/r06/r06q), for 4 B per element more written by the forward
+__device__ __forceinline__ void xs_store_f(float* hm, float* l, float* f, long u, f32x4 v) {
+    xs_store(hm, l, u, v);
+    if (f) __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(f) + u);
+}
+
 }  // namespace flsim
