@@ -153,6 +153,12 @@ class _ModelContext:
             self.defer_max = min(cw, MAX_BATCH // 128) * 128
         self.engine = self.engine_cls(dev, chunk_workers=min(self.defer_max // 128, 8) or 1)
         self.defer_rows = self.engine.max_samples if self.defer_max else 0
+        # Deferred forward (PerformantNet1, 128-sample calls): a call only stages its batch into
+        # the chunk's next rows and returns a _LazyLoss; the forward + loss of the staged calls
+        # runs as one batched pass (flush_forward) when a loss is read or the backward is due.
+        # FLSIM_FACADE_LAZY_LOSS=0: every call runs its forward now and returns a plain array.
+        self.lazy_loss = os.environ.get("FLSIM_FACADE_LAZY_LOSS", "1") != "0"
+        self.block = None            # _LossBlock of the staged calls whose forward has not run
         self.epoch_rows = 0          # rows forwarded this epoch
         self.pending = 0             # rows forwarded whose backward is not queued yet
         self.pending_dropout = None  # their dropout flag (one per backward pass)
@@ -269,8 +275,22 @@ class _ModelContext:
         self.version = v
         return self.theta_run
 
+    def flush_forward(self):
+        """Run the forward + loss of the staged calls (one worker-batched pass over their rows);
+        their _LazyLoss values are then ready on the stream."""
+        b = self.block
+        if b is None:
+            return
+        self.block = None
+        n = len(b.indices)
+        wt = worker_table([(self.t, i, 0) for i in b.indices], self.device)
+        b.dev = torch.empty(n, device=self.device)
+        self.engine.forward_loaded_rows(self.theta_run, b.row0, n * 128, wt, self.seed,
+                                        b.dropout, b.dev, b.slot)
+
     def flush_backward(self):
         """Queue the backward of the pending forward rows (one worker-batched pass)."""
+        self.flush_forward()
         if self.pending:
             self.engine.backward_rows(self.theta_run, self.pending, self.pending_dropout,
                                       self.slot)
@@ -420,6 +440,105 @@ def _flat_of(view, ctx):
     return flat
 
 
+class _LossBlock:
+    """The staged 128-sample calls of one deferred forward: rows [row0, row0 + 128 * len) of
+    workspace `slot`, their Worker indices (dropout keys) and, once flush_forward has run, their
+    losses (`dev`, fetched to the host once, on the first read of any of them)."""
+
+    def __init__(self, ctx, row0, slot, dropout):
+        self.ctx = weakref.ref(ctx)
+        self.row0, self.slot, self.dropout = row0, slot, dropout
+        self.indices = []
+        self.dev = None
+        self.host = None
+
+    def value(self, g):
+        if self.host is None:
+            if self.dev is None:
+                ctx = self.ctx()
+                if ctx is None:
+                    raise RuntimeError("the model of this loss was freed before its forward ran")
+                ctx.flush_forward()
+            self.host = self.dev.cpu().numpy()
+            self.dev = None
+        return self.host[g]
+
+
+class _LazyLoss:
+    """What Worker.fwd_bkwd returns as the loss of a deferred 128-sample call: agents.py:40's
+    `lossval.detach().cpu().numpy()` (a 0-d float32 array), computed on first read.  Reading it
+    (np.mean over a list of them as main.py:181 does, float(), print, arithmetic, any ndarray
+    attribute) runs the forward of the calls staged so far as one batched pass and fetches their
+    losses in one copy; the value is the per-call forward's, bit for bit."""
+
+    __slots__ = ("_block", "_g", "_arr")
+    __array_priority__ = 1000
+
+    def __init__(self, block, g):
+        self._block, self._g, self._arr = block, g, None
+
+    def _value(self):
+        if self._arr is None:
+            self._arr = np.asarray(np.float32(self._block.value(self._g)), np.float32)
+            self._block = None
+        return self._arr
+
+    def __array__(self, dtype=None, copy=None):
+        a = self._value()
+        return a if dtype is None else a.astype(dtype)
+
+    def __array_ufunc__(self, ufunc, method, *inputs, **kwargs):
+        inputs = tuple(x._value() if isinstance(x, _LazyLoss) else x for x in inputs)
+        return getattr(ufunc, method)(*inputs, **kwargs)
+
+    def __getattr__(self, name):
+        return getattr(self._value(), name)
+
+    def __float__(self):
+        return float(self._value())
+
+    def __int__(self):
+        return int(self._value())
+
+    def __bool__(self):
+        return bool(self._value())
+
+    def __repr__(self):
+        return repr(self._value())
+
+    def __str__(self):
+        return str(self._value())
+
+    def __format__(self, spec):
+        return format(self._value(), spec)
+
+    def __reduce__(self):
+        return (np.asarray, (self._value(),))
+
+    def __neg__(self):
+        return -self._value()
+
+    def __abs__(self):
+        return abs(self._value())
+
+
+def _binop(name):
+    def f(self, other):
+        other = other._value() if isinstance(other, _LazyLoss) else other
+        return getattr(self._value(), name)(other)
+    f.__name__ = name
+    return f
+
+
+for _op in ("add", "sub", "mul", "truediv", "floordiv", "pow", "mod"):
+    setattr(_LazyLoss, f"__{_op}__", _binop(f"__{_op}__"))
+    setattr(_LazyLoss, f"__r{_op}__", _binop(f"__r{_op}__"))
+for _op in ("lt", "le", "gt", "ge", "eq", "ne"):
+    setattr(_LazyLoss, f"__{_op}__", _binop(f"__{_op}__"))
+_LazyLoss.__hash__ = None                # as ndarray
+del _op
+
+
 class Worker:
     """agents.py:27-40."""
 
@@ -454,7 +573,8 @@ class Worker:
             # out the parameters' own .grad, the same objects for every worker of the epoch)
             ctx.views = _lazy_views(ctx.G[:ctx.P], ctx.shapes, ctx)
         groups = -(-n // 128)
-        wt = ctx.worker_rec(self.index, groups)
+        lazy_call = defer and ctx.lazy_loss and n == 128
+        wt = None if lazy_call else ctx.worker_rec(self.index, groups)
         lb = ctx.loss_buf[:groups]
         kw = {}
         if ctx.bn_stats is not None:
@@ -463,6 +583,7 @@ class Worker:
                                           "on 128-sample batches (main.py:43-44, 132)")
             kw = {"stats_out": ctx.bn_stats}
         x = inp.to(ctx.device, torch.float32)
+        lazy = None
         if defer:
             # this call's forward + loss into the chunk's next rows; the backward waits for the
             # chunk (one batched pass, flush_backward)
@@ -471,8 +592,17 @@ class Worker:
             if ctx.pending and (ctx.pending + rows > ctx.defer_rows or
                                 training != ctx.pending_dropout):
                 ctx.flush_backward()
-            eng.forward_rows(theta, x, outp.to(ctx.device), wt, ctx.seed, training, lb,
-                             ctx.pending, ctx.slot)
+            if lazy_call:
+                # staged only: the forward runs with the other staged calls (flush_forward)
+                eng.load_rows(x, outp.to(ctx.device), ctx.pending, ctx.slot)
+                if ctx.block is None:
+                    ctx.block = _LossBlock(ctx, ctx.pending, ctx.slot, training)
+                lazy = _LazyLoss(ctx.block, len(ctx.block.indices))
+                ctx.block.indices.append(self.index)
+            else:
+                ctx.flush_forward()          # the staged block's rows stay contiguous
+                eng.forward_rows(theta, x, outp.to(ctx.device), wt, ctx.seed, training, lb,
+                                 ctx.pending, ctx.slot)
             ctx.pending += rows
             ctx.epoch_rows += rows
             ctx.pending_dropout = training
@@ -494,6 +624,8 @@ class Worker:
         for p, gv in zip(ctx.params, grads):
             if p.grad is not gv:
                 p.grad = gv                      # agents.py:35: accumulated in place
+        if lazy is not None:
+            return list(grads), lazy
         # CrossEntropyLoss(mean) over the n samples: group sums / n (padding contributes 0)
         tot = lb.item() if groups == 1 else float(lb.double().sum().cpu())
         lossval = np.float32(tot * 128.0 / n)

@@ -899,6 +899,19 @@ static int run_pipelined(void* gradstate, void* workspace, int max_samples, cons
                           er);
 }
 
+// rows a queued backward still reads are not overwritten: `stream` waits for the last backward
+// that read this workspace
+static int wait_workspace(void* gradstate, void* workspace, hipStream_t stream) {
+    std::lock_guard<std::mutex> lk(g_pipe_mu);
+    auto it = g_pipes.find(gradstate);
+    if (it != g_pipes.end()) {
+        auto e = it->second.ws_free.find(workspace);
+        if (e != it->second.ws_free.end() && e->second)
+            FLSIM_CHECK_HIP(hipStreamWaitEvent(stream, e->second, 0));
+    }
+    return 0;
+}
+
 extern "C" {
 
 int flsim_pn1_fwd_bwd_chunk_async(void* gradstate, void* workspace, int max_samples,
@@ -973,15 +986,7 @@ int flsim_pn1_fwd_rows(void* gradstate, void* workspace, int max_samples, int ro
     FLSIM_REQUIRE(max_samples <= 16384, "workspace of %d samples exceeds the 32-bit index budget",
                   max_samples);
     FLSIM_REQUIRE(epoch_rows(gradstate), "forward rows without flsim_pn1_begin_epoch");
-    {   // rows a queued backward still reads are not overwritten
-        std::lock_guard<std::mutex> lk(g_pipe_mu);
-        auto it = g_pipes.find(gradstate);
-        if (it != g_pipes.end()) {
-            auto e = it->second.ws_free.find(workspace);
-            if (e != it->second.ws_free.end() && e->second)
-                FLSIM_CHECK_HIP(hipStreamWaitEvent(stream, e->second, 0));
-        }
-    }
+    RC(wait_workspace(gradstate, workspace, stream));
     WS w = ws_layout((char*)workspace, max_samples, row0);
     GradState g = gs_layout((float*)gradstate);
     hipLaunchKernelGGL(k_load_input, dim3(S), dim3(256), 0, stream, x, y, n_samples, w.x0, w.y);
@@ -990,6 +995,53 @@ int flsim_pn1_fwd_rows(void* gradstate, void* workspace, int max_samples, int ro
     return head_and_loss<256>(w.e2, theta + P_OFF[16], theta + P_OFF[17], w.y, w.loss_s, w.dlog,
                               w.dh2, S, 1, dropout ? SCALE_P50 : 1.f, 1.f / (float)n_samples,
                               worker_loss, stream, workers);
+}
+
+// The facade's deferred forward (Worker.fwd_bkwd of 128-sample batches): a call only stages its
+// batch into workspace rows [row0, row0 + 128) now (flsim_pn1_load_rows); the forward + loss of a
+// run of staged rows then runs as ONE worker-batched pass (flsim_pn1_fwd_loaded_rows), when a
+// loss is read or the chunk's backward is due.  The kernels are the batched engine's: the same
+// sums per output as the one-call forward of flsim_pn1_fwd_rows (the tiles' K order does not
+// depend on the row count, linear1's split-K is fixed), so the losses are bit-identical.
+int flsim_pn1_load_rows(void* gradstate, void* workspace, int max_samples, int row0,
+                        const float* x, const int64_t* y, int n_samples, hipStream_t stream) {
+    FLSIM_REQUIRE(gradstate && workspace && x && y, "null pointer");
+    FLSIM_REQUIRE(n_samples > 0, "empty batch");
+    FLSIM_REQUIRE(row0 >= 0 && row0 % SAMPLES_PER_WORKER == 0,
+                  "row0 %d is not a multiple of %d", row0, SAMPLES_PER_WORKER);
+    const int S = ceil_div(n_samples, SAMPLES_PER_WORKER) * SAMPLES_PER_WORKER;
+    FLSIM_REQUIRE((long)row0 + S <= max_samples, "rows [%d, %d) exceed workspace (%d)", row0,
+                  row0 + S, max_samples);
+    FLSIM_REQUIRE(max_samples <= 16384, "workspace of %d samples exceeds the 32-bit index budget",
+                  max_samples);
+    RC(wait_workspace(gradstate, workspace, stream));
+    WS w = ws_layout((char*)workspace, max_samples, row0);
+    hipLaunchKernelGGL(k_load_input, dim3(S), dim3(256), 0, stream, x, y, n_samples, w.x0, w.y);
+    FLSIM_LAUNCH_CHECK();
+    return 0;
+}
+
+// forward + CrossEntropyLoss of rows [row0, row0 + n_rows) staged by flsim_pn1_load_rows, every
+// 128-row group one full batch: workers[n_rows / 128] the groups' dropout keys, worker_loss[g] =
+// group g's mean loss (agents.py:40's lossval of that call)
+int flsim_pn1_fwd_loaded_rows(void* gradstate, void* workspace, int max_samples, int row0,
+                              int n_rows, const float* theta, const WorkerRec* workers,
+                              uint64_t seed, int dropout, float* worker_loss, hipStream_t stream) {
+    FLSIM_REQUIRE(gradstate && workspace && theta && workers && worker_loss, "null pointer");
+    FLSIM_REQUIRE(row0 >= 0 && row0 % SAMPLES_PER_WORKER == 0 && n_rows > 0 &&
+                  n_rows % SAMPLES_PER_WORKER == 0, "bad rows [%d, +%d)", row0, n_rows);
+    FLSIM_REQUIRE((long)row0 + n_rows <= max_samples, "rows [%d, %d) exceed workspace (%d)", row0,
+                  row0 + n_rows, max_samples);
+    FLSIM_REQUIRE(max_samples <= 16384, "workspace of %d samples exceeds the 32-bit index budget",
+                  max_samples);
+    FLSIM_REQUIRE(epoch_rows(gradstate), "forward rows without flsim_pn1_begin_epoch");
+    RC(wait_workspace(gradstate, workspace, stream));
+    WS w = ws_layout((char*)workspace, max_samples, row0);
+    GradState g = gs_layout((float*)gradstate);
+    RC(forward(g, w, theta, n_rows, workers, seed, dropout, stream));
+    return head_and_loss<256>(w.e2, theta + P_OFF[16], theta + P_OFF[17], w.y, w.loss_s, w.dlog,
+                              w.dh2, n_rows, 1, dropout ? SCALE_P50 : 1.f,
+                              1.f / SAMPLES_PER_WORKER, worker_loss, stream, workers);
 }
 
 // the backward of rows [0, n_rows) written by flsim_pn1_fwd_rows with this theta and dropout

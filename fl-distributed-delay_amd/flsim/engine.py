@@ -183,6 +183,26 @@ class NetEngine:
             int(x.shape[0]), ptr(workers_dev), ctypes.c_uint64(seed), int(bool(dropout)),
             ptr(loss_out), stream_ptr()))
 
+    def load_rows(self, x, y, row0, slot):
+        """The facade's deferred forward (PN1Engine): stage an explicit batch into workspace rows
+        [row0, row0 + ceil(n/128)*128) of workspace `slot`; nothing is computed yet."""
+        ws = self._slot_workspace(slot)
+        self.last_workspace = ws
+        x = x.contiguous()
+        y = y.to(torch.int64).contiguous()
+        check(lib().flsim_pn1_load_rows(ptr(self.gradstate), ptr(ws), self.max_samples,
+                                        int(row0), ptr(x), ptr(y), int(x.shape[0]), stream_ptr()))
+
+    def forward_loaded_rows(self, theta, row0, n_rows, workers_dev, seed, dropout, loss_out,
+                            slot):
+        """Forward + loss of the staged rows [row0, row0 + n_rows) of workspace `slot` as one
+        batched pass (every 128-row group one whole batch): loss_out[g] = group g's mean loss."""
+        ws = self._slot_workspace(slot)
+        check(lib().flsim_pn1_fwd_loaded_rows(
+            ptr(self.gradstate), ptr(ws), self.max_samples, int(row0), int(n_rows), ptr(theta),
+            ptr(workers_dev), ctypes.c_uint64(seed), int(bool(dropout)), ptr(loss_out),
+            stream_ptr()))
+
     def backward_rows(self, theta, n_rows, dropout, slot):
         """The backward of rows [0, n_rows) of workspace `slot` (forward_rows) into the epoch's
         slabs, on the library's backward stream (the next slot's forwards overlap it)."""

@@ -136,6 +136,17 @@ int flsim_pn1_fwd_rows(void* gradstate, void* workspace, int max_samples, int ro
                        const float* theta, const float* x, const int64_t* y, int n_samples,
                        const WorkerRec* workers, uint64_t seed, int dropout, float* worker_loss,
                        flsim_stream_t stream);
+/* The deferred forward of 128-sample calls: flsim_pn1_load_rows stages a call's batch (x, y as
+ * for flsim_pn1_fwd_rows) into rows [row0, row0 + ceil(n/128)*128) and returns; later
+ * flsim_pn1_fwd_loaded_rows runs the forward + CrossEntropyLoss of staged rows
+ * [row0, row0 + n_rows) as one batched pass, each 128-row group one whole batch (workers[g] its
+ * dropout key, worker_loss[g] its mean loss, bit-identical to flsim_pn1_fwd_rows on that batch). */
+int flsim_pn1_load_rows(void* gradstate, void* workspace, int max_samples, int row0,
+                        const float* x, const int64_t* y, int n_samples, flsim_stream_t stream);
+int flsim_pn1_fwd_loaded_rows(void* gradstate, void* workspace, int max_samples, int row0,
+                              int n_rows, const float* theta, const WorkerRec* workers,
+                              uint64_t seed, int dropout, float* worker_loss,
+                              flsim_stream_t stream);
 /* ...then one backward over rows [0, n_rows) (the same theta and dropout flag as their forwards)
  * adds every call's gradient to the epoch's slabs (agents.py:35 accumulation).  It runs on the
  * gradstate's backward stream after everything queued on `stream`, so the next chunk's forwards

@@ -178,3 +178,59 @@ def test_deferred_facade_equals_simulation(pool, monkeypatch):
             a = getattr(ctx, name)[:ctx.P]
             b = getattr(sim, name)[:sim.P]
             assert torch.equal(a, b), (t, name, int((a != b).sum()))
+
+
+def _lazy_loop(pool, monkeypatch, lazy, n=20, epochs=2):
+    """main.py:126-188's worker loop through FL.agents with losses kept as returned and read
+    only by np.mean at the epoch's end (main.py:181); deferred chunks of 8 calls, one call of 64
+    samples (worker 5: a one-call forward between staged blocks) and one .grad read mid-epoch
+    (worker 11 of epoch 1: the staged forwards and the pending backward run there)."""
+    from FL.agents import Agg, Central, Worker, rule
+    from FL.models import PerformantNet1
+    from oracle import oracle as O
+    monkeypatch.setenv("FLSIM_FACADE_CHUNK", "8")
+    monkeypatch.setenv("FLSIM_FACADE_LAZY_LOSS", "1" if lazy else "0")
+    torch.manual_seed(0)
+    model = PerformantNet1().to(DEV)
+    central = Central(model, torch.optim.Adam(model.parameters(), lr=0.001))
+    workers = [Worker(nn.CrossEntropyLoss()) for _ in range(n)]
+    agg = Agg(rule)
+    rs = np.random.RandomState(3)
+    lut = O.normalize_lut()
+    means, all_losses, reads = [], [], []
+    for t in range(epochs):
+        ups_all, losses = [], []
+        model.train()
+        for i in range(n):
+            b = 64 if i == 5 else 128
+            idx = rs.randint(0, pool[0].shape[0], b)
+            x = torch.from_numpy(lut[pool[0][idx]]).to(DEV)
+            y = torch.from_numpy(pool[1][idx]).to(DEV)
+            workers[i].model = central.model
+            ups, lv = workers[i].fwd_bkwd(x, y)
+            losses.append(lv)
+            ups_all.append(ups)
+            if t == 1 and i == 11:
+                reads.append(torch.cat([g.reshape(-1) for g in ups]).cpu())
+        central.update_model(agg.rule(ups_all))
+        means.append(np.mean(losses))
+        all_losses.append(np.asarray([float(v) for v in losses], np.float32))
+    return central.ctx, means, all_losses, reads
+
+
+def test_facade_lazy_loss_matches_eager(pool, monkeypatch):
+    """The deferred forward (128-sample calls staged, one batched forward per block of calls,
+    _LazyLoss returned) against every call running its forward at once: per-call losses, the
+    epoch's np.mean (float32, as the reference's), a .grad read mid-epoch and theta / m / v after
+    each update bit for bit -- the batched forward's sums per output are the one-call forward's."""
+    ca, ma, la, ra = _lazy_loop(pool, monkeypatch, lazy=False)
+    cb, mb, lb, rb = _lazy_loop(pool, monkeypatch, lazy=True)
+    for t, (x, y) in enumerate(zip(la, lb)):
+        assert np.array_equal(x.view(np.uint32), y.view(np.uint32)), (t, x, y)
+    for x, y in zip(ma, mb):
+        assert isinstance(y, np.floating) and y.dtype == np.float32 and x.dtype == y.dtype
+        assert x == y
+    for x, y in zip(ra, rb):
+        assert torch.equal(x, y)
+    for name in ("theta", "m", "v"):
+        assert torch.equal(getattr(ca, name), getattr(cb, name)), name
