@@ -149,14 +149,16 @@ class _ModelContext:
         # what an epoch used (so a 4-worker loop holds 1.6 GB, a 1024-worker one 2 x 26 GB).
         cw = int(os.environ.get("FLSIM_FACADE_CHUNK", "128"))
         self.defer_max = 0
-        if self.engine_cls.PREFIX == "pn1" and cw > 0:
+        if self.engine_cls.PREFIX in ("pn1", "vgg11") and cw > 0:
             self.defer_max = min(cw, MAX_BATCH // 128) * 128
         self.engine = self.engine_cls(dev, chunk_workers=min(self.defer_max // 128, 8) or 1)
         self.defer_rows = self.engine.max_samples if self.defer_max else 0
-        # Deferred forward (PerformantNet1, 128-sample calls): a call only stages its batch into
-        # the chunk's next rows and returns a _LazyLoss; the forward + loss of the staged calls
-        # runs as one batched pass (flush_forward) when a loss is read or the backward is due.
-        # FLSIM_FACADE_LAZY_LOSS=0: every call runs its forward now and returns a plain array.
+        # Deferred forward (PerformantNet1 and vgg11, 128-sample calls): a call only stages its
+        # batch into the chunk's next rows and returns a _LazyLoss; the forward + loss of the
+        # staged calls runs as one batched pass (flush_forward; vgg11: forward, loss and backward
+        # together, the batched engine's chunk) when a loss is read or the backward is due.
+        # FLSIM_FACADE_LAZY_LOSS=0: every call runs its forward now and returns a plain array
+        # (vgg11: its forward and backward, as before).
         self.lazy_loss = os.environ.get("FLSIM_FACADE_LAZY_LOSS", "1") != "0"
         self.block = None            # _LossBlock of the staged calls whose forward has not run
         self.epoch_rows = 0          # rows forwarded this epoch
@@ -285,8 +287,15 @@ class _ModelContext:
         n = len(b.indices)
         wt = worker_table([(self.t, i, 0) for i in b.indices], self.device)
         b.dev = torch.empty(n, device=self.device)
-        self.engine.forward_loaded_rows(self.theta_run, b.row0, n * 128, wt, self.seed,
-                                        b.dropout, b.dev, b.slot)
+        if hasattr(self.engine, "fwd_bwd_loaded_rows"):
+            # vgg11: forward, loss and backward of the staged rows [0, n * 128) in one chunk
+            assert b.row0 == 0 and self.pending == n * 128
+            self.engine.fwd_bwd_loaded_rows(self.theta_run, n * 128, wt, self.seed, b.dropout,
+                                            b.dev)
+            self.pending = 0
+        else:
+            self.engine.forward_loaded_rows(self.theta_run, b.row0, n * 128, wt, self.seed,
+                                            b.dropout, b.dev, b.slot)
 
     def flush_backward(self):
         """Queue the backward of the pending forward rows (one worker-batched pass)."""
@@ -562,6 +571,7 @@ class Worker:
         eng = ctx.engine
         theta = ctx.theta
         defer = ctx.defer_rows and ctx.bn_stats is None
+        rows_api = defer and eng.PREFIX == "pn1"     # one-call forwards into chunk rows
         if defer:
             theta = ctx.prepare_rows()
         elif not ctx.packed:
@@ -584,7 +594,12 @@ class Worker:
             kw = {"stats_out": ctx.bn_stats}
         x = inp.to(ctx.device, torch.float32)
         lazy = None
-        if defer:
+        if defer and not lazy_call and not rows_api:
+            # vgg11, a call that is not staged: the staged calls run first, then this call's
+            # forward and backward at once (the workspace rows are the staged calls')
+            ctx.flush_backward()
+            eng.run_input(theta, x, outp.to(ctx.device), wt, ctx.seed, self.model.training, lb)
+        elif defer:
             # this call's forward + loss into the chunk's next rows; the backward waits for the
             # chunk (one batched pass, flush_backward)
             training = bool(self.model.training)

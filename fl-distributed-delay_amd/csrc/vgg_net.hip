@@ -511,6 +511,39 @@ static int vgg_fwd_bwd_input(void* gradstate, void* workspace, int max_samples,
                           BN ? 1.f / SAMPLES_PER_WORKER : 1.f / (float)n_samples);
 }
 
+// The facade's deferred fwd_bkwd for vgg11 (Worker.fwd_bkwd of 128-sample batches, agents.py:32-40):
+// a call stages its batch into workspace rows [row0, row0 + 128) (vgg_load_rows); the forward,
+// loss and backward of the staged rows [0, n_rows) then run as ONE worker-batched pass
+// (vgg_fwd_bwd_loaded_rows, the batched engine's own chunk), when a loss or the gradient is needed.
+template <bool BN>
+static int vgg_load_rows(void* gradstate, void* workspace, int max_samples, int row0,
+                         const float* x, const int64_t* y, int n_samples, hipStream_t stream) {
+    FLSIM_REQUIRE(gradstate && workspace && x && y, "null pointer");
+    FLSIM_REQUIRE(n_samples > 0, "empty batch");
+    FLSIM_REQUIRE(row0 >= 0 && row0 % SAMPLES_PER_WORKER == 0,
+                  "row0 %d is not a multiple of %d", row0, SAMPLES_PER_WORKER);
+    const int S = ceil_div(n_samples, SAMPLES_PER_WORKER) * SAMPLES_PER_WORKER;
+    FLSIM_REQUIRE((long)row0 + S <= max_samples && max_samples <= 16384,
+                  "rows [%d, %d) exceed workspace (%d)", row0, row0 + S, max_samples);
+    VWS w = vws_layout((char*)workspace, max_samples, BN);
+    hipLaunchKernelGGL(k_load_input, dim3(S), dim3(256), 0, stream, x, y, n_samples,
+                       w.x0 + (long)row0 * 4096, w.y + row0);
+    FLSIM_LAUNCH_CHECK();
+    return 0;
+}
+
+template <bool BN>
+static int vgg_fwd_bwd_loaded_rows(void* gradstate, void* workspace, int max_samples, int n_rows,
+                                   const float* theta, const WorkerRec* workers, uint64_t seed,
+                                   int dropout, float* worker_loss, hipStream_t stream) {
+    FLSIM_REQUIRE(gradstate && workspace && theta && workers && worker_loss, "null pointer");
+    FLSIM_REQUIRE(n_rows > 0 && n_rows % SAMPLES_PER_WORKER == 0 && n_rows <= max_samples &&
+                  n_rows <= 16384, "bad row count %d (workspace %d)", n_rows, max_samples);
+    VWS w = vws_layout((char*)workspace, max_samples, BN);
+    return vrun_chunk<BN>(gradstate, w, theta, workers, n_rows / SAMPLES_PER_WORKER, seed, dropout,
+                          1, worker_loss, nullptr, stream);
+}
+
 // Evaluation (util.py:31-45 after central.model.eval(), main.py:190: dropout off; vgg11_bn:
 // BatchNorm with the running buffers)
 template <bool BN>
@@ -618,6 +651,18 @@ int flsim_vgg11_fwd_bwd_input(void* gradstate, void* workspace, int max_samples,
     return vgg_fwd_bwd_input<false>(gradstate, workspace, max_samples, theta, x, y, n_samples,
                                     workers, seed, dropout, backward_pass, worker_loss, nullptr,
                                     stream);
+}
+
+int flsim_vgg11_load_rows(void* gradstate, void* workspace, int max_samples, int row0,
+                          const float* x, const int64_t* y, int n_samples, hipStream_t stream) {
+    return vgg_load_rows<false>(gradstate, workspace, max_samples, row0, x, y, n_samples, stream);
+}
+
+int flsim_vgg11_fwd_bwd_loaded_rows(void* gradstate, void* workspace, int max_samples, int n_rows,
+                                    const float* theta, const WorkerRec* workers, uint64_t seed,
+                                    int dropout, float* worker_loss, hipStream_t stream) {
+    return vgg_fwd_bwd_loaded_rows<false>(gradstate, workspace, max_samples, n_rows, theta,
+                                          workers, seed, dropout, worker_loss, stream);
 }
 
 int flsim_vgg11_eval_pool(void* gradstate, void* workspace, int max_samples, const float* theta,

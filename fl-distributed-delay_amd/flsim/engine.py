@@ -190,8 +190,8 @@ class NetEngine:
         self.last_workspace = ws
         x = x.contiguous()
         y = y.to(torch.int64).contiguous()
-        check(lib().flsim_pn1_load_rows(ptr(self.gradstate), ptr(ws), self.max_samples,
-                                        int(row0), ptr(x), ptr(y), int(x.shape[0]), stream_ptr()))
+        check(self._fn("load_rows")(ptr(self.gradstate), ptr(ws), self.max_samples, int(row0),
+                                    ptr(x), ptr(y), int(x.shape[0]), stream_ptr()))
 
     def forward_loaded_rows(self, theta, row0, n_rows, workers_dev, seed, dropout, loss_out,
                             slot):
@@ -344,6 +344,17 @@ class VGG11Engine(NetEngine):
     FLOP_PER_WORKER_STEP = 117_276_672_000          # 916,224,000 FLOP/sample x 128
     WORKSPACE = ("x0 d1 d2 a3 d4 a5 d6 a7 f0 e1 e2 dh1 dh2 ga gb gy loss_s dlog y "
                  "i1 i2 i4 i6 i8").split()
+
+    def _slot_workspace(self, slot):
+        return self.workspace                 # one workspace: the vgg11 facade has no pipeline
+
+    def fwd_bwd_loaded_rows(self, theta, n_rows, workers_dev, seed, dropout, loss_out):
+        """The facade's deferred fwd_bkwd: forward, loss and backward of the staged rows
+        [0, n_rows) (load_rows) as one batched chunk; loss_out[g] = call g's loss."""
+        check(lib().flsim_vgg11_fwd_bwd_loaded_rows(
+            ptr(self.gradstate), ptr(self.workspace), self.max_samples, int(n_rows), ptr(theta),
+            ptr(workers_dev), ctypes.c_uint64(seed), int(bool(dropout)), ptr(loss_out),
+            stream_ptr()))
 
 
 class VGG11BNEngine(NetEngine):

@@ -204,6 +204,15 @@ int flsim_vgg11_fwd_bwd_input(void* gradstate, void* workspace, int max_samples,
                               const float* theta, const float* x, const int64_t* y, int n_samples,
                               const WorkerRec* workers, uint64_t seed, int dropout,
                               int backward_pass, float* worker_loss, flsim_stream_t stream);
+/* the facade's deferred fwd_bkwd for vgg11() (128-sample calls, agents.py:32-40): load_rows stages
+ * a call's batch into workspace rows [row0, row0 + 128) as flsim_pn1_load_rows does; then
+ * fwd_bwd_loaded_rows runs forward, CrossEntropyLoss and backward of the staged rows [0, n_rows) as
+ * one batched chunk into the epoch's slabs (workers[g] / worker_loss[g]: one per 128-row call). */
+int flsim_vgg11_load_rows(void* gradstate, void* workspace, int max_samples, int row0,
+                          const float* x, const int64_t* y, int n_samples, flsim_stream_t stream);
+int flsim_vgg11_fwd_bwd_loaded_rows(void* gradstate, void* workspace, int max_samples, int n_rows,
+                                    const float* theta, const WorkerRec* workers, uint64_t seed,
+                                    int dropout, float* worker_loss, flsim_stream_t stream);
 int flsim_vgg11_end_epoch(void* gradstate, float* grad_out, flsim_stream_t stream);
 int flsim_vgg11_eval_input(void* gradstate, void* workspace, int max_samples, const float* theta,
                            const float* x, int n_images, int32_t* pred, flsim_stream_t stream);

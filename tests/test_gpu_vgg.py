@@ -286,3 +286,50 @@ def test_vgg_reference_api_facade(pool):
     # Adam's first step is ~lr * sign(g): near-zero gradients flip, so theta is
     # compared loosely, as in test_gpu_parity.test_reference_api_facade_loop
     assert _rel_l2(th.astype(np.float64), osim.theta.astype(np.float64)) < 0.03
+
+
+def _vgg_facade_loop(pool, monkeypatch, lazy, n=6):
+    """One epoch of main.py:126-188's worker loop through FL.agents with vgg11: losses kept as
+    returned (np.mean at the end, main.py:181), chunks of 4 staged calls, the epoch's .grad read
+    before update_model."""
+    import torch.nn as nn
+    from FL.agents import Agg, Central, Worker, rule
+    from FL.models import vgg11
+    from oracle import oracle as O
+    monkeypatch.setenv("FLSIM_FACADE_CHUNK", "4")
+    monkeypatch.setenv("FLSIM_FACADE_LAZY_LOSS", "1" if lazy else "0")
+    torch.manual_seed(0)
+    model = vgg11().to(DEV)
+    central = Central(model, torch.optim.Adam(model.parameters(), lr=0.001))
+    workers = [Worker(nn.CrossEntropyLoss()) for _ in range(n)]
+    rs = np.random.RandomState(7)
+    lut = O.normalize_lut()
+    model.train()
+    ups, losses = [], []
+    for i in range(n):
+        idx = rs.randint(0, pool[0].shape[0], 128)
+        workers[i].model = central.model
+        g, lv = workers[i].fwd_bkwd(torch.from_numpy(lut[pool[0][idx]]).to(DEV),
+                                    torch.from_numpy(pool[1][idx]).to(DEV))
+        ups.append(g)
+        losses.append(lv)
+    grad = torch.cat([t.reshape(-1) for t in ups[0]]).double().cpu()
+    central.update_model(Agg(rule).rule(ups))
+    mean = np.mean(losses)
+    th = central.ctx.theta[:central.ctx.P].double().cpu()
+    return np.asarray([float(v) for v in losses], np.float32), mean, grad, th
+
+
+def test_vgg_facade_lazy_loss_matches_eager(pool, monkeypatch):
+    """vgg11 through the facade with the deferred fwd_bkwd (staged 128-sample calls, one batched
+    forward + backward per chunk of 4, flsim_vgg11_load_rows / fwd_bwd_loaded_rows) against a
+    forward and backward per call: per-call losses and their float32 mean bit for bit (the
+    forward's sums per output do not depend on the row count); the epoch's gradient differs only
+    in the order the calls' partial sums are added (rel-L2 <= 1e-6), theta after the Adam step by
+    at most the ~2 lr a near-zero gradient component can move."""
+    la, ma, ga, ta = _vgg_facade_loop(pool, monkeypatch, lazy=False)
+    lb, mb, gb, tb = _vgg_facade_loop(pool, monkeypatch, lazy=True)
+    assert np.array_equal(la.view(np.uint32), lb.view(np.uint32)), (la, lb)
+    assert ma.dtype == mb.dtype == np.float32 and ma == mb
+    assert float((ga - gb).norm() / ga.norm()) <= 1e-6
+    assert float((ta - tb).abs().max()) <= 2.1e-3

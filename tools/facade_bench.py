@@ -31,9 +31,10 @@ def main():
     ap.add_argument("--delay", type=int, default=50)
     ap.add_argument("--epochs", type=int, default=3)
     ap.add_argument("--batch_size", type=int, default=128)
+    ap.add_argument("--model", default="PerformantNet1", choices=["PerformantNet1", "vgg11"])
     args = ap.parse_args()
     from FL.agents import Agg, Central, Worker, rule
-    from FL.models import PerformantNet1
+    from FL.models import PerformantNet1, vgg11
     from flsim.data import DevicePool
 
     dev = torch.device("cuda", 0)
@@ -42,7 +43,7 @@ def main():
     lut = pool.lut
     npool = int(pool.imgs.shape[0])
     torch.manual_seed(0)
-    model = PerformantNet1().to(dev)
+    model = (vgg11() if args.model == "vgg11" else PerformantNet1()).to(dev)
     central = Central(model, torch.optim.Adam(model.parameters(), lr=0.001))
     workers = [Worker(nn.CrossEntropyLoss()) for _ in range(n)]
     agg = Agg(rule)
@@ -92,7 +93,7 @@ def main():
             timed_s += dt
     print(json.dumps({"metric": "facade worker-steps/s (FL.agents reference loop)",
                       "value": round(timed_ws / timed_s, 2) if timed_s else None,
-                      "unit": "worker-steps/s", "n_workers": n, "delay": d, "batch_size": B,
+                      "unit": "worker-steps/s", "model": args.model, "n_workers": n, "delay": d, "batch_size": B,
                       "timed_epochs": args.epochs - 1, "epochs": per_epoch}), flush=True)
 
 
