@@ -29,8 +29,14 @@ Worker.index is the worker's position in the worker list: workers are numbered i
 from the last Central (main.py:110-113 builds Central, then the workers).
 
 vgg11_bn(): the module's BatchNorm running_mean / running_var alias the engine's device buffer;
-every train-mode fwd_bkwd call advances them (and num_batches_tracked) as nn.BatchNorm2d does;
-batches must be 128 samples (one BatchNorm batch per call).
+every train-mode fwd_bkwd call advances them (and num_batches_tracked) as nn.BatchNorm2d does
+(with staged calls: when the buffers are next read, _LazyBuffer); batches must be 128 samples
+(one BatchNorm batch per call).
+
+Staged calls (PerformantNet1, vgg11, vgg11_bn; 128-sample batches): fwd_bkwd stages the batch and
+returns a _LazyLoss that reads as agents.py:40's 0-d float32 array; the staged calls run as one
+worker-batched pass when a loss, a .grad view or a BatchNorm buffer is read, or the chunk is due
+(FLSIM_FACADE_LAZY_LOSS=0: a call's forward runs at once).
 
 Requirements (raise otherwise): the model is FL.models.PerformantNet1, vgg11() or vgg11_bn() on
 a HIP device, the optimizer is torch.optim.Adam without weight decay / amsgrad / maximize.
@@ -109,6 +115,30 @@ class _LazyGrad(torch.Tensor):
         return repr(self.as_subclass(torch.Tensor))
 
 
+class _LazyBuffer(torch.Tensor):
+    """A vgg11_bn running buffer (running_mean / running_var / num_batches_tracked) of a facade
+    with staged calls: any torch function or method that touches it first runs the staged calls
+    (their BatchNorm statistics fold into the running buffers there), so every read sees what the
+    reference's module holds after each train-mode call (nn.BatchNorm2d)."""
+
+    @classmethod
+    def __torch_function__(cls, func, types, args=(), kwargs=None):
+        kwargs = kwargs or {}
+        if func not in _META:
+            for a in list(args) + list(kwargs.values()):
+                for x in (a if isinstance(a, (list, tuple)) else (a,)):
+                    if isinstance(x, _LazyBuffer):
+                        ctx = x.__dict__.get("_flsim_ctx")
+                        ctx = ctx() if ctx is not None else None
+                        if ctx is not None and ctx.block is not None:
+                            ctx.flush_backward()
+        with torch._C.DisableTorchFunctionSubclass():
+            return func(*args, **kwargs)
+
+    def __repr__(self, *, tensor_contents=None):
+        return repr(self.as_subclass(torch.Tensor))
+
+
 def _lazy_views(flat, shapes, ctx):
     ref = weakref.ref(ctx)
     out = []
@@ -148,8 +178,11 @@ class _ModelContext:
         # backward per call.  The chunk workspace starts at 8 workers and grows between epochs to
         # what an epoch used (so a 4-worker loop holds 1.6 GB, a 1024-worker one 2 x 26 GB).
         cw = int(os.environ.get("FLSIM_FACADE_CHUNK", "128"))
+        lazy = os.environ.get("FLSIM_FACADE_LAZY_LOSS", "1") != "0"
         self.defer_max = 0
-        if self.engine_cls.PREFIX in ("pn1", "vgg11") and cw > 0:
+        # (vgg11_bn defers only with the lazy loss: its calls are always staged, see below)
+        if cw > 0 and (self.engine_cls.PREFIX in ("pn1", "vgg11") or
+                       (self.engine_cls.PREFIX == "vgg11_bn" and lazy)):
             self.defer_max = min(cw, MAX_BATCH // 128) * 128
         self.engine = self.engine_cls(dev, chunk_workers=min(self.defer_max // 128, 8) or 1)
         self.defer_rows = self.engine.max_samples if self.defer_max else 0
@@ -158,8 +191,11 @@ class _ModelContext:
         # staged calls runs as one batched pass (flush_forward; vgg11: forward, loss and backward
         # together, the batched engine's chunk) when a loss is read or the backward is due.
         # FLSIM_FACADE_LAZY_LOSS=0: every call runs its forward now and returns a plain array
-        # (vgg11: its forward and backward, as before).
-        self.lazy_loss = os.environ.get("FLSIM_FACADE_LAZY_LOSS", "1") != "0"
+        # (vgg11: its forward and backward, as before).  vgg11_bn: the staged calls' BatchNorm
+        # statistics fold into the running buffers in call order at the flush; the module's
+        # running_mean / running_var / num_batches_tracked are then _LazyBuffer views that run the
+        # staged calls first whenever they are read.
+        self.lazy_loss = lazy
         self.block = None            # _LossBlock of the staged calls whose forward has not run
         self.epoch_rows = 0          # rows forwarded this epoch
         self.pending = 0             # rows forwarded whose backward is not queued yet
@@ -196,12 +232,25 @@ class _ModelContext:
         bns = [mod for mod in model.modules() if isinstance(mod, torch.nn.BatchNorm2d)]
         views = self.engine.running_views()
         assert len(bns) == len(views)
-        for mod, (_, rm, rv) in zip(bns, views):
-            rm.copy_(mod.running_mean.detach().reshape(-1))
-            rv.copy_(mod.running_var.detach().reshape(-1))
-            mod.running_mean.data = rm
-            mod.running_var.data = rv
         self.engine.num_batches_tracked = int(bns[0].num_batches_tracked)
+        lazy = self.defer_max > 0
+        ref = weakref.ref(self)
+
+        def wrap(t):
+            t = torch.Tensor._make_subclass(_LazyBuffer, t, False)
+            t.__dict__["_flsim_ctx"] = ref
+            return t
+        for mod, (_, rm, rv) in zip(bns, views):
+            with torch._C.DisableTorchFunctionSubclass():
+                rm.copy_(mod.running_mean.detach().reshape(-1))
+                rv.copy_(mod.running_var.detach().reshape(-1))
+            if lazy:
+                mod.running_mean = wrap(rm)
+                mod.running_var = wrap(rv)
+                mod.num_batches_tracked = wrap(mod.num_batches_tracked.detach())
+            else:
+                mod.running_mean.data = rm
+                mod.running_var.data = rv
         self.bns = bns
 
     def ensure_capacity(self, n_samples):
@@ -287,7 +336,19 @@ class _ModelContext:
         n = len(b.indices)
         wt = worker_table([(self.t, i, 0) for i in b.indices], self.device)
         b.dev = torch.empty(n, device=self.device)
-        if hasattr(self.engine, "fwd_bwd_loaded_rows"):
+        if self.bns:
+            # vgg11_bn: forward, loss, backward and each call's BatchNorm statistics in one
+            # chunk, then nn.BatchNorm2d's running updates of the n calls in call order
+            assert b.row0 == 0 and self.pending == n * 128
+            stats = torch.empty(n * self.engine.STATS_PER_WORKER, device=self.device)
+            self.engine.fwd_bwd_loaded_rows(self.theta_run, n * 128, wt, self.seed, b.dropout,
+                                            b.dev, stats)
+            self.pending = 0
+            self.engine.update_running(stats, n)
+            with torch._C.DisableTorchFunctionSubclass():
+                for mod in self.bns:
+                    mod.num_batches_tracked.fill_(self.engine.num_batches_tracked)
+        elif hasattr(self.engine, "fwd_bwd_loaded_rows"):
             # vgg11: forward, loss and backward of the staged rows [0, n * 128) in one chunk
             assert b.row0 == 0 and self.pending == n * 128
             self.engine.fwd_bwd_loaded_rows(self.theta_run, n * 128, wt, self.seed, b.dropout,
@@ -324,7 +385,11 @@ class _ModelContext:
             # the last epoch's calls did not fit one deferred chunk: a larger workspace (the
             # epoch's gradient is consumed, nothing is pending)
             cw = -(-min(self.epoch_rows, self.defer_max) // 128)
+            old = self.engine
             self.engine = self.engine_cls(self.device, chunk_workers=cw)
+            if old.STATS_PER_WORKER:        # the running buffers stay where the module sees them
+                self.engine.running = old.running
+                self.engine.num_batches_tracked = old.num_batches_tracked
             self.defer_rows = self.engine.max_samples
             self.slot = 0
         self.epoch_rows = 0
@@ -570,7 +635,7 @@ class Worker:
         ctx.ensure_capacity(n)
         eng = ctx.engine
         theta = ctx.theta
-        defer = ctx.defer_rows and ctx.bn_stats is None
+        defer = bool(ctx.defer_rows)
         rows_api = defer and eng.PREFIX == "pn1"     # one-call forwards into chunk rows
         if defer:
             theta = ctx.prepare_rows()
@@ -591,7 +656,7 @@ class Worker:
             if not self.model.training or n != 128:
                 raise NotImplementedError("vgg11_bn: the HIP engine runs BatchNorm in train mode "
                                           "on 128-sample batches (main.py:43-44, 132)")
-            kw = {"stats_out": ctx.bn_stats}
+            kw = {} if lazy_call else {"stats_out": ctx.bn_stats}   # staged: at the flush
         x = inp.to(ctx.device, torch.float32)
         lazy = None
         if defer and not lazy_call and not rows_api:
@@ -630,7 +695,7 @@ class Worker:
         else:
             eng.run_input(theta, x, outp.to(ctx.device), wt, ctx.seed, self.model.training, lb,
                           **kw)
-        if ctx.bn_stats is not None:             # nn.BatchNorm2d's running update, this call
+        if ctx.bn_stats is not None and not lazy_call:   # nn.BatchNorm2d's running update
             eng.update_running(ctx.bn_stats, 1)
             for mod in ctx.bns:
                 mod.num_batches_tracked.fill_(eng.num_batches_tracked)

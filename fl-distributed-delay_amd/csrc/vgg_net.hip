@@ -535,13 +535,15 @@ static int vgg_load_rows(void* gradstate, void* workspace, int max_samples, int 
 template <bool BN>
 static int vgg_fwd_bwd_loaded_rows(void* gradstate, void* workspace, int max_samples, int n_rows,
                                    const float* theta, const WorkerRec* workers, uint64_t seed,
-                                   int dropout, float* worker_loss, hipStream_t stream) {
+                                   int dropout, float* worker_loss, float* bn_stats,
+                                   hipStream_t stream) {
     FLSIM_REQUIRE(gradstate && workspace && theta && workers && worker_loss, "null pointer");
+    FLSIM_REQUIRE(!BN || bn_stats, "null bn_stats");
     FLSIM_REQUIRE(n_rows > 0 && n_rows % SAMPLES_PER_WORKER == 0 && n_rows <= max_samples &&
                   n_rows <= 16384, "bad row count %d (workspace %d)", n_rows, max_samples);
     VWS w = vws_layout((char*)workspace, max_samples, BN);
     return vrun_chunk<BN>(gradstate, w, theta, workers, n_rows / SAMPLES_PER_WORKER, seed, dropout,
-                          1, worker_loss, nullptr, stream);
+                          1, worker_loss, bn_stats, stream);
 }
 
 // Evaluation (util.py:31-45 after central.model.eval(), main.py:190: dropout off; vgg11_bn:
@@ -662,7 +664,23 @@ int flsim_vgg11_fwd_bwd_loaded_rows(void* gradstate, void* workspace, int max_sa
                                     const float* theta, const WorkerRec* workers, uint64_t seed,
                                     int dropout, float* worker_loss, hipStream_t stream) {
     return vgg_fwd_bwd_loaded_rows<false>(gradstate, workspace, max_samples, n_rows, theta,
-                                          workers, seed, dropout, worker_loss, stream);
+                                          workers, seed, dropout, worker_loss, nullptr, stream);
+}
+
+int flsim_vgg11_bn_load_rows(void* gradstate, void* workspace, int max_samples, int row0,
+                             const float* x, const int64_t* y, int n_samples, hipStream_t stream) {
+    FLSIM_REQUIRE(n_samples % SAMPLES_PER_WORKER == 0,
+                  "vgg11_bn batch of %d samples: must be a multiple of %d", n_samples,
+                  SAMPLES_PER_WORKER);
+    return vgg_load_rows<true>(gradstate, workspace, max_samples, row0, x, y, n_samples, stream);
+}
+
+int flsim_vgg11_bn_fwd_bwd_loaded_rows(void* gradstate, void* workspace, int max_samples,
+                                       int n_rows, const float* theta, const WorkerRec* workers,
+                                       uint64_t seed, int dropout, float* worker_loss,
+                                       float* bn_stats, hipStream_t stream) {
+    return vgg_fwd_bwd_loaded_rows<true>(gradstate, workspace, max_samples, n_rows, theta,
+                                         workers, seed, dropout, worker_loss, bn_stats, stream);
 }
 
 int flsim_vgg11_eval_pool(void* gradstate, void* workspace, int max_samples, const float* theta,

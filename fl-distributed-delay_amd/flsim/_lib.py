@@ -37,7 +37,8 @@ EXPORTS = [
     "flsim_pn1_fwd_bwd_chunk_async", "flsim_pn1_fwd_bwd_input_async",
     "flsim_aggregate_adam_rule_push", "flsim_pn1_fwd_rows", "flsim_pn1_bwd_rows",
     "flsim_pn1_load_rows", "flsim_pn1_fwd_loaded_rows", "flsim_vgg11_load_rows",
-    "flsim_vgg11_fwd_bwd_loaded_rows",
+    "flsim_vgg11_fwd_bwd_loaded_rows", "flsim_vgg11_bn_load_rows",
+    "flsim_vgg11_bn_fwd_bwd_loaded_rows",
     "flsim_comm_unique_id", "flsim_comm_create", "flsim_comm_size", "flsim_comm_rank",
     "flsim_allreduce_sum", "flsim_comm_destroy",
 ]
@@ -123,6 +124,9 @@ def lib():
     L.flsim_vgg11_load_rows.argtypes = L.flsim_pn1_load_rows.argtypes
     L.flsim_vgg11_fwd_bwd_loaded_rows.argtypes = [
         vp, vp, ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_uint64, ctypes.c_int, vp, vp]
+    L.flsim_vgg11_bn_load_rows.argtypes = L.flsim_pn1_load_rows.argtypes
+    L.flsim_vgg11_bn_fwd_bwd_loaded_rows.argtypes = [
+        vp, vp, ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_uint64, ctypes.c_int, vp, vp, vp]
     L.flsim_pn1_fwd_loaded_rows.argtypes = [
         vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_uint64, ctypes.c_int,
         vp, vp]

@@ -379,6 +379,19 @@ class VGG11BNEngine(NetEngine):
                                   for _, c in VGG11_BN_BUFFERS]).to(self.device)
         self.num_batches_tracked = 0
 
+    def _slot_workspace(self, slot):
+        return self.workspace                 # one workspace: the vgg11_bn facade has no pipeline
+
+    def fwd_bwd_loaded_rows(self, theta, n_rows, workers_dev, seed, dropout, loss_out,
+                            stats_out):
+        """The facade's deferred fwd_bkwd: forward, loss and backward of the staged rows
+        [0, n_rows) as one batched chunk; stats_out[g] = call g's BatchNorm statistics (for
+        update_running), loss_out[g] = its loss."""
+        check(lib().flsim_vgg11_bn_fwd_bwd_loaded_rows(
+            ptr(self.gradstate), ptr(self.workspace), self.max_samples, int(n_rows), ptr(theta),
+            ptr(workers_dev), ctypes.c_uint64(seed), int(bool(dropout)), ptr(loss_out),
+            ptr(stats_out), stream_ptr()))
+
     def update_running(self, stats, n_workers):
         n = int(n_workers)
         if n:

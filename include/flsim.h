@@ -213,6 +213,16 @@ int flsim_vgg11_load_rows(void* gradstate, void* workspace, int max_samples, int
 int flsim_vgg11_fwd_bwd_loaded_rows(void* gradstate, void* workspace, int max_samples, int n_rows,
                                     const float* theta, const WorkerRec* workers, uint64_t seed,
                                     int dropout, float* worker_loss, flsim_stream_t stream);
+/* vgg11_bn: the same two calls; each staged 128-row call is one BatchNorm batch, and bn_stats
+ * [n_rows / 128][flsim_vgg11_bn_stats_per_worker()] receives the calls' statistics for
+ * flsim_vgg11_bn_update_running (in call order, as nn.BatchNorm2d's per-call updates). */
+int flsim_vgg11_bn_load_rows(void* gradstate, void* workspace, int max_samples, int row0,
+                             const float* x, const int64_t* y, int n_samples,
+                             flsim_stream_t stream);
+int flsim_vgg11_bn_fwd_bwd_loaded_rows(void* gradstate, void* workspace, int max_samples,
+                                       int n_rows, const float* theta, const WorkerRec* workers,
+                                       uint64_t seed, int dropout, float* worker_loss,
+                                       float* bn_stats, flsim_stream_t stream);
 int flsim_vgg11_end_epoch(void* gradstate, float* grad_out, flsim_stream_t stream);
 int flsim_vgg11_eval_input(void* gradstate, void* workspace, int max_samples, const float* theta,
                            const float* x, int n_images, int32_t* pred, flsim_stream_t stream);

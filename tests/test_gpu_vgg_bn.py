@@ -319,3 +319,60 @@ def test_vgg_bn_reference_api_facade(pool):
     run = torch.cat([torch.cat([mod.running_mean, mod.running_var]) for mod in model.modules()
                      if isinstance(mod, nn.BatchNorm2d)]).double().cpu().numpy()
     np.testing.assert_allclose(run, osim.bn.flat(), rtol=1e-5, atol=1e-6)
+
+
+def _bn_facade_loop(pool, monkeypatch, lazy, n=6):
+    """One epoch of the reference worker loop through FL.agents with vgg11_bn: chunks of 4 staged
+    calls, the running buffers read after call 3 (mid-chunk) and at the epoch's end."""
+    import torch.nn as nn
+    from FL.agents import Agg, Central, Worker, rule
+    from FL.models import vgg11_bn
+    from oracle import oracle as O
+    monkeypatch.setenv("FLSIM_FACADE_CHUNK", "4")
+    monkeypatch.setenv("FLSIM_FACADE_LAZY_LOSS", "1" if lazy else "0")
+    torch.manual_seed(0)
+    model = vgg11_bn().to(DEV)
+    central = Central(model, torch.optim.Adam(model.parameters(), lr=0.001))
+    workers = [Worker(nn.CrossEntropyLoss()) for _ in range(n)]
+    rs = np.random.RandomState(11)
+    lut = O.normalize_lut()
+    model.train()
+    ups, losses, mids = [], [], None
+    bn = [m for m in model.modules() if isinstance(m, torch.nn.BatchNorm2d)]
+    for i in range(n):
+        idx = rs.randint(0, pool[0].shape[0], 128)
+        workers[i].model = central.model
+        g, lv = workers[i].fwd_bkwd(torch.from_numpy(lut[pool[0][idx]]).to(DEV),
+                                    torch.from_numpy(pool[1][idx]).to(DEV))
+        ups.append(g)
+        losses.append(lv)
+        if i == 2:
+            mids = (torch.cat([bn[0].running_mean.cpu(), bn[-1].running_var.cpu()]),
+                    int(bn[3].num_batches_tracked))
+    grad = torch.cat([t.reshape(-1) for t in ups[0]]).double().cpu()
+    central.update_model(Agg(rule).rule(ups))
+    mean = np.mean(losses)
+    sd = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()
+          if "running" in k or "num_batches" in k}
+    return np.asarray([float(v) for v in losses], np.float32), mean, grad, sd, mids
+
+
+def test_vgg_bn_facade_lazy_matches_per_call(pool, monkeypatch):
+    """vgg11_bn through the facade with staged calls (one batched forward + backward per chunk of
+    4, each call its own BatchNorm batch, the running updates folded in call order at the flush;
+    the module's buffers are lazy views that run the staged calls when read) against a forward and
+    backward per call: losses, running buffers read mid-chunk and after the epoch, and
+    num_batches_tracked agree, the gradient within the order of the calls' partial sums."""
+    la, ma, ga, sa, mida = _bn_facade_loop(pool, monkeypatch, lazy=False)
+    lb, mb, gb, sb, midb = _bn_facade_loop(pool, monkeypatch, lazy=True)
+    np.testing.assert_allclose(lb, la, rtol=2e-6)
+    assert mb.dtype == np.float32 and abs(float(mb) - float(ma)) <= 2e-6 * abs(float(ma))
+    assert midb[1] == mida[1] == 3
+    torch.testing.assert_close(midb[0], mida[0], rtol=2e-6, atol=1e-7)
+    assert sa.keys() == sb.keys()
+    for k in sa:
+        if "num_batches" in k:
+            assert int(sa[k]) == int(sb[k]) == 6, k
+        else:
+            torch.testing.assert_close(sb[k], sa[k], rtol=2e-6, atol=1e-7)
+    assert float((ga - gb).norm() / ga.norm()) <= 1e-5

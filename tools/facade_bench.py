@@ -31,10 +31,10 @@ def main():
     ap.add_argument("--delay", type=int, default=50)
     ap.add_argument("--epochs", type=int, default=3)
     ap.add_argument("--batch_size", type=int, default=128)
-    ap.add_argument("--model", default="PerformantNet1", choices=["PerformantNet1", "vgg11"])
+    ap.add_argument("--model", default="PerformantNet1", choices=["PerformantNet1", "vgg11", "vgg11_bn"])
     args = ap.parse_args()
     from FL.agents import Agg, Central, Worker, rule
-    from FL.models import PerformantNet1, vgg11
+    from FL.models import PerformantNet1, vgg11, vgg11_bn
     from flsim.data import DevicePool
 
     dev = torch.device("cuda", 0)
@@ -43,7 +43,7 @@ def main():
     lut = pool.lut
     npool = int(pool.imgs.shape[0])
     torch.manual_seed(0)
-    model = (vgg11() if args.model == "vgg11" else PerformantNet1()).to(dev)
+    model = {"vgg11": vgg11, "vgg11_bn": vgg11_bn}.get(args.model, PerformantNet1)().to(dev)
     central = Central(model, torch.optim.Adam(model.parameters(), lr=0.001))
     workers = [Worker(nn.CrossEntropyLoss()) for _ in range(n)]
     agg = Agg(rule)

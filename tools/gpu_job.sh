@@ -23,7 +23,7 @@
 #   aggceil           tools/agg_ceiling.py (torch streams at the aggregation paths' sizes)
 #   facadeab:<VAR=VAL> the facade loop with one environment setting, E A E A
 #   facade            tools/facade_bench.py (the FL.agents reference loop, n = 1024)
-#   vfacadeab:<VAR=VAL> the same loop with vgg11, one environment setting, E A E A
+#   vfacadeab:<VAR=VAL> the same loop with vgg11, one environment setting, E A E A (bfacadeab: vgg11_bn)
 #   configs           tools/gpu_configs_all.sh (the other BASELINE configs)
 #   lab:<bin>[:<arg>] a lab binary from tools/lab (built beforehand on the CPU)
 #   labab:<b0>:<b1>:<arg>  two lab binaries A B A B on the same box
@@ -196,14 +196,15 @@ for STEP in "$@"; do
         D=$(dirname $(find $OUT/c1trace -name "run_kernel_trace.csv" | head -1))
         cp $D/run_kernel_stats.csv $OUT/c1_kernel_stats.csv
         python3 tools/trace_gaps.py $D 0.5 > $OUT/c1_gaps.txt && head -30 $OUT/c1_gaps.txt ;;
-    vfacadeab:*)     # the vgg11 facade loop (n = 1024) with one environment setting, E A E A
-        KV=${STEP#vfacadeab:}
+    vfacadeab:*|bfacadeab:*)   # the vgg11 / vgg11_bn facade loop (n = 1024), one setting, E A E A
+        KV=${STEP#?facadeab:}
+        FM=vgg11; [ ${STEP:0:1} = b ] && FM=vgg11_bn
         for R in E1 A1 E2 A2; do
             if [ ${R:0:1} = E ]; then ENVS="$KV"; else ENVS="FLSIM_NOOP=1"; fi
-            env $ENVS timeout -k 10 300 python3 -u tools/facade_bench.py --model vgg11 --epochs 4 \
-                > $OUT/vfacade_$R.json 2> $OUT/vfacade_$R.err \
-                || { echo "vgg facade $R failed $?"; tail -5 $OUT/vfacade_$R.err; exit 1; }
-            echo "$R $(cut -c1-120 $OUT/vfacade_$R.json)"
+            env $ENVS timeout -k 10 300 python3 -u tools/facade_bench.py --model $FM --epochs 4 \
+                > $OUT/${FM}_facade_$R.json 2> $OUT/${FM}_facade_$R.err \
+                || { echo "$FM facade $R failed $?"; tail -5 $OUT/${FM}_facade_$R.err; exit 1; }
+            echo "$R $(cut -c1-130 $OUT/${FM}_facade_$R.json)"
         done ;;
     facadeab:*)
         KV=${STEP#facadeab:}
