@@ -132,6 +132,14 @@ struct HasPre : std::false_type {};
 template <class E>
 struct HasPre<E, std::void_t<decltype(E::PRE)>> : std::bool_constant<E::PRE> {};
 
+// One-wave blocks (PerformantNet1's conv2 weight gradient, 48 x 48) keep a single LDS buffer: their
+// barriers are wave-local, so the store -> barrier -> read order costs little, and half the LDS
+// (13.4 -> 6.7 KB) lifts them from 3 to 5 waves per SIMD: conv2's weight gradient 7.37 -> 6.85 ms,
+// the same arithmetic (A B A B, profiles/r06/ab_single_buf).  Lab override -DFLSIM_SINGLE_BUF=0.
+#ifndef FLSIM_SINGLE_BUF
+#define FLSIM_SINGLE_BUF 1
+#endif
+
 template <int FM, int FN, int WAVES_M, int WAVES_N, class AL, class BL, class EPI>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N)
 gemm_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, int tiles_m,
@@ -148,7 +156,8 @@ gemm_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, int t
     // the staged tile goes out in passes of WM_PASS wave-rows (16 FM rows each) that fit the
     // pipeline's own LDS footprint or 32 KB, whichever is larger (conv1: one pass in 26.6 KB,
     // 1.23 vs 1.33 ms for two; conv2 data-grad: two passes in the pipeline's 38 KB)
-    constexpr int BASE_FL = 2 * (A_FL + B_FL);
+    constexpr bool SB = FLSIM_SINGLE_BUF && WAVES_M * WAVES_N == 1 && !STAGED;
+    constexpr int BASE_FL = (SB ? 1 : 2) * (A_FL + B_FL);
     constexpr int STAGE_BUDGET = BASE_FL > 8192 ? BASE_FL : 8192;
     constexpr int WROWS = 16 * FM;
     constexpr int WM_FIT = STAGE_BUDGET / (WROWS * STAGE_LD);
@@ -200,11 +209,13 @@ gemm_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, int t
     if (ks0 < ks1) {
         al.load(ks0, ra);
         bl.load(ks0, rb);
-        al.store(lds, ra);
-        bl.store(lds + A_FL, rb);
-        if (ks0 + 1 < ks1) {
-            al.load(ks0 + 1, ra);
-            bl.load(ks0 + 1, rb);
+        if constexpr (!SB) {
+            al.store(lds, ra);
+            bl.store(lds + A_FL, rb);
+            if (ks0 + 1 < ks1) {
+                al.load(ks0 + 1, ra);
+                bl.load(ks0 + 1, rb);
+            }
         }
     }
     __syncthreads();
@@ -219,7 +230,15 @@ gemm_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, int t
     // for the split forwards, made conv3's data gradient 3 % slower here and left VGG-11's fp32
     // data gradients unchanged, profiles/r05/ab/core_interleave.txt: removed)
     for (int ks = ks0; ks < ks1; ++ks) {
-        if (ks + 1 < ks1) {
+        if constexpr (SB) {
+            al.store(lds, ra);
+            bl.store(lds + A_FL, rb);
+            if (ks + 1 < ks1) {
+                al.load(ks + 1, ra);
+                bl.load(ks + 1, rb);
+            }
+            __syncthreads();
+        } else if (ks + 1 < ks1) {
             al.store(lds + (cur ^ 1) * BUF, ra);
             bl.store(lds + (cur ^ 1) * BUF + A_FL, rb);
             if (ks + 2 < ks1) {
@@ -227,7 +246,7 @@ gemm_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, int t
                 bl.load(ks + 2, rb);
             }
         }
-        const float* A = lds + cur * BUF;
+        const float* A = lds + (SB ? 0 : cur * BUF);
         const float* B = A + A_FL;
         if constexpr (EPI::ASUM) {
             // bias gradient fused into the weight gradient: column sums of the KM dZ tile
