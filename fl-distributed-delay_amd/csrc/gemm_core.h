@@ -132,12 +132,14 @@ struct HasPre : std::false_type {};
 template <class E>
 struct HasPre<E, std::void_t<decltype(E::PRE)>> : std::bool_constant<E::PRE> {};
 
-// One-wave blocks (PerformantNet1's conv2 weight gradient, 48 x 48) keep a single LDS buffer: their
-// barriers are wave-local, so the store -> barrier -> read order costs little, and half the LDS
-// (13.4 -> 6.7 KB) lifts them from 3 to 5 waves per SIMD: conv2's weight gradient 7.37 -> 6.85 ms,
-// the same arithmetic (A B A B, profiles/r06/ab_single_buf).  Lab override -DFLSIM_SINGLE_BUF=0.
+// Blocks of one or two waves keep a single LDS buffer: their barriers span at most two waves, so
+// the store -> barrier -> read order costs little, and half the LDS lifts the LDS-bound ones
+// (PerformantNet1's conv2 / conv3 weight gradients, 48 x 48 of 1 wave, 96 x 48 of 2) from 3 to 5 and
+// 4 to 5 waves per SIMD: conv2 7.37 -> 6.85 ms, conv3 4.43 -> 4.25 ms, the same arithmetic (A B A B,
+// profiles/r06/ab_single_buf; vgg11 unchanged, 1238.6-1242.2 against 1240.6-1242.8).
+// FLSIM_SINGLE_BUF = the largest block (waves) that runs single-buffered; lab override 0 / 1.
 #ifndef FLSIM_SINGLE_BUF
-#define FLSIM_SINGLE_BUF 1
+#define FLSIM_SINGLE_BUF 2
 #endif
 
 template <int FM, int FN, int WAVES_M, int WAVES_N, class AL, class BL, class EPI>
@@ -156,7 +158,7 @@ gemm_kernel(AL al, BL bl, EPI epi, int ksteps_total, int ksteps_per_split, int t
     // the staged tile goes out in passes of WM_PASS wave-rows (16 FM rows each) that fit the
     // pipeline's own LDS footprint or 32 KB, whichever is larger (conv1: one pass in 26.6 KB,
     // 1.23 vs 1.33 ms for two; conv2 data-grad: two passes in the pipeline's 38 KB)
-    constexpr bool SB = FLSIM_SINGLE_BUF && WAVES_M * WAVES_N == 1 && !STAGED;
+    constexpr bool SB = WAVES_M * WAVES_N <= FLSIM_SINGLE_BUF && !STAGED;
     constexpr int BASE_FL = (SB ? 1 : 2) * (A_FL + B_FL);
     constexpr int STAGE_BUDGET = BASE_FL > 8192 ? BASE_FL : 8192;
     constexpr int WROWS = 16 * FM;
