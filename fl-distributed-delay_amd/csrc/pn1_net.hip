@@ -698,7 +698,12 @@ static int backward(const GradState& g, const WS& w, const float* theta, int S, 
         dz3, w.d1f, S, 96, 432, g.sw[2], g.sb[2], GEO[2].ZW, sw, K_WG3, 432, zi(2), &zu[2])));
 #endif
     // (gemm_kernel: the direct-A form measured 3.87 vs 3.78 ms with this staged epilogue, r03b)
-    RC((conv_like_sz<20, 20, 96, 0, 4, 2, 3, 4, 1>(dz3, S, g.wd[2], 48, 864,
+    // (128 x 48 tiles on large chunks too, FM 2 against 4: 3.68-3.69 against 3.79 ms, the same
+    // sums per output, A B A B, profiles/r06/ab_dg3_fm; lab override -DFLSIM_DG3_FM)
+#ifndef FLSIM_DG3_FM
+#define FLSIM_DG3_FM 2
+#endif
+    RC((conv_like_sz<20, 20, 96, 0, FLSIM_DG3_FM, 2, 3, 4, 1>(dz3, S, g.wd[2], 48, 864,
         EpiDropScatterXs<18, 18, 48, false, true>{w.a2, nullptr, w.d1, w.i1, s25, S * 18 * 18}, st,
         K_DG3, 864)));
     if (debug_stop() == 3) return finish();       // (debug: dz2 in a2, dz3 in gx)
