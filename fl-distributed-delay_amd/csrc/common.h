@@ -16,7 +16,7 @@
     (defined(FLSIM_X6_FRESH) || defined(FLSIM_X6_PP_V) || defined(FLSIM_DG_FMS) ||          \
      defined(FLSIM_DIRECT_FENCES) || defined(FLSIM_DX6_FENCES) || defined(FLSIM_BUFLOAD) ||  \
      defined(FLSIM_SEQ_EARLY_EXIT) || defined(FLSIM_X6_FLUSH) || defined(FLSIM_WGRAD_X6) ||     \
-     defined(FLSIM_ZL1F) || defined(FLSIM_SINGLE_BUF) || defined(FLSIM_DG3_FM))
+     defined(FLSIM_ZL1F) || defined(FLSIM_SINGLE_BUF) || defined(FLSIM_DG3_FM) || defined(FLSIM_DX_FM))
 #error "FLSIM_* measurement overrides need a lab build (make LAB=1)"
 #endif
 

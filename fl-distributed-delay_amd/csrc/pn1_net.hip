@@ -329,19 +329,26 @@ static int conv1_fwd(const float* x0, const float* W, const float* bias, XsT a1,
 // at most small_chunk_samples() samples take half-height blocks: the same arithmetic per output
 // (bit-identical), twice the blocks.  conv2 (N = 48) runs 64-row waves, 4 per block: 6.67 against
 // 7.24 ms for 32-row waves, 8 per block (profiles/r04/r04j/lab_fwd2.txt, "fwd2v e")
-constexpr int DX_FM = 2, DX_KB = 3, DX_DEPTH = 2, DX_NPL = 2;
+// conv3 / conv4 forwards: 64-row waves (FM 4, 512-row blocks) on large chunks, 16-row waves on
+// small ones.  FM 4 against round 5's 2: conv4's forward 5.96-5.98 -> 5.72-5.76 ms, the headline
+// 1092.4 / 1093.0 -> 1104.8 / 1106.0 worker-steps/s (A B A B, profiles/r06/ab_dx_fm), the same sums
+// per output (lab override -DFLSIM_DX_FM)
+#ifndef FLSIM_DX_FM
+#define FLSIM_DX_FM 4
+#endif
+constexpr int DX_FM = FLSIM_DX_FM, DX_FMS = 1, DX_KB = 3, DX_DEPTH = 2, DX_NPL = 2;
 
 // (One-call passes, the facade's 128-sample forwards, on quarter-height 64-row blocks: bit-identical
 // and 8 % slower on the facade loop, 748 / 746 against 814 / 804 worker-steps/s, E A E A on one box,
 // profiles/r06/facade/facade_tiny_ab: more blocks each staging the same B panel.  Not kept.)
 
 template <int IH, int IW, int CI, int PAD, int FN, bool WIN, int OHX, int FM = DX_FM,
-          int WAVES = 8, class EPI>
+          int WAVES = 8, int FMS = (FM == DX_FM ? DX_FMS : FM / 2), class EPI>
 static int dx6(XsT X, int S, XsT W, int N, int KP, const EPI& epi, hipStream_t st, int kid,
                int kreal) {
     // the inputs of conv2-4 (a1, d1, a3) are channel-slice-major (XsSrcSM)
     if (S <= small_chunk_samples())
-        return conv_dx6<IH, IW, CI, PAD, FM / 2, FN, WAVES, DX_KB, DX_DEPTH, DX_NPL, WIN, OHX,
+        return conv_dx6<IH, IW, CI, PAD, FMS, FN, WAVES, DX_KB, DX_DEPTH, DX_NPL, WIN, OHX,
                         XsSrcSM>(X, S, W, N, KP, epi, st, kid, kreal);
     return conv_dx6<IH, IW, CI, PAD, FM, FN, WAVES, DX_KB, DX_DEPTH, DX_NPL, WIN, OHX, XsSrcSM>(
         X, S, W, N, KP, epi, st, kid, kreal);
@@ -369,7 +376,7 @@ static int forward(const GradState& g, const WS& w, const float* theta, int S,
     // conv1 + ReLU (models.py:29), a1 written split
     RC(conv1_fwd(w.x0, theta + P_OFF[0], theta + P_OFF[1], a1, w.a1f, S, st));
     // conv2 + ReLU + pool1 + dropout1 (models.py:30-32), one fused launch -> d1 (split)
-    RC((dx6<34, 34, 48, 2, 3, true, 0, 4, 4>(a1, S, g.wfx[1], 48, 432,
+    RC((dx6<34, 34, 48, 2, 3, true, 0, 4, 4, 2>(a1, S, g.wfx[1], 48, 432,
         EpiPoolDropXs<18, 18, 48, true>{d1.hm, d1.l, w.i1, theta + P_OFF[3], workers, seed, SITE_DROP1,
                                   THR_P25, SCALE_P25, dropout, S * 18 * 18 * 4, w.d1f}, st,
         K_FWD2, 432)));
